@@ -1,0 +1,194 @@
+/*
+ * lira_hip.h -- C-ABI of liblira_hip.so, the MI355X (gfx950) implementation of
+ * LIRA's query-time hot path: partition ranking, candidate scan and exact
+ * top-k over the probed partitions.
+ *
+ * Every entry point is extern "C", takes plain pointers and sizes (no torch or
+ * HIP C++ types) and returns an int status: LIRA_OK (0) or a negative
+ * LIRA_E* code; lira_last_error() returns a thread-local message for the last
+ * failure.  No C++ exception crosses this boundary.
+ *
+ * Pointers documented as "device" are HBM pointers (e.g. torch tensors'
+ * data_ptr()); "host" pointers are ordinary CPU memory.  `stream` is a
+ * hipStream_t passed as void* (NULL = the null stream).  Compute entry points
+ * are stream-ordered and asynchronous unless stated otherwise.
+ *
+ * What each entry point replaces in the reference (qfshen23/LIRA-ANN-search,
+ * file:line) is stated above it.  INTEGRATION.md shows the ctypes binding the
+ * reference's Python side would use, and lira_amd/_lib.py is that binding.
+ */
+#ifndef LIRA_HIP_H
+#define LIRA_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LIRA_ABI_VERSION 1
+
+/* status codes */
+#define LIRA_OK 0
+#define LIRA_EINVAL (-1)     /* bad argument (shape, k, metric, null pointer) */
+#define LIRA_ERANGE (-2)     /* bucket / probe id out of range */
+#define LIRA_ENOMEM (-3)     /* device allocation failed */
+#define LIRA_EHIP (-4)       /* HIP runtime error (message has the HIP string) */
+#define LIRA_ESTATE (-5)     /* call not valid in the handle's current state */
+#define LIRA_EUNSUPPORTED (-6) /* shape outside what the kernels implement */
+
+/* metrics: search.cpp:362-364 / LIRA_smallscale.py:62-66 */
+#define LIRA_METRIC_L2 0 /* squared L2, ascending  (search.cpp:253-260, faiss IndexFlatL2) */
+#define LIRA_METRIC_IP 1 /* inner product, descending (search.cpp:263-269, faiss IndexFlatIP) */
+
+/* lira_scan_topk flags */
+#define LIRA_SCAN_DEDUP 1u         /* keep each gid once (search.cpp:496-514 does not: Appendix A) */
+#define LIRA_SCAN_PER_PARTITION 2u /* k best of every probed slot on its own (LIRA_smallscale.py:145-174) */
+
+/* lira_select_probes modes */
+#define LIRA_PROBE_NEAREST 0      /* nprobe smallest values, ties -> smaller bucket (IVF nprobe) */
+#define LIRA_PROBE_THRESHOLD_GE 1 /* score >= thr, argmax fallback (search.cpp:447-466) */
+#define LIRA_PROBE_THRESHOLD_GT 2 /* score >  thr, no fallback (LIRA_smallscale.py:206) */
+
+typedef struct lira_index lira_index; /* opaque; one handle per device */
+
+/* ---------------------------------------------------------------- misc */
+int lira_abi_version(void);
+const char *lira_last_error(void);
+/* number of compute units of `device` (for launch sizing in callers/tests) */
+int lira_device_cu_count(int device, int *out);
+
+/* -------------------------------------------------------------- handle */
+/*
+ * Create an empty partitioned index for d-dimensional fp32 vectors.
+ * Replaces faiss.IndexFlatL2(d) / IndexFlatIP(d) construction
+ * (utils.py:415-418) and search.cpp's `std::vector<Bucket> buckets`
+ * (search.cpp:273-276, 387-388).
+ */
+int lira_index_create(int device, int64_t d, int metric, lira_index **out);
+int lira_index_destroy(lira_index *idx);
+
+/*
+ * Load the inverted lists.  Replaces search.cpp:387-403 (per-bucket contiguous
+ * copy of x_d rows) and faiss `index.add(x_d[ids])` per bucket
+ * (utils.py:413-420).
+ *   n_lists           number of buckets B
+ *   list_offsets      host, n_lists+1 int64: bucket b owns list_ids[off[b]:off[b+1]]
+ *   list_ids          device int32, global row ids (sorted unique per bucket for
+ *                     search.cpp parity; any order is accepted)
+ *   x                 device fp32 (n_rows, d) row-major base vectors (x_d)
+ * The module gathers x[list_ids] into its own HBM layout (64-row, d-major tiles),
+ * so x may be freed afterwards.  max_replicas = the largest number of buckets
+ * any one row sits in (data_2_bkt's effective n_mul; 1 without redundancy);
+ * it sizes the dedup merge.  Synchronous w.r.t. the host on return.
+ */
+int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *list_offsets,
+                              const int32_t *list_ids, const float *x, int64_t n_rows,
+                              int32_t max_replicas, void *stream);
+
+/* sizes: ntotal = total rows incl. replicas (faiss .ntotal, LIRA_smallscale.py:171) */
+int lira_index_info(const lira_index *idx, int64_t *d, int *metric, int64_t *n_lists,
+                    int64_t *ntotal, int64_t *max_list);
+/* host copy of one bucket's size (search.cpp:476 `sz`) */
+int lira_index_list_size(const lira_index *idx, int64_t list_no, int64_t *out);
+/* bytes of HBM the index holds */
+int lira_index_memory(const lira_index *idx, int64_t *bytes);
+
+/* ----------------------------------------------------------- ranking */
+/*
+ * Query -> centroid Euclidean distances, exact fp32 in search.cpp's order:
+ * out[q, b] = sqrt(sum_j (q_j - c_bj)^2), summed sequentially without FMA
+ * (search.cpp:220-235); when scaler_mean/scaler_scale are non-NULL the result
+ * is standardised in place: (d - mean_b) / (scale_b == 0 ? 1 : scale_b)
+ * (search.cpp:238-250).  Replaces get_dist_cid (utils.py:98-118, scipy cdist)
+ * for the query side.  q (nq,d), centroids (B,d), out (nq,B): device.
+ */
+int lira_centroid_dist(const float *q, int64_t nq, const float *centroids, int64_t n_centroids,
+                       int64_t d, const float *scaler_mean, const float *scaler_scale,
+                       float *out, void *stream);
+
+/*
+ * MFMA ranking GEMM (v_mfma_f32_32x32x2_f32): approximate squared distances
+ * ||q||^2 + ||c||^2 - 2 q.c for every (q, b), out_sq (nq, B) device, plus a
+ * per-query absolute error bound out_err (nq) such that
+ * |out_sq - exact_sq| <= out_err for every b.  Feeds
+ * lira_rank_nearest, which re-checks the nprobe boundary exactly.
+ */
+int lira_centroid_gemm(const float *q, int64_t nq, const float *centroids, int64_t n_centroids,
+                       int64_t d, float *out_sq, float *out_err, void *stream);
+
+/*
+ * Fused IVF ranking: MFMA GEMM + exact boundary re-check.  Writes the nprobe
+ * nearest centroids of every query, ordered by the exact search.cpp distance
+ * sqrt(l2) ascending, ties -> smaller bucket id; identical to
+ * lira_centroid_dist followed by lira_select_probes(NEAREST).  workspace:
+ * device, at least lira_rank_workspace_size() bytes, or NULL to use the
+ * handle-free internal path (allocates; not graph-capturable).
+ */
+int lira_rank_workspace_size(int64_t nq, int64_t n_centroids, size_t *bytes);
+int lira_rank_nearest(const float *q, int64_t nq, const float *centroids, int64_t n_centroids,
+                      int64_t d, int64_t nprobe, int32_t *out_probe, void *workspace,
+                      size_t workspace_bytes, void *stream);
+
+/*
+ * Probe selection from an (n, B) score/distance matrix (device) into
+ * out_probe (n, max_probe) int32 padded with -1, and out_nprobe (n) (nullable).
+ *  NEAREST:       the max_probe smallest scores (ties -> smaller b), ascending.
+ *  THRESHOLD_GE:  buckets with score >= thr in ascending b, argmax fallback
+ *                 when none (first max wins) -- search.cpp:447-466.
+ *  THRESHOLD_GT:  score > thr, no fallback -- LIRA_smallscale.py:206.
+ * Threshold modes truncate at max_probe (pass max_probe = B for no truncation).
+ */
+int lira_select_probes(const float *scores, int64_t n, int64_t n_centroids, int mode, float thr,
+                       int64_t max_probe, int32_t *out_probe, int32_t *out_nprobe, void *stream);
+
+/* -------------------------------------------------------------- scan */
+/*
+ * Batched candidate scan + exact top-k over the probed buckets.
+ * Replaces search.cpp:468-514 (the per-query scan loop and nth_element top-k)
+ * and the per-(query, bucket) faiss IndexFlat*.search calls of
+ * get_cmp_recall (LIRA_smallscale.py:158-172).
+ *   q          device fp32 (nq, d)
+ *   probe      device int32 (nq, nprobe_max), -1 = unused slot
+ *   k          1..256
+ *   flags      LIRA_SCAN_DEDUP | LIRA_SCAN_PER_PARTITION
+ *   out_D      device fp32  (nq, k)  or (nq, nprobe_max, k) with PER_PARTITION
+ *   out_I      device int64 (nq, k)  or (nq, nprobe_max, k) with PER_PARTITION
+ *   out_ncand  device int64 (nq) or NULL: search.cpp's cmp_for_query
+ *              (candidates scanned, replicas included, search.cpp:468-477)
+ * Distances are bit-identical to search.cpp's sequential fp32 l2_sq / ip.
+ * Order: faiss convention -- L2 ascending squared distance, IP descending
+ * inner product; ties -> smaller gid; pads (+inf, -1) for L2, (-inf, -1) IP.
+ * workspace: device, >= lira_scan_workspace_size() bytes, or NULL to use a
+ * buffer cached in the handle (grown on demand; not graph-capturable).
+ */
+int lira_scan_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe_max, int64_t k,
+                             unsigned flags, size_t *bytes);
+int lira_scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
+                   int64_t nprobe_max, int64_t k, unsigned flags, float *out_D, int64_t *out_I,
+                   int64_t *out_ncand, void *workspace, size_t workspace_bytes, void *stream);
+
+/*
+ * Kernel timing for benchmarks.  While enabled, every lira_scan_topk records
+ * HIP events on the caller's stream around its planning kernels, the k_scan
+ * launch and the k_merge launch.  lira_index_profile_read synchronises on the
+ * last recorded event, returns the summed milliseconds and the number of calls
+ * since the previous read (or enable), and resets the sums.
+ */
+int lira_index_set_profiling(lira_index *idx, int enable);
+int lira_index_profile_read(lira_index *idx, double *plan_ms, double *scan_ms, double *merge_ms,
+                            int64_t *calls);
+
+/*
+ * Device-side error word of the last scan/select on this handle (e.g. a probe
+ * id >= n_lists, skipped): synchronises `stream`, returns LIRA_OK or LIRA_ERANGE
+ * and clears the word.
+ */
+int lira_index_check(lira_index *idx, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LIRA_HIP_H */

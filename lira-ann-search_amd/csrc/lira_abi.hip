@@ -1,0 +1,341 @@
+// lira_abi.hip -- the extern "C" boundary of liblira_hip.so (include/lira_hip.h)
+// and the partitioned-index object: gathering x_d rows into the HBM tile layout
+// (replaces search.cpp:387-403 and faiss index.add per bucket, utils.py:413-420).
+#include <algorithm>
+#include <new>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "lira_device.hpp"
+#include "lira_internal.hpp"
+
+namespace lira {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string &msg) { g_last_error = msg; }
+
+int fail(int code, const std::string &msg) {
+    g_last_error = msg;
+    return code;
+}
+
+int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+// scan entry points (lira_scan.hip)
+int scan_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, size_t *bytes);
+int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe, int64_t nprobe,
+              int64_t k, unsigned flags, float *out_D, int64_t *out_I, int64_t *out_ncand,
+              void *ws, size_t ws_bytes, hipStream_t st);
+
+// Gather x[list_ids] into [tile][dpad][64]; one workgroup per tile, lane = row.
+__global__ __launch_bounds__(256) void k_tile_gather(const float *x, int64_t d, int64_t dpad,
+                                                     const int32_t *list_ids,
+                                                     const int64_t *list_off,
+                                                     const int32_t *tile_off,
+                                                     const int32_t *tile_list, int64_t n_tiles,
+                                                     float *X, int32_t *ids) {
+    const int l = threadIdx.x & 63, jg = threadIdx.x >> 6;
+    for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        const int b = tile_list[t];
+        const int64_t r = (t - tile_off[b]) * kTile + l;
+        const int64_t n = list_off[b + 1] - list_off[b];
+        const bool valid = r < n;
+        const int32_t gid = valid ? list_ids[list_off[b] + r] : -1;
+        const float *src = valid ? x + (int64_t)gid * d : nullptr;
+        float *dst = X + t * dpad * kTile + l;
+        for (int64_t j = jg; j < dpad; j += 4) dst[j * kTile] = (valid && j < d) ? src[j] : 0.0f;
+        if (jg == 0) ids[t * kTile + l] = gid;
+    }
+}
+
+__global__ void k_check_ids(const int32_t *ids, int64_t n, int64_t n_rows, int32_t *bad) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        if (ids[i] < 0 || ids[i] >= n_rows) atomicOr(bad, 1);
+}
+
+static void free_storage(lira_index *idx) {
+    if (idx->X) hipFree(idx->X);
+    if (idx->ids) hipFree(idx->ids);
+    if (idx->tile_off) hipFree(idx->tile_off);
+    if (idx->list_size) hipFree(idx->list_size);
+    idx->X = nullptr;
+    idx->ids = nullptr;
+    idx->tile_off = nullptr;
+    idx->list_size = nullptr;
+    idx->n_lists = idx->ntotal = idx->n_tiles = idx->max_list = idx->max_list_tiles = 0;
+    idx->h_list_size.clear();
+    idx->h_tile_off.clear();
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) hipSetDevice(prev);
+    }
+};
+
+}  // namespace lira
+
+using namespace lira;
+
+extern "C" {
+
+int lira_abi_version(void) { return LIRA_ABI_VERSION; }
+
+const char *lira_last_error(void) { return g_last_error.c_str(); }
+
+int lira_device_cu_count(int device, int *out) {
+    if (!out) return fail(LIRA_EINVAL, "out is NULL");
+    int v = 0;
+    LIRA_HIP_TRY(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device));
+    *out = v;
+    return LIRA_OK;
+}
+
+int lira_index_create(int device, int64_t d, int metric, lira_index **out) {
+    if (!out) return fail(LIRA_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (d <= 0) return fail(LIRA_EINVAL, "d must be > 0");
+    if (metric != LIRA_METRIC_L2 && metric != LIRA_METRIC_IP)
+        return fail(LIRA_EINVAL, "metric must be LIRA_METRIC_L2 or LIRA_METRIC_IP");
+    int ndev = 0;
+    LIRA_HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev)
+        return fail(LIRA_EINVAL, "device " + std::to_string(device) + " not present");
+    DeviceGuard g(device);
+    lira_index *idx = new (std::nothrow) lira_index();
+    if (!idx) return fail(LIRA_ENOMEM, "host allocation failed");
+    idx->device = device;
+    idx->d = d;
+    idx->dpad = round_up(d, kDimChunk);
+    idx->metric = metric;
+    if (hipMalloc(&idx->err, 16) != hipSuccess || hipMemset(idx->err, 0, 16) != hipSuccess) {
+        delete idx;
+        return fail(LIRA_ENOMEM, "hipMalloc of the error word failed");
+    }
+    *out = idx;
+    return LIRA_OK;
+}
+
+int lira_index_destroy(lira_index *idx) {
+    if (!idx) return LIRA_OK;
+    DeviceGuard g(idx->device);
+    hipDeviceSynchronize();
+    free_storage(idx);
+    if (idx->err) hipFree(idx->err);
+    if (idx->ws) hipFree(idx->ws);
+    for (hipEvent_t e : idx->ev_pool) hipEventDestroy(e);
+    delete idx;
+    return LIRA_OK;
+}
+
+int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *list_offsets,
+                              const int32_t *list_ids, const float *x, int64_t n_rows,
+                              int32_t max_replicas, void *stream) {
+    if (!idx) return fail(LIRA_EINVAL, "index is NULL");
+    if (n_lists <= 0 || !list_offsets) return fail(LIRA_EINVAL, "n_lists must be > 0 with offsets");
+    if (n_rows < 0) return fail(LIRA_EINVAL, "n_rows < 0");
+    DeviceGuard g(idx->device);
+    hipStream_t st = (hipStream_t)stream;
+    if (list_offsets[0] != 0) return fail(LIRA_EINVAL, "list_offsets[0] must be 0");
+    std::vector<int64_t> size(n_lists), toff(n_lists + 1);
+    std::vector<int32_t> toff32(n_lists + 1), size32(n_lists);
+    int64_t tiles = 0, mx = 0, mxt = 0;
+    for (int64_t b = 0; b < n_lists; ++b) {
+        int64_t n = list_offsets[b + 1] - list_offsets[b];
+        if (n < 0) return fail(LIRA_EINVAL, "list_offsets must be non-decreasing");
+        if (n > INT32_MAX) return fail(LIRA_EUNSUPPORTED, "bucket larger than 2^31 rows");
+        size[b] = n;
+        size32[b] = (int32_t)n;
+        toff[b] = tiles;
+        toff32[b] = (int32_t)tiles;
+        int64_t nt = (n + kTile - 1) / kTile;
+        tiles += nt;
+        mx = std::max(mx, n);
+        mxt = std::max(mxt, nt);
+    }
+    toff[n_lists] = tiles;
+    if (tiles >= INT32_MAX) return fail(LIRA_EUNSUPPORTED, "more than 2^31 tiles");
+    toff32[n_lists] = (int32_t)tiles;
+    const int64_t total = list_offsets[n_lists];
+    if (total > 0 && (!list_ids || !x)) return fail(LIRA_EINVAL, "list_ids / x is NULL");
+    if (n_rows > INT32_MAX) return fail(LIRA_EUNSUPPORTED, "more than 2^31 base rows (int32 gids)");
+
+    free_storage(idx);
+    std::vector<int32_t> tile_list(tiles);
+    for (int64_t b = 0; b < n_lists; ++b)
+        for (int64_t t = toff[b]; t < toff[b + 1]; ++t) tile_list[t] = (int32_t)b;
+
+    const size_t xbytes = (size_t)std::max<int64_t>(tiles, 1) * idx->dpad * kTile * 4;
+    if (hipMalloc(&idx->X, xbytes) != hipSuccess ||
+        hipMalloc(&idx->ids, (size_t)std::max<int64_t>(tiles, 1) * kTile * 4) != hipSuccess ||
+        hipMalloc(&idx->tile_off, (n_lists + 1) * 4) != hipSuccess ||
+        hipMalloc(&idx->list_size, n_lists * 4) != hipSuccess) {
+        free_storage(idx);
+        return fail(LIRA_ENOMEM, "hipMalloc of " + std::to_string(xbytes) + " bytes for the lists failed");
+    }
+    int64_t *d_loff = nullptr;
+    int32_t *d_tlist = nullptr, *d_bad = nullptr;
+    int rc = LIRA_OK;
+    do {
+        if (hipMalloc(&d_loff, (n_lists + 1) * 8) != hipSuccess ||
+            hipMalloc(&d_tlist, (size_t)std::max<int64_t>(tiles, 1) * 4) != hipSuccess ||
+            hipMalloc(&d_bad, 4) != hipSuccess) {
+            rc = fail(LIRA_ENOMEM, "hipMalloc of build scratch failed");
+            break;
+        }
+        hipError_t e = hipMemcpyAsync(d_loff, list_offsets, (n_lists + 1) * 8, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(d_tlist, tile_list.data(), tiles * 4, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(idx->tile_off, toff32.data(), (n_lists + 1) * 4, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(idx->list_size, size32.data(), n_lists * 4, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipMemsetAsync(d_bad, 0, 4, st);
+        if (e != hipSuccess) {
+            rc = fail(LIRA_EHIP, std::string("upload failed: ") + hipGetErrorString(e));
+            break;
+        }
+        if (total > 0) {
+            hipLaunchKernelGGL(k_check_ids, dim3(1024), dim3(256), 0, st, list_ids, total, n_rows, d_bad);
+            int32_t bad = 0;
+            e = hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) {
+                rc = fail(LIRA_EHIP, std::string("id check failed: ") + hipGetErrorString(e));
+                break;
+            }
+            if (bad) {
+                rc = fail(LIRA_ERANGE, "list_ids holds a row id outside [0, n_rows)");
+                break;
+            }
+        }
+        if (tiles > 0) {
+            int grid = (int)std::min<int64_t>(tiles, 65536);
+            hipLaunchKernelGGL(k_tile_gather, dim3(grid), dim3(256), 0, st, x, idx->d, idx->dpad,
+                               list_ids, d_loff, idx->tile_off, d_tlist, tiles, idx->X, idx->ids);
+        }
+        e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) {
+            rc = fail(LIRA_EHIP, std::string("tile gather failed: ") + hipGetErrorString(e));
+            break;
+        }
+    } while (0);
+    if (d_loff) hipFree(d_loff);
+    if (d_tlist) hipFree(d_tlist);
+    if (d_bad) hipFree(d_bad);
+    if (rc != LIRA_OK) {
+        free_storage(idx);
+        return rc;
+    }
+    idx->n_lists = n_lists;
+    idx->ntotal = total;
+    idx->n_tiles = tiles;
+    idx->max_list = mx;
+    idx->max_list_tiles = mxt;
+    idx->max_replicas = std::max<int32_t>(1, max_replicas);
+    idx->h_list_size = size;
+    idx->h_tile_off = toff;
+    return LIRA_OK;
+}
+
+int lira_index_info(const lira_index *idx, int64_t *d, int *metric, int64_t *n_lists,
+                    int64_t *ntotal, int64_t *max_list) {
+    if (!idx) return fail(LIRA_EINVAL, "index is NULL");
+    if (d) *d = idx->d;
+    if (metric) *metric = idx->metric;
+    if (n_lists) *n_lists = idx->n_lists;
+    if (ntotal) *ntotal = idx->ntotal;
+    if (max_list) *max_list = idx->max_list;
+    return LIRA_OK;
+}
+
+int lira_index_list_size(const lira_index *idx, int64_t list_no, int64_t *out) {
+    if (!idx || !out) return fail(LIRA_EINVAL, "NULL argument");
+    if (list_no < 0 || list_no >= idx->n_lists) return fail(LIRA_ERANGE, "list_no out of range");
+    *out = idx->h_list_size[list_no];
+    return LIRA_OK;
+}
+
+int lira_index_memory(const lira_index *idx, int64_t *bytes) {
+    if (!idx || !bytes) return fail(LIRA_EINVAL, "NULL argument");
+    *bytes = idx->n_tiles * idx->dpad * kTile * 4 + idx->n_tiles * kTile * 4 + idx->n_lists * 8;
+    return LIRA_OK;
+}
+
+int lira_scan_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe_max, int64_t k,
+                             unsigned flags, size_t *bytes) {
+    (void)flags;
+    if (!idx || !bytes) return fail(LIRA_EINVAL, "NULL argument");
+    if (nq < 0 || nprobe_max <= 0 || k <= 0 || k > 256)
+        return fail(LIRA_EINVAL, "need nq >= 0, nprobe_max > 0, 1 <= k <= 256");
+    return scan_workspace_size(idx, nq, nprobe_max, k, bytes);
+}
+
+int lira_scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
+                   int64_t nprobe_max, int64_t k, unsigned flags, float *out_D, int64_t *out_I,
+                   int64_t *out_ncand, void *workspace, size_t workspace_bytes, void *stream) {
+    if (!idx) return fail(LIRA_EINVAL, "index is NULL");
+    if (idx->n_lists == 0) return fail(LIRA_ESTATE, "index has no lists (add_partitions first)");
+    if (nq < 0 || nprobe_max <= 0) return fail(LIRA_EINVAL, "need nq >= 0 and nprobe_max > 0");
+    if (k <= 0 || k > 256) return fail(LIRA_EUNSUPPORTED, "k must be in [1, 256]");
+    if (flags & ~(LIRA_SCAN_DEDUP | LIRA_SCAN_PER_PARTITION)) return fail(LIRA_EINVAL, "unknown flags");
+    if (nq > 0 && (!q || !probe || !out_D || !out_I)) return fail(LIRA_EINVAL, "NULL buffer");
+    DeviceGuard g(idx->device);
+    return scan_topk(idx, q, nq, probe, nprobe_max, k, flags, out_D, out_I, out_ncand, workspace,
+                     workspace_bytes, (hipStream_t)stream);
+}
+
+int lira_index_set_profiling(lira_index *idx, int enable) {
+    if (!idx) return fail(LIRA_EINVAL, "index is NULL");
+    idx->profiling = enable != 0;
+    idx->ev_used = 0;
+    return LIRA_OK;
+}
+
+int lira_index_profile_read(lira_index *idx, double *plan_ms, double *scan_ms, double *merge_ms,
+                            int64_t *calls) {
+    if (!idx) return fail(LIRA_EINVAL, "index is NULL");
+    DeviceGuard g(idx->device);
+    double sp = 0, ss = 0, sm = 0;
+    const size_t n = idx->ev_used / 4;
+    if (n) LIRA_HIP_TRY(hipEventSynchronize(idx->ev_pool[idx->ev_used - 1]));
+    for (size_t c = 0; c < n; ++c) {
+        hipEvent_t *e = &idx->ev_pool[4 * c];
+        float a = 0, b = 0, m = 0;
+        LIRA_HIP_TRY(hipEventElapsedTime(&a, e[0], e[1]));
+        LIRA_HIP_TRY(hipEventElapsedTime(&b, e[1], e[2]));
+        LIRA_HIP_TRY(hipEventElapsedTime(&m, e[2], e[3]));
+        sp += a;
+        ss += b;
+        sm += m;
+    }
+    idx->ev_used = 0;
+    if (plan_ms) *plan_ms = sp;
+    if (scan_ms) *scan_ms = ss;
+    if (merge_ms) *merge_ms = sm;
+    if (calls) *calls = (int64_t)n;
+    return LIRA_OK;
+}
+
+int lira_index_check(lira_index *idx, void *stream) {
+    if (!idx) return fail(LIRA_EINVAL, "index is NULL");
+    DeviceGuard g(idx->device);
+    hipStream_t st = (hipStream_t)stream;
+    int32_t e = 0;
+    LIRA_HIP_TRY(hipMemcpyAsync(&e, idx->err, 4, hipMemcpyDeviceToHost, st));
+    LIRA_HIP_TRY(hipStreamSynchronize(st));
+    if (e) {
+        LIRA_HIP_TRY(hipMemsetAsync(idx->err, 0, 4, st));
+        LIRA_HIP_TRY(hipStreamSynchronize(st));
+        return fail(LIRA_ERANGE, "a probe id was >= n_lists (slot skipped)");
+    }
+    return LIRA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,124 @@
+// lira_device.hpp -- device helpers shared by the gfx950 kernels:
+// ordered (score, gid) keys and wave64 bitonic networks for exact top-k.
+//
+// Keys.  A candidate is the 64-bit key  (ord(score) << 32) | gid  where ord()
+// maps fp32 to an order-preserving u32, so unsigned key order is exactly the
+// canonical (score asc, gid asc) order of oracle/lira_oracle.c.  The empty key
+// is ~0 (sorts last).  Scores are l2_sq (L2) or -ip (IP), as search.cpp:483-488.
+//
+// Lists.  A wave keeps a sorted list of N = 64*R keys in R registers per lane;
+// element e = r*64 + lane.  Merging a 64-key batch costs one bitonic sort of the
+// batch (21 shuffle stages) + one bitonic merge of the list (log2 N stages).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lira {
+
+typedef unsigned long long u64;
+static constexpr u64 kEmptyKey = ~0ull;
+static constexpr int kWave = 64;
+
+__device__ __forceinline__ uint32_t f2ord(float s) {
+    s = s + 0.0f;  // -0 -> +0 so both zeros order as one value (== in the oracle)
+    uint32_t u = __float_as_uint(s);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(uint32_t u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+__device__ __forceinline__ u64 make_key(float score, int32_t gid) {
+    return gid < 0 ? kEmptyKey : ((u64)f2ord(score) << 32) | (uint32_t)gid;
+}
+__device__ __forceinline__ float key_score(u64 k) { return ord2f((uint32_t)(k >> 32)); }
+__device__ __forceinline__ int32_t key_gid(u64 k) { return (int32_t)(uint32_t)(k & 0xffffffffu); }
+
+__device__ __forceinline__ u64 kmin(u64 a, u64 b) { return a < b ? a : b; }
+__device__ __forceinline__ u64 kmax(u64 a, u64 b) { return a < b ? b : a; }
+
+__device__ __forceinline__ u64 shfl_xor64(u64 v, int m) {
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    lo = __shfl_xor((int)lo, m, 64);
+    hi = __shfl_xor((int)hi, m, 64);
+    return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ u64 shfl64(u64 v, int src) {
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    lo = __shfl((int)lo, src, 64);
+    hi = __shfl((int)hi, src, 64);
+    return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+
+// Full ascending bitonic sort of 64 keys, one per lane.
+__device__ __forceinline__ u64 wave_sort64(u64 v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            u64 o = shfl_xor64(v, stride);
+            bool lower = (lane & stride) == 0;
+            bool asc = (lane & size) == 0;
+            v = (lower == asc) ? kmin(v, o) : kmax(v, o);
+        }
+    }
+    return v;
+}
+
+// Sort a bitonic sequence of 64*R keys ascending.
+template <int R>
+__device__ __forceinline__ void wave_bitonic_merge(u64 (&v)[R]) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int rs = R / 2; rs >= 1; rs >>= 1) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if ((r & rs) == 0) {
+                u64 a = v[r], b = v[r | rs];
+                v[r] = kmin(a, b);
+                v[r | rs] = kmax(a, b);
+            }
+        }
+    }
+#pragma unroll
+    for (int stride = 32; stride > 0; stride >>= 1) {
+        bool lower = (lane & stride) == 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            u64 o = shfl_xor64(v[r], stride);
+            v[r] = lower ? kmin(v[r], o) : kmax(v[r], o);
+        }
+    }
+}
+
+// list (sorted, 64*R) <- the 64*R smallest of list U batch (batch: any order).
+// Half-cleaner: only the last register can change; min(list_last, reversed
+// sorted batch) keeps the smallest 64 of that register U batch and leaves the
+// whole list bitonic, so one merge network re-sorts it.
+template <int R>
+__device__ __forceinline__ void wave_merge_batch(u64 (&list)[R], u64 batch) {
+    const int lane = lane_id();
+    batch = wave_sort64(batch);
+    u64 rev = shfl64(batch, 63 - lane);
+    list[R - 1] = kmin(list[R - 1], rev);
+    wave_bitonic_merge<R>(list);
+}
+
+// Broadcast list element e (compile-time-unknown) to the whole wave.
+template <int R>
+__device__ __forceinline__ u64 wave_list_at(const u64 (&list)[R], int e) {
+    u64 x = list[0];
+#pragma unroll
+    for (int r = 1; r < R; ++r)
+        if ((e >> 6) == r) x = list[r];
+    return shfl64(x, e & 63);
+}
+
+__device__ __forceinline__ int popc64(u64 m) { return __popcll(m); }
+// number of set bits of m in lanes below this lane
+__device__ __forceinline__ int mbcnt64(u64 m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
+}  // namespace lira

@@ -1,0 +1,57 @@
+// lira_internal.hpp -- host-side state shared by the C-ABI translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "lira_hip.h"
+
+namespace lira {
+
+// thread-local message behind lira_last_error()
+void set_error(const std::string &msg);
+int fail(int code, const std::string &msg);
+
+#define LIRA_HIP_TRY(expr)                                                                     \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return ::lira::fail(LIRA_EHIP, std::string(#expr " failed: ") + hipGetErrorString(e_)); \
+    } while (0)
+
+// HBM layout of the partitioned base vectors.
+//   X    : [n_tiles][dpad][64] fp32   -- 64 candidates per tile, d-major, so a
+//          wave reading dims j..j+3 of a tile reads 1 KiB contiguous; dims in
+//          [d, dpad) are zero (dpad = d rounded up to kDimChunk).
+//   ids  : [n_tiles*64] int32 global row ids, -1 for the padding slots.
+//   tile_off[b]..tile_off[b+1]: the tiles of bucket b; list_size[b]: its rows.
+static constexpr int kTile = 64;
+static constexpr int kDimChunk = 32;
+
+struct lira_index_impl {
+    int device = 0;
+    int64_t d = 0, dpad = 0;
+    int metric = LIRA_METRIC_L2;
+    int64_t n_lists = 0, ntotal = 0, n_tiles = 0, max_list = 0, max_list_tiles = 0;
+    int32_t max_replicas = 1;
+    std::vector<int64_t> h_list_size, h_tile_off;
+    float *X = nullptr;
+    int32_t *ids = nullptr;
+    int32_t *tile_off = nullptr;   // n_lists+1 (int32: < 2^31 tiles)
+    int32_t *list_size = nullptr;  // n_lists
+    int32_t *err = nullptr;        // device error word
+    void *ws = nullptr;            // cached scan workspace
+    size_t ws_bytes = 0;
+    // profiling: 4 events per recorded call (start, after plan, after scan, after merge)
+    bool profiling = false;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+};
+
+int64_t round_up(int64_t x, int64_t m);
+
+}  // namespace lira
+
+struct lira_index : lira::lira_index_impl {};

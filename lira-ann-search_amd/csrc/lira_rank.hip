@@ -1,0 +1,360 @@
+// lira_rank.hip -- query -> centroid ranking and probe selection (gfx950).
+//
+//   k_centroid_dist   exact search.cpp distances: sqrt of the sequential fp32
+//                     sum of fl(q-c)^2 (search.cpp:220-235), optional
+//                     standardisation (search.cpp:238-250).  Feeds the probing
+//                     MLP and the threshold probe (search.cpp:430-466).
+//   k_centroid_gemm   MFMA (v_mfma_f32_32x32x2_f32) ||q||^2+||c||^2-2q.c with a
+//                     per-query error bound; the batched ranking GEMM.
+//   k_rank_select     nearest-nprobe from the GEMM, exact boundary re-check so
+//                     the result equals ranking by the exact distances.
+//   k_select_probes   nearest / threshold(>=, argmax fallback) / threshold(>)
+//                     over a score matrix (search.cpp:447-466, LIRA_smallscale.py:206).
+#include <algorithm>
+#include <string>
+
+#include "lira_device.hpp"
+#include "lira_internal.hpp"
+
+namespace lira {
+
+// ---------------------------------------------------------------- exact dist
+// One wave per query, lane = centroid.  Centroids are re-read from L2 (B*d*4
+// bytes, 32 KiB at SIFT/B=64); the query row is wave-uniform.
+__global__ __launch_bounds__(256) void k_centroid_dist(const float *__restrict__ q, int64_t nq,
+                                                       const float *__restrict__ cent, int nb,
+                                                       int64_t d, const float *mean,
+                                                       const float *scale, float *out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t qi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (qi >= nq) return;
+    const float *qr = q + qi * d;
+    for (int b0 = 0; b0 < nb; b0 += 64) {
+        const int b = b0 + lane;
+        if (b >= nb) break;
+        const float *cr = cent + (int64_t)b * d;
+        float acc = 0.0f;
+        for (int64_t j = 0; j < d; ++j) {
+            float df = qr[j] - cr[j];
+            acc = acc + df * df;
+        }
+        float r = __fsqrt_rn(acc);
+        if (mean) {
+            float s = scale[b];
+            if (s == 0.0f) s = 1.0f;
+            r = __fdiv_rn(r - mean[b], s);
+        }
+        out[qi * nb + b] = r;
+    }
+}
+
+// ---------------------------------------------------------------- MFMA GEMM
+// Workgroup = 4 waves = 64 queries x 64 centroids; wave (wr, wc) owns a 32x32
+// accumulator of v_mfma_f32_32x32x2_f32 (A: lane -> row lane&31, k lane>>5;
+// B: k lane>>5, col lane&31; C: col lane&31, row (r&3)+8(r>>2)+4(lane>>5)).
+// Operands are staged through LDS in 32-dim chunks (padded rows, no conflicts).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__global__ __launch_bounds__(256) void k_centroid_gemm(const float *__restrict__ q, int64_t nq,
+                                                       const float *__restrict__ cent, int nb,
+                                                       int64_t d, float *out_sq, float *out_err) {
+    __shared__ float Qs[64][33];
+    __shared__ float Cs[64][33];
+    __shared__ float nrm[128];  // [0,64) query norms, [64,128) centroid norms
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wr = w >> 1, wc = w & 1;
+    const int64_t q0 = (int64_t)blockIdx.x * 64;
+    const int c0 = blockIdx.y * 64;
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+    float nacc = 0.0f;  // thread t<128 accumulates norm of row t
+    for (int64_t k0 = 0; k0 < d; k0 += 32) {
+        __syncthreads();
+        for (int i = tid; i < 64 * 32; i += 256) {
+            int r = i >> 5, kk = i & 31;
+            int64_t k = k0 + kk;
+            int64_t qr = q0 + r;
+            int cr = c0 + r;
+            Qs[r][kk] = (qr < nq && k < d) ? q[qr * d + k] : 0.0f;
+            Cs[r][kk] = (cr < nb && k < d) ? cent[(int64_t)cr * d + k] : 0.0f;
+        }
+        __syncthreads();
+        if (tid < 128) {
+            const float *row = tid < 64 ? Qs[tid] : Cs[tid - 64];
+#pragma unroll 8
+            for (int kk = 0; kk < 32; ++kk) nacc = fmaf(row[kk], row[kk], nacc);
+        }
+#pragma unroll
+        for (int kk = 0; kk < 32; kk += 2) {
+            float a = Qs[wr * 32 + (lane & 31)][kk + (lane >> 5)];
+            float b = Cs[wc * 32 + (lane & 31)][kk + (lane >> 5)];
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+        }
+    }
+    if (tid < 128) nrm[tid] = nacc;
+    __syncthreads();
+    // |A - R| <= (2 gamma_d + 4u)(nq + nc) and |E - R| <= 2 gamma_{d+3}(nq + nc)
+    // (R real, E = search.cpp's sequential sum), so |A - E| <= (4d + 10)u(nq + nc);
+    // 8(d+8)u leaves room for sqrt() merging nearby E values into one float.
+    const float ebound = 8.0f * (float)(d + 8) * 5.9604645e-08f;
+    const int col = lane & 31;
+    const int cb = c0 + wc * 32 + col;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        int64_t qr = q0 + wr * 32 + row;
+        float nq_ = nrm[wr * 32 + row], nc_ = nrm[64 + wc * 32 + col];
+        float v = (nq_ + nc_) - 2.0f * acc[r];
+        if (qr < nq && cb < nb) {
+            out_sq[qr * nb + cb] = v;
+            if (out_err) atomicMax((unsigned int *)&out_err[qr], __float_as_uint(ebound * (nq_ + nc_) + 1e-30f));
+        }
+    }
+}
+
+// -------------------------------------------------------- nearest, re-checked
+// One wave per query.  1) T = nprobe-th smallest approximate value; 2) every b
+// with A_b <= T + 2M (M = the query's error bound) gets its exact search.cpp
+// distance; 3) exact (sqrt(l2), b) top-nprobe.  Any b of the exact top-nprobe
+// satisfies A_b <= T + 2M, so the result equals ranking all B exactly.
+template <int R>
+__global__ __launch_bounds__(256) void k_rank_select(const float *__restrict__ A,
+                                                     const float *__restrict__ err,
+                                                     const float *__restrict__ q, int64_t nq,
+                                                     const float *__restrict__ cent, int nb,
+                                                     int64_t d, int nprobe, int32_t *out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t qi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (qi >= nq) return;
+    const float *arow = A + qi * nb;
+    u64 lst[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) lst[r] = kEmptyKey;
+    for (int b0 = 0; b0 < nb; b0 += 64) {
+        int b = b0 + lane;
+        u64 key = b < nb ? make_key(arow[b], b) : kEmptyKey;
+        u64 thr = wave_list_at<R>(lst, nprobe - 1);
+        if (__ballot(key < thr)) wave_merge_batch<R>(lst, key);
+    }
+    const u64 tk = wave_list_at<R>(lst, nprobe - 1);
+    const float lim = tk == kEmptyKey ? __builtin_inff() : key_score(tk) + 2.0f * err[qi] * 1.0001f;
+    const float *qr = q + qi * d;
+    u64 fin[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) fin[r] = kEmptyKey;
+    for (int b0 = 0; b0 < nb; b0 += 64) {
+        int b = b0 + lane;
+        bool cand = b < nb && arow[b] <= lim;
+        if (!__ballot(cand)) continue;
+        u64 key = kEmptyKey;
+        if (cand) {
+            const float *cr = cent + (int64_t)b * d;
+            float acc = 0.0f;
+            for (int64_t j = 0; j < d; ++j) {
+                float df = qr[j] - cr[j];
+                acc = acc + df * df;
+            }
+            key = make_key(__fsqrt_rn(acc), b);
+        }
+        wave_merge_batch<R>(fin, key);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        int e = r * 64 + lane;
+        if (e < nprobe) out[qi * nprobe + e] = fin[r] == kEmptyKey ? -1 : key_gid(fin[r]);
+    }
+}
+
+// -------------------------------------------------------------- probe select
+template <int R>
+__global__ __launch_bounds__(256) void k_select_nearest(const float *__restrict__ s, int64_t n,
+                                                        int nb, int np, int32_t *out,
+                                                        int32_t *out_np) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const float *row = s + i * nb;
+    u64 lst[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) lst[r] = kEmptyKey;
+    for (int b0 = 0; b0 < nb; b0 += 64) {
+        int b = b0 + lane;
+        u64 key = b < nb ? make_key(row[b], b) : kEmptyKey;
+        u64 thr = wave_list_at<R>(lst, np - 1);
+        if (__ballot(key < thr)) wave_merge_batch<R>(lst, key);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        int e = r * 64 + lane;
+        if (e < np) out[i * np + e] = lst[r] == kEmptyKey ? -1 : key_gid(lst[r]);
+    }
+    if (out_np && lane == 0) out_np[i] = min(np, nb);
+}
+
+// threshold: ascending bucket order; ge = (>=, argmax fallback) else (>, none)
+__global__ __launch_bounds__(256) void k_select_threshold(const float *__restrict__ s, int64_t n,
+                                                          int nb, float thr, int ge, int maxp,
+                                                          int32_t *out, int32_t *out_np) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const float *row = s + i * nb;
+    int32_t *o = out + i * maxp;
+    int m = 0;
+    float best = -__builtin_inff();
+    int bestb = 0x7fffffff;
+    for (int b0 = 0; b0 < nb; b0 += 64) {
+        int b = b0 + lane;
+        float v = b < nb ? row[b] : 0.0f;
+        bool take = b < nb && (ge ? v >= thr : v > thr);
+        u64 bal = __ballot(take);
+        int pos = m + mbcnt64(bal);
+        if (take && pos < maxp) o[pos] = b;
+        m += popc64(bal);
+        // running argmax, first max wins (search.cpp:456-466: strict >)
+        if (b < nb && (v > best || (v == best && b < bestb))) {
+            best = v;
+            bestb = b;
+        }
+    }
+    if (ge && m == 0) {
+        // wave argmax over (best, bestb): larger value, then smaller bucket
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            float ov = __shfl_xor(best, off, 64);
+            int ob = __shfl_xor(bestb, off, 64);
+            if (ov > best || (ov == best && ob < bestb)) {
+                best = ov;
+                bestb = ob;
+            }
+        }
+        // search.cpp seeds with bucket 0 and replaces only on strictly greater
+        // values: a NaN in bucket 0 (or a row of NaNs) probes bucket 0
+        if (bestb == 0x7fffffff || row[0] != row[0]) bestb = 0;
+        if (lane == 0) o[0] = bestb;
+        m = 1;
+    }
+    const int mm = min(m, maxp);
+    for (int e = mm + lane; e < maxp; e += 64) o[e] = -1;
+    if (out_np && lane == 0) out_np[i] = mm;
+}
+
+static int sel_r(int64_t np) { return np <= 64 ? 1 : np <= 128 ? 2 : np <= 256 ? 4 : -1; }
+
+}  // namespace lira
+
+using namespace lira;
+
+extern "C" {
+
+int lira_centroid_dist(const float *q, int64_t nq, const float *centroids, int64_t n_centroids,
+                       int64_t d, const float *scaler_mean, const float *scaler_scale, float *out,
+                       void *stream) {
+    if (nq < 0 || n_centroids <= 0 || d <= 0) return fail(LIRA_EINVAL, "bad shape");
+    if (n_centroids > INT32_MAX) return fail(LIRA_EUNSUPPORTED, "too many centroids");
+    if ((scaler_mean == nullptr) != (scaler_scale == nullptr))
+        return fail(LIRA_EINVAL, "scaler_mean and scaler_scale must both be set or both NULL");
+    if (nq == 0) return LIRA_OK;
+    if (!q || !centroids || !out) return fail(LIRA_EINVAL, "NULL buffer");
+    hipLaunchKernelGGL(k_centroid_dist, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, q, nq, centroids, (int)n_centroids, d, scaler_mean,
+                       scaler_scale, out);
+    LIRA_HIP_TRY(hipGetLastError());
+    return LIRA_OK;
+}
+
+int lira_centroid_gemm(const float *q, int64_t nq, const float *centroids, int64_t n_centroids,
+                       int64_t d, float *out_sq, float *out_err, void *stream) {
+    if (nq < 0 || n_centroids <= 0 || d <= 0) return fail(LIRA_EINVAL, "bad shape");
+    if (n_centroids > INT32_MAX) return fail(LIRA_EUNSUPPORTED, "too many centroids");
+    if (nq == 0) return LIRA_OK;
+    if (!q || !centroids || !out_sq) return fail(LIRA_EINVAL, "NULL buffer");
+    hipStream_t st = (hipStream_t)stream;
+    if (out_err) LIRA_HIP_TRY(hipMemsetAsync(out_err, 0, nq * 4, st));
+    dim3 grid((unsigned)((nq + 63) / 64), (unsigned)((n_centroids + 63) / 64));
+    hipLaunchKernelGGL(k_centroid_gemm, grid, dim3(256), 0, st, q, nq, centroids,
+                       (int)n_centroids, d, out_sq, out_err);
+    LIRA_HIP_TRY(hipGetLastError());
+    return LIRA_OK;
+}
+
+int lira_rank_workspace_size(int64_t nq, int64_t n_centroids, size_t *bytes) {
+    if (!bytes || nq < 0 || n_centroids <= 0) return fail(LIRA_EINVAL, "bad arguments");
+    *bytes = (size_t)round_up(nq * n_centroids * 4, 256) + (size_t)round_up(nq * 4, 256);
+    return LIRA_OK;
+}
+
+int lira_rank_nearest(const float *q, int64_t nq, const float *centroids, int64_t n_centroids,
+                      int64_t d, int64_t nprobe, int32_t *out_probe, void *workspace,
+                      size_t workspace_bytes, void *stream) {
+    if (nq < 0 || n_centroids <= 0 || d <= 0) return fail(LIRA_EINVAL, "bad shape");
+    int R = sel_r(nprobe);
+    if (nprobe <= 0 || R < 0) return fail(LIRA_EUNSUPPORTED, "nprobe must be in [1, 256]");
+    if (nq == 0) return LIRA_OK;
+    if (!q || !centroids || !out_probe) return fail(LIRA_EINVAL, "NULL buffer");
+    size_t need = 0;
+    lira_rank_workspace_size(nq, n_centroids, &need);
+    hipStream_t st = (hipStream_t)stream;
+    void *ws = workspace;
+    bool own = false;
+    if (!ws) {
+        LIRA_HIP_TRY(hipMallocAsync(&ws, need, st));
+        own = true;
+    } else if (workspace_bytes < need) {
+        return fail(LIRA_EINVAL, "rank workspace too small: need " + std::to_string(need));
+    }
+    float *A = (float *)ws;
+    float *err = (float *)((char *)ws + round_up(nq * n_centroids * 4, 256));
+    int rc = lira_centroid_gemm(q, nq, centroids, n_centroids, d, A, err, stream);
+    if (rc == LIRA_OK) {
+        dim3 g((unsigned)((nq + 3) / 4));
+        if (R == 1)
+            hipLaunchKernelGGL(k_rank_select<1>, g, dim3(256), 0, st, A, err, q, nq, centroids,
+                               (int)n_centroids, d, (int)nprobe, out_probe);
+        else if (R == 2)
+            hipLaunchKernelGGL(k_rank_select<2>, g, dim3(256), 0, st, A, err, q, nq, centroids,
+                               (int)n_centroids, d, (int)nprobe, out_probe);
+        else
+            hipLaunchKernelGGL(k_rank_select<4>, g, dim3(256), 0, st, A, err, q, nq, centroids,
+                               (int)n_centroids, d, (int)nprobe, out_probe);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) rc = fail(LIRA_EHIP, std::string("k_rank_select: ") + hipGetErrorString(e));
+    }
+    if (own) hipFreeAsync(ws, st);
+    return rc;
+}
+
+int lira_select_probes(const float *scores, int64_t n, int64_t n_centroids, int mode, float thr,
+                       int64_t max_probe, int32_t *out_probe, int32_t *out_nprobe, void *stream) {
+    if (n < 0 || n_centroids <= 0 || max_probe <= 0) return fail(LIRA_EINVAL, "bad shape");
+    if (n_centroids > INT32_MAX) return fail(LIRA_EUNSUPPORTED, "too many centroids");
+    if (n == 0) return LIRA_OK;
+    if (!scores || !out_probe) return fail(LIRA_EINVAL, "NULL buffer");
+    hipStream_t st = (hipStream_t)stream;
+    dim3 g((unsigned)((n + 3) / 4));
+    if (mode == LIRA_PROBE_NEAREST) {
+        int R = sel_r(max_probe);
+        if (R < 0) return fail(LIRA_EUNSUPPORTED, "nearest mode supports max_probe <= 256");
+        if (R == 1)
+            hipLaunchKernelGGL(k_select_nearest<1>, g, dim3(256), 0, st, scores, n, (int)n_centroids,
+                               (int)max_probe, out_probe, out_nprobe);
+        else if (R == 2)
+            hipLaunchKernelGGL(k_select_nearest<2>, g, dim3(256), 0, st, scores, n, (int)n_centroids,
+                               (int)max_probe, out_probe, out_nprobe);
+        else
+            hipLaunchKernelGGL(k_select_nearest<4>, g, dim3(256), 0, st, scores, n, (int)n_centroids,
+                               (int)max_probe, out_probe, out_nprobe);
+    } else if (mode == LIRA_PROBE_THRESHOLD_GE || mode == LIRA_PROBE_THRESHOLD_GT) {
+        if (max_probe > INT32_MAX) return fail(LIRA_EUNSUPPORTED, "max_probe too large");
+        hipLaunchKernelGGL(k_select_threshold, g, dim3(256), 0, st, scores, n, (int)n_centroids, thr,
+                           mode == LIRA_PROBE_THRESHOLD_GE ? 1 : 0, (int)max_probe, out_probe,
+                           out_nprobe);
+    } else {
+        return fail(LIRA_EINVAL, "unknown probe mode");
+    }
+    LIRA_HIP_TRY(hipGetLastError());
+    return LIRA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,646 @@
+// lira_scan.hip -- batched candidate scan + exact top-k over probed buckets
+// (gfx950).  Replaces search.cpp:468-514 and the per-(query, bucket) faiss
+// IndexFlat*.search calls of get_cmp_recall (LIRA_smallscale.py:158-172).
+//
+// Schedule (partition-major).  The (query, slot) pairs of a batch are grouped
+// by the bucket they probe; a work item is (bucket, block of 32 queries, chunk
+// of the bucket).  A workgroup streams the chunk's 64-row d-major tiles
+// through LDS once for its 32 queries, so each candidate byte read from
+// HBM/L2 serves 32 query distances instead of one (search.cpp reads it once
+// per query).  The kernel is therefore VALU-bound, not HBM-bound.
+//
+// Exactness.  Every distance is one lane's sequential fp32 sum over dims
+// 0..d-1 of fl(fl(q-x)^2) (L2) or fl(q*x) (IP), with FP contraction off
+// (Makefile: -ffp-contract=off), i.e. bit-identical to search.cpp:253-269.
+// Top-k is exact over (score, gid) keys (lira_device.hpp).
+//
+// Kernels (one call = 5 launches, all stream-ordered, no host sync):
+//   k_count  pairs per bucket                  (probe histogram)
+//   k_plan   offsets, chunks per bucket, work-item prefix (one workgroup)
+//   k_fill   bucket -> pair lists
+//   k_scan   persistent; pulls work items from an atomic head
+//   k_merge  per query: merge the per-(slot, chunk) top-k lists, dedup, emit
+#include <algorithm>
+#include <string>
+
+#include "lira_device.hpp"
+#include "lira_internal.hpp"
+
+namespace lira {
+
+static constexpr int kQT = 32;        // queries per work item
+static constexpr int kBlockTiles = 4; // tiles per candidate block
+static constexpr int kCT = kBlockTiles * kTile;  // 256 candidates per block
+static constexpr int kScanThreads = 256;
+
+struct ScanArgs {
+    const float *Q;       // (nq, d)
+    const float *X;       // [n_tiles][dpad][64]
+    const int32_t *ids;   // [n_tiles*64]
+    const int32_t *tile_off;
+    const int32_t *cnt, *qoff, *qlist, *item_off, *nch;
+    int32_t *head;        // [0] = next item, [1] = n_items
+    u64 *partial;         // [pair][nch_max][k]
+    int64_t d, dpad;
+    int n_lists, nprobe, k, bpc, nch_max;
+};
+
+__global__ void k_count(const int32_t *probe, int64_t npairs, int n_lists, int32_t *cnt,
+                        int32_t *err) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < npairs;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int p = probe[i];
+        if (p >= n_lists) {
+            atomicOr(err, 1);
+            continue;
+        }
+        if (p >= 0) atomicAdd(&cnt[p], 1);
+    }
+}
+
+// One workgroup of 1024 threads: exclusive scans over the buckets.
+__global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t *tile_off,
+                                               int n_lists, int bpc, int32_t *qoff,
+                                               int32_t *item_off, int32_t *nch, int32_t *head) {
+    __shared__ int32_t s_a[1024], s_b[1024];
+    __shared__ int32_t carry_a, carry_b;
+    if (threadIdx.x == 0) carry_a = carry_b = 0;
+    __syncthreads();
+    for (int base = 0; base < n_lists; base += 1024) {
+        int p = base + threadIdx.x;
+        int c = 0, items = 0;
+        if (p < n_lists) {
+            c = cnt[p];
+            int ntl = tile_off[p + 1] - tile_off[p];
+            int nblk = (ntl + kBlockTiles - 1) / kBlockTiles;
+            int nc = (nblk + bpc - 1) / bpc;
+            nch[p] = nc;
+            items = ((c + kQT - 1) / kQT) * nc;
+        }
+        s_a[threadIdx.x] = c;
+        s_b[threadIdx.x] = items;
+        __syncthreads();
+        for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+            int va = threadIdx.x >= off ? s_a[threadIdx.x - off] : 0;
+            int vb = threadIdx.x >= off ? s_b[threadIdx.x - off] : 0;
+            __syncthreads();
+            s_a[threadIdx.x] += va;
+            s_b[threadIdx.x] += vb;
+            __syncthreads();
+        }
+        if (p < n_lists) {
+            qoff[p] = carry_a + s_a[threadIdx.x] - c;
+            item_off[p] = carry_b + s_b[threadIdx.x] - items;
+        }
+        __syncthreads();
+        if (threadIdx.x == 1023) {
+            carry_a += s_a[1023];
+            carry_b += s_b[1023];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        qoff[n_lists] = carry_a;
+        item_off[n_lists] = carry_b;
+        head[0] = 0;
+        head[1] = carry_b;
+    }
+}
+
+__global__ void k_fill(const int32_t *probe, int64_t npairs, int n_lists, const int32_t *qoff,
+                       int32_t *cursor, int32_t *qlist) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < npairs;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int p = probe[i];
+        if (p < 0 || p >= n_lists) continue;
+        int pos = atomicAdd(&cursor[p], 1);
+        qlist[qoff[p] + pos] = (int32_t)i;
+    }
+}
+
+// LDS carve (bytes): X staging / distance tile, Q staging, per-query lists,
+// per-wave compaction scratch, item metadata.
+template <int R>
+struct ScanSmem {
+    static constexpr int kX = kBlockTiles * kDimChunk * kTile * 4;  // 32 KiB
+    static constexpr int kQ = kDimChunk * kQT * 4;                  // 4 KiB
+    static constexpr int kLists = kQT * 64 * R * 8;
+    static constexpr int kScratch = (kScanThreads / 64) * kCT * 8;
+    static constexpr int kMeta = 64 * 4;
+    static constexpr int kTotal = kX + kQ + kLists + kScratch + kMeta;
+};
+
+template <int R, int METRIC>
+__global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    typedef ScanSmem<R> S;
+    float *Xs = (float *)smem;                       // [4][32][64] (alias: dist [32][256])
+    float *Qs = (float *)(smem + S::kX);             // [32 dims][32 queries]
+    u64 *lists = (u64 *)(smem + S::kX + S::kQ);      // [32][64R]
+    u64 *scratch = (u64 *)(smem + S::kX + S::kQ + S::kLists);
+    int *meta = (int *)(smem + S::kX + S::kQ + S::kLists + S::kScratch);
+    constexpr int KP = 64 * R;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tx = tid & 31, ty = tid >> 5;
+    const int k = a.k;
+
+    for (;;) {
+        if (tid == 0) {
+            int item = atomicAdd(&a.head[0], 1);
+            int n_items = a.head[1];
+            int ok = item < n_items;
+            int p = 0, qb = 0, ch = 0;
+            if (ok) {
+                int lo = 0, hi = a.n_lists - 1;  // last p with item_off[p] <= item
+                while (lo < hi) {
+                    int mid = (lo + hi + 1) >> 1;
+                    if (a.item_off[mid] <= item) lo = mid; else hi = mid - 1;
+                }
+                p = lo;
+                int local = item - a.item_off[p];
+                int nqb = (a.cnt[p] + kQT - 1) / kQT;
+                ch = local / nqb;
+                qb = local - ch * nqb;
+            }
+            meta[0] = ok;
+            meta[1] = p;
+            meta[2] = qb;
+            meta[3] = ch;
+        }
+        __syncthreads();
+        if (!meta[0]) break;
+        const int p = meta[1], qb = meta[2], ch = meta[3];
+        const int q0 = qb * kQT;
+        const int nqb_valid = min(kQT, a.cnt[p] - q0);
+        if (tid < kQT) meta[8 + tid] = tid < nqb_valid ? a.qlist[a.qoff[p] + q0 + tid] : -1;
+        for (int i = tid; i < kQT * KP; i += kScanThreads) lists[i] = kEmptyKey;
+        __syncthreads();
+
+        const int tile0 = a.tile_off[p];
+        const int ntl = a.tile_off[p + 1] - tile0;
+        const int tb_begin = ch * a.bpc * kBlockTiles;
+        const int tb_end = min(ntl, tb_begin + a.bpc * kBlockTiles);
+        // query staged by this thread: slot sq, dims (tid&7)*4 .. +3 of each chunk
+        const int sq = tid >> 3, sj = (tid & 7) * 4;
+        const int spair = meta[8 + sq];
+        const float *qrow = spair >= 0 ? a.Q + (int64_t)(spair / a.nprobe) * a.d : nullptr;
+
+        for (int tb = tb_begin; tb < tb_end; tb += kBlockTiles) {
+            const int ntv = min(kBlockTiles, tb_end - tb);
+            float acc[4][8];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int v = 0; v < 8; ++v) acc[u][v] = 0.0f;
+
+            for (int jc = 0; jc < a.dpad; jc += kDimChunk) {
+                __syncthreads();
+                {   // X chunk: tile t rows jc..jc+31 = 8 KiB contiguous in HBM and in LDS
+                    const float4 *src = (const float4 *)a.X;
+                    float4 *dst = (float4 *)Xs;
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        int f = i * kScanThreads + tid;
+                        int t = f >> 9, off = f & 511;
+                        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                        if (t < ntv)
+                            v = src[((int64_t)(tile0 + tb + t) * a.dpad + jc) * (kTile / 4) + off];
+                        dst[f] = v;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    int j = jc + sj + u;
+                    Qs[(sj + u) * kQT + sq] = (qrow && j < a.d) ? qrow[j] : 0.0f;
+                }
+                __syncthreads();
+#pragma unroll 4
+                for (int j = 0; j < kDimChunk; ++j) {
+                    float4 q4 = *(const float4 *)&Qs[j * kQT + ty * 4];
+                    float4 xa = *(const float4 *)&Xs[(tx >> 4) * (kDimChunk * kTile) + j * kTile + (tx & 15) * 4];
+                    float4 xb = *(const float4 *)&Xs[(2 + (tx >> 4)) * (kDimChunk * kTile) + j * kTile + (tx & 15) * 4];
+                    const float qv[4] = {q4.x, q4.y, q4.z, q4.w};
+                    const float xv[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+#pragma unroll
+                        for (int v = 0; v < 8; ++v) {
+                            if (METRIC == LIRA_METRIC_L2) {
+                                float df = qv[u] - xv[v];
+                                acc[u][v] = acc[u][v] + df * df;
+                            } else {
+                                acc[u][v] = acc[u][v] + qv[u] * xv[v];
+                            }
+                        }
+                }
+            }
+            __syncthreads();
+            float *dist = Xs;  // [32 queries][256 candidates]
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                *(float4 *)&dist[(ty * 4 + u) * kCT + tx * 4] =
+                    make_float4(acc[u][0], acc[u][1], acc[u][2], acc[u][3]);
+                *(float4 *)&dist[(ty * 4 + u) * kCT + 128 + tx * 4] =
+                    make_float4(acc[u][4], acc[u][5], acc[u][6], acc[u][7]);
+            }
+            __syncthreads();
+
+            // selection: wave w owns query rows 8w..8w+7; lane owns candidates 4*lane..+3
+            int gid[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                int c = lane * 4 + i;
+                gid[i] = (c >> 6) < ntv ? a.ids[(int64_t)(tile0 + tb) * kTile + c] : -1;
+            }
+            for (int rr = 0; rr < 8; ++rr) {
+                const int row = wave * 8 + rr;
+                if (meta[8 + row] < 0) continue;
+                u64 *L = lists + row * KP;
+                const u64 thr = L[k - 1];
+                const float4 d4 = *(const float4 *)&dist[row * kCT + lane * 4];
+                const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
+                u64 key[4], bal[4];
+                int tot = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    float s = METRIC == LIRA_METRIC_IP ? -dv[i] : dv[i];
+                    key[i] = make_key(s, gid[i]);
+                    bal[i] = __ballot(key[i] < thr);
+                    tot += popc64(bal[i]);
+                }
+                if (tot == 0) continue;
+                u64 *sc = scratch + wave * kCT;
+                int base = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    if ((bal[i] >> lane) & 1ull) sc[base + mbcnt64(bal[i])] = key[i];
+                    base += popc64(bal[i]);
+                }
+                __builtin_amdgcn_wave_barrier();
+                u64 lst[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) lst[r] = L[r * 64 + lane];
+                for (int b0 = 0; b0 < tot; b0 += 64) {
+                    u64 bk = (b0 + lane < tot) ? sc[b0 + lane] : kEmptyKey;
+                    wave_merge_batch<R>(lst, bk);
+                }
+#pragma unroll
+                for (int r = 0; r < R; ++r) L[r * 64 + lane] = lst[r];
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+
+        // emit: each wave writes the k best of its own rows
+        for (int rr = 0; rr < 8; ++rr) {
+            const int row = wave * 8 + rr;
+            const int pair = meta[8 + row];
+            if (pair < 0) continue;
+            u64 *dst = a.partial + ((int64_t)pair * a.nch_max + ch) * k;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                int e = r * 64 + lane;
+                if (e < k) dst[e] = lists[row * KP + e];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+struct MergeArgs {
+    const u64 *partial;
+    const int32_t *probe, *nch, *list_size;
+    float *D;
+    int64_t *I;
+    int64_t *ncand;
+    int64_t nq;
+    int n_lists, nprobe, k, nch_max, metric, dedup, per_partition;
+};
+
+__device__ __forceinline__ void emit_key(u64 key, int metric, float *D, int64_t *I) {
+    if (key == kEmptyKey) {
+        *D = metric == LIRA_METRIC_IP ? -__builtin_inff() : __builtin_inff();
+        *I = -1;
+    } else {
+        float s = key_score(key);
+        *D = metric == LIRA_METRIC_IP ? -s : s;
+        *I = key_gid(key);
+    }
+}
+
+// Append the k keys of one partial list to the wave's batch, merging full batches.
+template <int R>
+__device__ __forceinline__ void merge_list(u64 (&lst)[R], u64 &batch, int &bc, const u64 *src,
+                                           int k) {
+    const int lane = lane_id();
+    for (int e0 = 0; e0 < k; e0 += 64) {
+        int n = min(64, k - e0);
+        if (bc + n > 64) {
+            u64 thr = wave_list_at<R>(lst, 64 * R - 1);
+            if (__ballot(batch < thr)) wave_merge_batch<R>(lst, batch);
+            batch = kEmptyKey;
+            bc = 0;
+        }
+        if (lane >= bc && lane < bc + n) batch = src[e0 + lane - bc];
+        bc += n;
+    }
+}
+
+template <int R>
+__device__ __forceinline__ void flush_batch(u64 (&lst)[R], u64 &batch, int &bc) {
+    if (bc) {
+        u64 thr = wave_list_at<R>(lst, 64 * R - 1);
+        if (__ballot(batch < thr)) wave_merge_batch<R>(lst, batch);
+    }
+    batch = kEmptyKey;
+    bc = 0;
+}
+
+// Write the first k keys of a sorted list, optionally skipping repeated keys
+// (a gid replicated across probed buckets has the same key in each).
+template <int R>
+__device__ __forceinline__ void emit_list(const u64 (&lst)[R], int k, int dedup, int metric,
+                                          float *D, int64_t *I) {
+    const int lane = lane_id();
+    int outpos = 0;
+    u64 prev_last = kEmptyKey;
+    bool have_prev = false;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        u64 up = shfl64(lst[r], lane == 0 ? 0 : lane - 1);
+        u64 prev = lane == 0 ? prev_last : up;
+        bool has_prev = lane == 0 ? have_prev : true;
+        bool keep = lst[r] != kEmptyKey && !(dedup && has_prev && prev == lst[r]);
+        u64 bal = __ballot(keep);
+        int pos = outpos + mbcnt64(bal);
+        if (keep && pos < k) emit_key(lst[r], metric, D + pos, I + pos);
+        outpos += popc64(bal);
+        prev_last = shfl64(lst[r], 63);
+        have_prev = true;
+    }
+    for (int e = outpos + lane; e < k; e += 64) emit_key(kEmptyKey, metric, D + e, I + e);
+}
+
+template <int R>
+__global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= a.nq) return;
+    const int k = a.k;
+    const int32_t *prow = a.probe + q * a.nprobe;
+    int64_t ncand = 0;
+    if (a.per_partition) {
+        for (int s = 0; s < a.nprobe; ++s) {
+            int p = prow[s];
+            u64 lst[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) lst[r] = kEmptyKey;
+            if (p >= 0 && p < a.n_lists) {
+                ncand += a.list_size[p];
+                u64 batch = kEmptyKey;
+                int bc = 0;
+                for (int c = 0; c < a.nch[p]; ++c)
+                    merge_list<R>(lst, batch, bc,
+                                  a.partial + ((q * a.nprobe + s) * (int64_t)a.nch_max + c) * k, k);
+                flush_batch<R>(lst, batch, bc);
+            }
+            int64_t o = (q * a.nprobe + s) * (int64_t)k;
+            emit_list<R>(lst, k, 0, a.metric, a.D + o, a.I + o);
+        }
+    } else {
+        u64 lst[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) lst[r] = kEmptyKey;
+        u64 batch = kEmptyKey;
+        int bc = 0;
+        for (int s = 0; s < a.nprobe; ++s) {
+            int p = prow[s];
+            if (p < 0 || p >= a.n_lists) continue;
+            ncand += a.list_size[p];
+            for (int c = 0; c < a.nch[p]; ++c)
+                merge_list<R>(lst, batch, bc,
+                              a.partial + ((q * a.nprobe + s) * (int64_t)a.nch_max + c) * k, k);
+        }
+        flush_batch<R>(lst, batch, bc);
+        emit_list<R>(lst, k, a.dedup, a.metric, a.D + q * k, a.I + q * k);
+    }
+    if (a.ncand && lane == 0) a.ncand[q] = ncand;
+}
+
+// ------------------------------------------------------------------ host side
+
+struct ScanPlan {
+    int bpc = 1, nch_max = 1, grid = 1;
+    size_t off_cnt, off_cursor, off_qoff, off_item, off_nch, off_head, off_qlist, off_partial,
+        total;
+};
+
+static int scan_r(int64_t k) { return k <= 64 ? 1 : k <= 128 ? 2 : 4; }
+
+static int merge_r(int64_t kp) {
+    return kp <= 64 ? 1 : kp <= 128 ? 2 : kp <= 256 ? 4 : kp <= 512 ? 8 : -1;
+}
+
+static int cu_count(int device) {
+    static int cached[64] = {0};
+    if (device < 0 || device >= 64) return 256;
+    if (!cached[device]) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+            v <= 0)
+            v = 256;
+        cached[device] = v;
+    }
+    return cached[device];
+}
+
+static ScanPlan make_plan(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k) {
+    ScanPlan pl;
+    const int64_t npairs = nq * nprobe;
+    const int ncu = cu_count(idx->device);
+    const int64_t target = 4LL * ncu;
+    const int64_t est_items = (npairs + kQT - 1) / kQT + std::min<int64_t>(idx->n_lists, npairs);
+    const int64_t max_blocks = std::max<int64_t>(1, (idx->max_list_tiles + kBlockTiles - 1) / kBlockTiles);
+    if (est_items >= target) {
+        pl.bpc = (int)max_blocks;
+    } else {
+        int64_t split = (target + est_items - 1) / std::max<int64_t>(1, est_items);
+        pl.bpc = (int)std::max<int64_t>(1, (max_blocks + split - 1) / split);
+    }
+    pl.nch_max = (int)((max_blocks + pl.bpc - 1) / pl.bpc);
+    const int occ = scan_r(k) >= 4 ? 1 : 2;
+    pl.grid = ncu * occ;
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        size_t at = o;
+        o += (bytes + 255) & ~size_t(255);
+        return at;
+    };
+    const size_t nl = (size_t)idx->n_lists;
+    pl.off_cnt = take(nl * 4);
+    pl.off_cursor = take(nl * 4);
+    pl.off_head = take(16);
+    pl.off_qoff = take((nl + 1) * 4);
+    pl.off_item = take((nl + 1) * 4);
+    pl.off_nch = take(nl * 4);
+    pl.off_qlist = take((size_t)npairs * 4);
+    pl.off_partial = take((size_t)npairs * pl.nch_max * (size_t)k * 8);
+    pl.total = o;
+    return pl;
+}
+
+template <int R, int M>
+static void launch_scan(const ScanArgs &a, int grid, hipStream_t st) {
+    hipLaunchKernelGGL((k_scan<R, M>), dim3(grid), dim3(kScanThreads), ScanSmem<R>::kTotal, st, a);
+}
+
+template <int R>
+static void launch_merge(const MergeArgs &a, hipStream_t st) {
+    hipLaunchKernelGGL((k_merge<R>), dim3((unsigned)((a.nq + 3) / 4)), dim3(256), 0, st, a);
+}
+
+static bool g_attr_done[3][2] = {{false}};
+
+template <int R, int M>
+static hipError_t set_smem_attr() {
+    return hipFuncSetAttribute((const void *)k_scan<R, M>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               ScanSmem<R>::kTotal);
+}
+
+static hipError_t ensure_attrs(int R, int M) {
+    int ri = R == 1 ? 0 : R == 2 ? 1 : 2;
+    if (g_attr_done[ri][M]) return hipSuccess;
+    hipError_t e = hipSuccess;
+    if (R == 1) e = M ? set_smem_attr<1, 1>() : set_smem_attr<1, 0>();
+    if (R == 2) e = M ? set_smem_attr<2, 1>() : set_smem_attr<2, 0>();
+    if (R == 4) e = M ? set_smem_attr<4, 1>() : set_smem_attr<4, 0>();
+    if (e == hipSuccess) g_attr_done[ri][M] = true;
+    return e;
+}
+
+int scan_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k,
+                        size_t *bytes) {
+    ScanPlan pl = make_plan(idx, nq, nprobe, k);
+    *bytes = pl.total;
+    return LIRA_OK;
+}
+
+int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe, int64_t nprobe,
+              int64_t k, unsigned flags, float *out_D, int64_t *out_I, int64_t *out_ncand,
+              void *ws, size_t ws_bytes, hipStream_t st) {
+    const bool dedup = (flags & LIRA_SCAN_DEDUP) != 0;
+    const bool per_part = (flags & LIRA_SCAN_PER_PARTITION) != 0;
+    const int R = scan_r(k);
+    int64_t kpm = std::max<int64_t>(64, per_part ? k : (dedup ? k * std::max(1, idx->max_replicas) : k));
+    int Rm = merge_r(kpm);
+    if (Rm < 0)
+        return fail(LIRA_EUNSUPPORTED,
+                    "k * max_replicas = " + std::to_string(k * idx->max_replicas) +
+                        " exceeds the 512-key merge list");
+    if (nq == 0) return LIRA_OK;
+    ScanPlan pl = make_plan(idx, nq, nprobe, k);
+    if (nq * nprobe > INT32_MAX) return fail(LIRA_EUNSUPPORTED, "nq * nprobe_max must be < 2^31");
+    if (!ws) {
+        if (idx->ws_bytes < pl.total) {
+            if (idx->ws) hipFree(idx->ws);
+            idx->ws = nullptr;
+            idx->ws_bytes = 0;
+            LIRA_HIP_TRY(hipMalloc(&idx->ws, pl.total));
+            idx->ws_bytes = pl.total;
+        }
+        ws = idx->ws;
+    } else if (ws_bytes < pl.total) {
+        return fail(LIRA_EINVAL, "workspace too small: need " + std::to_string(pl.total) + " bytes");
+    }
+    char *w = (char *)ws;
+    int32_t *cnt = (int32_t *)(w + pl.off_cnt);
+    int32_t *cursor = (int32_t *)(w + pl.off_cursor);
+    int32_t *head = (int32_t *)(w + pl.off_head);
+    int32_t *qoff = (int32_t *)(w + pl.off_qoff);
+    int32_t *item_off = (int32_t *)(w + pl.off_item);
+    int32_t *nch = (int32_t *)(w + pl.off_nch);
+    int32_t *qlist = (int32_t *)(w + pl.off_qlist);
+    u64 *partial = (u64 *)(w + pl.off_partial);
+
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    if (idx->profiling) {
+        while (idx->ev_pool.size() < idx->ev_used + 4) {
+            hipEvent_t e;
+            LIRA_HIP_TRY(hipEventCreate(&e));
+            idx->ev_pool.push_back(e);
+        }
+        for (int i = 0; i < 4; ++i) ev[i] = idx->ev_pool[idx->ev_used + i];
+        idx->ev_used += 4;
+        LIRA_HIP_TRY(hipEventRecord(ev[0], st));
+    }
+    // cnt, cursor and head are contiguous at the start of the workspace
+    LIRA_HIP_TRY(hipMemsetAsync(w, 0, pl.off_qoff, st));
+    const int64_t npairs = nq * nprobe;
+    const int nl = (int)idx->n_lists;
+    const int eg = (int)std::min<int64_t>(4096, (npairs + 255) / 256);
+    hipLaunchKernelGGL(k_count, dim3(eg), dim3(256), 0, st, probe, npairs, nl, cnt, idx->err);
+    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, pl.bpc, qoff,
+                       item_off, nch, head);
+    hipLaunchKernelGGL(k_fill, dim3(eg), dim3(256), 0, st, probe, npairs, nl, qoff, cursor, qlist);
+
+    ScanArgs a;
+    a.Q = q;
+    a.X = idx->X;
+    a.ids = idx->ids;
+    a.tile_off = idx->tile_off;
+    a.cnt = cnt;
+    a.qoff = qoff;
+    a.qlist = qlist;
+    a.item_off = item_off;
+    a.nch = nch;
+    a.head = head;
+    a.partial = partial;
+    a.d = idx->d;
+    a.dpad = idx->dpad;
+    a.n_lists = nl;
+    a.nprobe = (int)nprobe;
+    a.k = (int)k;
+    a.bpc = pl.bpc;
+    a.nch_max = pl.nch_max;
+    LIRA_HIP_TRY(ensure_attrs(R, idx->metric));
+    if (ev[1]) LIRA_HIP_TRY(hipEventRecord(ev[1], st));
+    if (idx->metric == LIRA_METRIC_L2) {
+        if (R == 1) launch_scan<1, LIRA_METRIC_L2>(a, pl.grid, st);
+        else if (R == 2) launch_scan<2, LIRA_METRIC_L2>(a, pl.grid, st);
+        else launch_scan<4, LIRA_METRIC_L2>(a, pl.grid, st);
+    } else {
+        if (R == 1) launch_scan<1, LIRA_METRIC_IP>(a, pl.grid, st);
+        else if (R == 2) launch_scan<2, LIRA_METRIC_IP>(a, pl.grid, st);
+        else launch_scan<4, LIRA_METRIC_IP>(a, pl.grid, st);
+    }
+    LIRA_HIP_TRY(hipGetLastError());
+    if (ev[2]) LIRA_HIP_TRY(hipEventRecord(ev[2], st));
+
+    MergeArgs m;
+    m.partial = partial;
+    m.probe = probe;
+    m.nch = nch;
+    m.list_size = idx->list_size;
+    m.D = out_D;
+    m.I = out_I;
+    m.ncand = out_ncand;
+    m.nq = nq;
+    m.n_lists = nl;
+    m.nprobe = (int)nprobe;
+    m.k = (int)k;
+    m.nch_max = pl.nch_max;
+    m.metric = idx->metric;
+    m.dedup = dedup ? 1 : 0;
+    m.per_partition = per_part ? 1 : 0;
+    switch (Rm) {
+        case 1: launch_merge<1>(m, st); break;
+        case 2: launch_merge<2>(m, st); break;
+        case 4: launch_merge<4>(m, st); break;
+        default: launch_merge<8>(m, st); break;
+    }
+    LIRA_HIP_TRY(hipGetLastError());
+    if (ev[3]) LIRA_HIP_TRY(hipEventRecord(ev[3], st));
+    return LIRA_OK;
+}
+
+}  // namespace lira

@@ -1,0 +1,286 @@
+"""Device-resident partitioned index: the MI355X replacement for search.cpp's
+``std::vector<Bucket>`` (search.cpp:273-276, 366-404) and for the per-bucket
+faiss flat indexes of ``create_flat_indexes`` (utils.py:407-422).
+
+All compute goes through liblira_hip.so (``_lib``); PyTorch only owns device
+memory and streams.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import LiraError
+
+METRICS = {"L2": _lib.LIRA_METRIC_L2, "inner_product": _lib.LIRA_METRIC_IP}
+
+
+def normalize_metric(metric: str) -> str:
+    """Metric names as LIRA_smallscale.py:62-66 / search.cpp:362-364 accept them."""
+    m = (metric or "L2").lower()
+    if m in ("l2", "euclidean", "euclidean_distance"):
+        return "L2"
+    if m in ("ip", "inner_product", "dot", "dot_product"):
+        return "inner_product"
+    raise ValueError(f"unknown metric {metric!r}: expected 'L2' or 'inner_product'")
+
+
+def _dev(t: torch.Tensor, dtype, device) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        t = torch.from_numpy(np.ascontiguousarray(t))
+    return t.to(device=device, dtype=dtype).contiguous()
+
+
+def build_csr(data_2_bkt: torch.Tensor, n_bkt: int):
+    """Inverted lists from a (N, n_mul) bucket assignment, -1 = empty slot.
+
+    Same semantics as search.cpp:366-385: every non-negative bucket id of row i
+    pushes i; each list is sorted ascending and de-duplicated.  Runs on the
+    tensor's device.  Returns (offsets int64 host numpy (n_bkt+1), ids int32
+    tensor, max_replicas int).
+    """
+    if data_2_bkt.dim() == 1:
+        data_2_bkt = data_2_bkt[:, None]
+    n, n_mul = data_2_bkt.shape
+    flat = data_2_bkt.reshape(-1).to(torch.int64)
+    if flat.numel() and int(flat.max()) >= n_bkt:
+        raise LiraError("bucket id out of range.")  # search.cpp:375-377
+    rows = torch.arange(n, device=flat.device, dtype=torch.int64).repeat_interleave(n_mul)
+    valid = flat >= 0
+    key = torch.unique(flat[valid] * max(n, 1) + rows[valid])  # sorted (bucket, row), unique
+    b = key // max(n, 1)
+    ids = (key - b * max(n, 1)).to(torch.int32)
+    counts = torch.bincount(b, minlength=n_bkt)
+    offsets = torch.zeros(n_bkt + 1, dtype=torch.int64, device=flat.device)
+    offsets[1:] = torch.cumsum(counts, 0)
+    max_rep = int(torch.bincount(ids.to(torch.int64), minlength=1).max()) if ids.numel() else 1
+    return offsets.cpu().numpy(), ids, max(1, max_rep)
+
+
+class PartitionedIndex:
+    """Inverted lists of fp32 vectors on one GPU, searched by the HIP scan.
+
+    Parameters mirror search.cpp's Args (search.cpp:18-31): d, metric
+    ("L2" | "inner_product").
+    """
+
+    def __init__(self, d: int, metric: str = "L2", device: int | torch.device | None = None):
+        self.d = int(d)
+        self.metric = normalize_metric(metric)
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = torch.device("cuda", device if isinstance(device, int) else device.index)
+        h = ctypes.c_void_p()
+        _lib.call("lira_index_create", self.device.index, self.d, METRICS[self.metric],
+                  ctypes.byref(h))
+        self._h = h
+        self.n_lists = 0
+        self.ntotal = 0
+        self.list_sizes = np.zeros(0, dtype=np.int64)
+        self.max_replicas = 1
+
+    # ------------------------------------------------------------- lifetime
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.load().lira_index_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    # ---------------------------------------------------------------- build
+    def add_lists(self, offsets, ids: torch.Tensor, x: torch.Tensor, max_replicas: int = 1):
+        """Load inverted lists: bucket b = rows ids[offsets[b]:offsets[b+1]] of x."""
+        offsets = np.ascontiguousarray(np.asarray(offsets, dtype=np.int64))
+        ids = _dev(ids, torch.int32, self.device)
+        x = _dev(x, torch.float32, self.device)
+        if x.dim() != 2 or x.shape[1] != self.d:
+            raise ValueError(f"x must be (n, {self.d})")
+        n_lists = offsets.shape[0] - 1
+        with torch.cuda.device(self.device):
+            _lib.call("lira_index_add_partitions", self._h, n_lists,
+                      offsets.ctypes.data_as(ctypes.c_void_p), _lib.ptr(ids), _lib.ptr(x),
+                      x.shape[0], int(max_replicas), _lib.stream_ptr())
+        self.n_lists = n_lists
+        self.list_sizes = np.diff(offsets)
+        self.ntotal = int(offsets[-1])
+        self.max_replicas = int(max_replicas)
+        return self
+
+    @classmethod
+    def from_assignment(cls, x_d, data_2_bkt, n_bkt: int, metric: str = "L2", device=None):
+        """search.cpp:366-404: lists from data_2_bkt (N, n_mul) over base vectors x_d."""
+        idx = cls(x_d.shape[1], metric, device)
+        d2b = _dev(data_2_bkt, torch.int32, idx.device)
+        offsets, ids, rep = build_csr(d2b, n_bkt)
+        idx.add_lists(offsets, ids, x_d, rep)
+        return idx
+
+    @classmethod
+    def from_cluster_ids(cls, x_d, cluster_ids, metric: str = "L2", device=None):
+        """From LIRA's ``cluster_ids`` (list of per-bucket id lists, utils.py:327-329)."""
+        sizes = np.array([len(c) for c in cluster_ids], dtype=np.int64)
+        offsets = np.zeros(len(cluster_ids) + 1, dtype=np.int64)
+        offsets[1:] = np.cumsum(sizes)
+        flat = np.concatenate([np.asarray(c, dtype=np.int64) for c in cluster_ids]) \
+            if offsets[-1] else np.zeros(0, dtype=np.int64)
+        rep = int(np.bincount(flat).max()) if flat.size else 1
+        idx = cls(x_d.shape[1], metric, device)
+        idx.add_lists(offsets, torch.from_numpy(flat.astype(np.int32)), x_d, rep)
+        return idx
+
+    # --------------------------------------------------------------- search
+    def search(self, q: torch.Tensor, probe: torch.Tensor, k: int, dedup: bool = True,
+               per_partition: bool = False, out=None, stream=None):
+        """Scan the probed lists of every query; exact top-k.
+
+        q (nq, d) fp32, probe (nq, nprobe_max) int32 (-1 = unused slot).
+        Returns (D, I, ncand) device tensors: D/I (nq, k) -- or
+        (nq, nprobe_max, k) with per_partition -- and ncand (nq,) int64, the
+        candidates scanned per query (search.cpp's cmp_for_query).
+        """
+        q = _dev(q, torch.float32, self.device)
+        probe = _dev(probe, torch.int32, self.device)
+        if probe.dim() == 1:
+            probe = probe[:, None]
+        nq = q.shape[0]
+        if q.dim() != 2 or q.shape[1] != self.d:
+            raise ValueError(f"queries must be (nq, {self.d})")
+        if probe.shape[0] != nq:
+            raise ValueError("probe must have one row per query")
+        npm = probe.shape[1]
+        shape = (nq, npm, k) if per_partition else (nq, k)
+        if out is None:
+            D = torch.empty(shape, dtype=torch.float32, device=self.device)
+            I = torch.empty(shape, dtype=torch.int64, device=self.device)
+            ncand = torch.empty(nq, dtype=torch.int64, device=self.device)
+        else:
+            D, I, ncand = out
+        flags = (_lib.LIRA_SCAN_DEDUP if dedup else 0) | \
+            (_lib.LIRA_SCAN_PER_PARTITION if per_partition else 0)
+        with torch.cuda.device(self.device):
+            _lib.call("lira_scan_topk", self._h, _lib.ptr(q), nq, _lib.ptr(probe), npm, int(k),
+                      flags, _lib.ptr(D), _lib.ptr(I), _lib.ptr(ncand), None, 0,
+                      _lib.stream_ptr(stream))
+        return D, I, ncand
+
+    def check(self, stream=None):
+        """Raise if the last searches hit an out-of-range probe id."""
+        with torch.cuda.device(self.device):
+            _lib.call("lira_index_check", self._h, _lib.stream_ptr(stream))
+
+    def set_profiling(self, enable: bool = True):
+        """Record HIP events around the scan kernels (see profile_read)."""
+        _lib.call("lira_index_set_profiling", self._h, int(bool(enable)))
+
+    def profile_read(self) -> dict:
+        """Summed kernel milliseconds since the last read: plan / scan / merge."""
+        a, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        n = ctypes.c_int64()
+        with torch.cuda.device(self.device):
+            _lib.call("lira_index_profile_read", self._h, ctypes.byref(a), ctypes.byref(b),
+                      ctypes.byref(c), ctypes.byref(n))
+        return {"plan_ms": a.value, "scan_ms": b.value, "merge_ms": c.value, "calls": n.value}
+
+    def memory_bytes(self) -> int:
+        v = ctypes.c_int64()
+        _lib.call("lira_index_memory", self._h, ctypes.byref(v))
+        return v.value
+
+
+# ------------------------------------------------------------------ ranking
+def centroid_dist(q: torch.Tensor, centroids: torch.Tensor, scaler_mean=None, scaler_scale=None,
+                  out=None, stream=None) -> torch.Tensor:
+    """Exact query->centroid Euclidean distances (search.cpp:220-250), (nq, B)."""
+    q = _dev(q, torch.float32, q.device if isinstance(q, torch.Tensor) and q.is_cuda else "cuda")
+    dev = q.device
+    c = _dev(centroids, torch.float32, dev)
+    nq, d = q.shape
+    nb = c.shape[0]
+    if c.shape[1] != d:
+        raise ValueError("centroid dim != query dim")
+    m = _dev(scaler_mean, torch.float32, dev) if scaler_mean is not None else None
+    s = _dev(scaler_scale, torch.float32, dev) if scaler_scale is not None else None
+    if (m is None) != (s is None):
+        raise ValueError("scaler_mean and scaler_scale go together")
+    if m is not None and (m.numel() != nb or s.numel() != nb):
+        raise LiraError("Scaler dimension mismatch.")  # search.cpp:242-244
+    out = torch.empty((nq, nb), dtype=torch.float32, device=dev) if out is None else out
+    with torch.cuda.device(dev):
+        _lib.call("lira_centroid_dist", _lib.ptr(q), nq, _lib.ptr(c), nb, d, _lib.ptr(m),
+                  _lib.ptr(s), _lib.ptr(out), _lib.stream_ptr(stream))
+    return out
+
+
+def centroid_gemm(q: torch.Tensor, centroids: torch.Tensor, stream=None):
+    """MFMA ranking GEMM: approximate squared distances (nq, B) + error bound (nq,)."""
+    dev = q.device
+    c = _dev(centroids, torch.float32, dev)
+    q = _dev(q, torch.float32, dev)
+    nq, d = q.shape
+    nb = c.shape[0]
+    A = torch.empty((nq, nb), dtype=torch.float32, device=dev)
+    err = torch.empty(nq, dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        _lib.call("lira_centroid_gemm", _lib.ptr(q), nq, _lib.ptr(c), nb, d, _lib.ptr(A),
+                  _lib.ptr(err), _lib.stream_ptr(stream))
+    return A, err
+
+
+class RankWorkspace:
+    """Pre-sized workspace for rank_nearest (keeps the call graph-capturable)."""
+
+    def __init__(self, nq: int, nb: int, device):
+        sz = ctypes.c_size_t()
+        _lib.call("lira_rank_workspace_size", nq, nb, ctypes.byref(sz))
+        self.buf = torch.empty(max(1, sz.value), dtype=torch.uint8, device=device)
+        self.nq, self.nb = nq, nb
+
+
+def rank_nearest(q: torch.Tensor, centroids: torch.Tensor, nprobe: int, out=None,
+                 workspace: RankWorkspace | None = None, stream=None) -> torch.Tensor:
+    """IVF probe list: the nprobe nearest centroids by the exact search.cpp
+    distance (ties -> smaller bucket), via the MFMA GEMM + exact re-check."""
+    dev = q.device
+    c = _dev(centroids, torch.float32, dev)
+    q = _dev(q, torch.float32, dev)
+    nq, d = q.shape
+    nb = c.shape[0]
+    out = torch.empty((nq, nprobe), dtype=torch.int32, device=dev) if out is None else out
+    if workspace is None or workspace.nq < nq or workspace.nb != nb:
+        workspace = RankWorkspace(nq, nb, dev)
+    with torch.cuda.device(dev):
+        _lib.call("lira_rank_nearest", _lib.ptr(q), nq, _lib.ptr(c), nb, d, int(nprobe),
+                  _lib.ptr(out), _lib.ptr(workspace.buf), workspace.buf.numel(),
+                  _lib.stream_ptr(stream))
+    return out
+
+
+def select_probes(scores: torch.Tensor, mode: str, max_probe: int, threshold: float = 0.0,
+                  stream=None):
+    """Probe lists from an (n, B) score matrix.
+
+    mode "nearest": max_probe smallest; "ge": score >= threshold with argmax
+    fallback (search.cpp:447-466); "gt": score > threshold (LIRA_smallscale.py:206).
+    Returns (probe (n, max_probe) int32 -1 padded, nprobe (n,) int32).
+    """
+    modes = {"nearest": _lib.LIRA_PROBE_NEAREST, "ge": _lib.LIRA_PROBE_THRESHOLD_GE,
+             "gt": _lib.LIRA_PROBE_THRESHOLD_GT}
+    s = _dev(scores, torch.float32, scores.device)
+    n, nb = s.shape
+    probe = torch.empty((n, max_probe), dtype=torch.int32, device=s.device)
+    cnt = torch.empty(n, dtype=torch.int32, device=s.device)
+    with torch.cuda.device(s.device):
+        _lib.call("lira_select_probes", _lib.ptr(s), n, nb, modes[mode], float(threshold),
+                  int(max_probe), _lib.ptr(probe), _lib.ptr(cnt), _lib.stream_ptr(stream))
+    return probe, cnt
