@@ -66,6 +66,38 @@ __device__ __forceinline__ u64 wave_sort64(u64 v) {
     return v;
 }
 
+// Full ascending bitonic sort of 64*R keys held R per lane (element r*64+lane).
+template <int R>
+__device__ __forceinline__ void wave_sort(u64 (&v)[R]) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int size = 2; size <= 64 * R; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            if (stride >= 64) {  // partner in another register of the same lane
+                const int rs = stride >> 6;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if ((r & rs) == 0) {
+                        const bool asc = ((r * 64) & size) == 0;
+                        u64 a = v[r], b = v[r | rs];
+                        v[r] = asc ? kmin(a, b) : kmax(a, b);
+                        v[r | rs] = asc ? kmax(a, b) : kmin(a, b);
+                    }
+                }
+            } else {
+                const bool lower = (lane & stride) == 0;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const bool asc = ((r * 64 + lane) & size) == 0;
+                    u64 o = shfl_xor64(v[r], stride);
+                    v[r] = (lower == asc) ? kmin(v[r], o) : kmax(v[r], o);
+                }
+            }
+        }
+    }
+}
+
 // Sort a bitonic sequence of 64*R keys ascending.
 template <int R>
 __device__ __forceinline__ void wave_bitonic_merge(u64 (&v)[R]) {

@@ -14,10 +14,16 @@
 // (Makefile: -ffp-contract=off), i.e. bit-identical to search.cpp:253-269.
 // Top-k is exact over (score, gid) keys (lira_device.hpp).
 //
-// Kernels (one call = 5 launches, all stream-ordered, no host sync):
-//   k_count  pairs per bucket                  (probe histogram)
+// Selection.  Per query row the workgroup keeps its k best keys (LDS, sorted)
+// and a 64-key survivor buffer.  The first 256-candidate block of an item is
+// bitonic-sorted outright; afterwards a candidate below the row's k-th key is
+// appended to the buffer (ballot compaction), and only a full buffer costs a
+// sort + merge -- ~2.4 merges per row per 15.6k candidates instead of ~23.
+//
+// Kernels (one call = 5 launches + 1 memset, stream-ordered, no host sync):
+//   k_count  pairs per bucket (LDS histogram, one atomic per bucket per block)
 //   k_plan   offsets, chunks per bucket, work-item prefix (one workgroup)
-//   k_fill   bucket -> pair lists
+//   k_fill   bucket -> pair lists (LDS ranks, one reservation per bucket per block)
 //   k_scan   persistent; pulls work items from an atomic head
 //   k_merge  per query: merge the per-(slot, chunk) top-k lists, dedup, emit
 #include <algorithm>
@@ -32,6 +38,8 @@ static constexpr int kQT = 32;        // queries per work item
 static constexpr int kBlockTiles = 4; // tiles per candidate block
 static constexpr int kCT = kBlockTiles * kTile;  // 256 candidates per block
 static constexpr int kScanThreads = 256;
+static constexpr int kHistMax = 16384;  // buckets the LDS histograms handle
+static constexpr int kPairsPerBlock = 4096;
 
 struct ScanArgs {
     const float *Q;       // (nq, d)
@@ -45,16 +53,30 @@ struct ScanArgs {
     int n_lists, nprobe, k, bpc, nch_max;
 };
 
-__global__ void k_count(const int32_t *probe, int64_t npairs, int n_lists, int32_t *cnt,
-                        int32_t *err) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < npairs;
-         i += (int64_t)gridDim.x * blockDim.x) {
+// Pairs per bucket.  With an LDS histogram each block issues one global
+// atomic per touched bucket (80k pairs on 64 buckets: 128 us -> ~5 us).
+__global__ __launch_bounds__(256) void k_count(const int32_t *probe, int64_t npairs, int n_lists,
+                                               int32_t *cnt, int32_t *err) {
+    extern __shared__ int32_t hist[];
+    const bool lds = n_lists <= kHistMax;
+    const int64_t s = (int64_t)blockIdx.x * kPairsPerBlock;
+    const int64_t e = min<int64_t>(npairs, s + kPairsPerBlock);
+    if (lds) {
+        for (int b = threadIdx.x; b < n_lists; b += blockDim.x) hist[b] = 0;
+        __syncthreads();
+    }
+    for (int64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
         int p = probe[i];
         if (p >= n_lists) {
             atomicOr(err, 1);
             continue;
         }
-        if (p >= 0) atomicAdd(&cnt[p], 1);
+        if (p >= 0) atomicAdd(lds ? &hist[p] : &cnt[p], 1);
+    }
+    if (lds) {
+        __syncthreads();
+        for (int b = threadIdx.x; b < n_lists; b += blockDim.x)
+            if (hist[b]) atomicAdd(&cnt[b], hist[b]);
     }
 }
 
@@ -107,43 +129,89 @@ __global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t
     }
 }
 
-__global__ void k_fill(const int32_t *probe, int64_t npairs, int n_lists, const int32_t *qoff,
-                       int32_t *cursor, int32_t *qlist) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < npairs;
-         i += (int64_t)gridDim.x * blockDim.x) {
+// bucket -> pair ids.  Each block reserves its slice of every bucket once
+// (global atomic), then places its pairs by LDS-atomic rank.  The order inside
+// a bucket's list is arbitrary; results do not depend on it.
+__global__ __launch_bounds__(256) void k_fill(const int32_t *probe, int64_t npairs, int n_lists,
+                                              const int32_t *qoff, int32_t *cursor,
+                                              int32_t *qlist) {
+    extern __shared__ int32_t sh[];
+    const bool lds = n_lists <= kHistMax / 2;
+    int32_t *hist = sh, *base = sh + (lds ? n_lists : 0);
+    const int64_t s = (int64_t)blockIdx.x * kPairsPerBlock;
+    const int64_t e = min<int64_t>(npairs, s + kPairsPerBlock);
+    if (!lds) {
+        for (int64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
+            int p = probe[i];
+            if (p < 0 || p >= n_lists) continue;
+            qlist[qoff[p] + atomicAdd(&cursor[p], 1)] = (int32_t)i;
+        }
+        return;
+    }
+    for (int b = threadIdx.x; b < n_lists; b += blockDim.x) hist[b] = 0;
+    __syncthreads();
+    for (int64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
+        int p = probe[i];
+        if (p >= 0 && p < n_lists) atomicAdd(&hist[p], 1);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < n_lists; b += blockDim.x) {
+        base[b] = hist[b] ? qoff[b] + atomicAdd(&cursor[b], hist[b]) : 0;
+        hist[b] = 0;
+    }
+    __syncthreads();
+    for (int64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
         int p = probe[i];
         if (p < 0 || p >= n_lists) continue;
-        int pos = atomicAdd(&cursor[p], 1);
-        qlist[qoff[p] + pos] = (int32_t)i;
+        qlist[base[p] + atomicAdd(&hist[p], 1)] = (int32_t)i;
     }
 }
 
-// LDS carve (bytes): X staging / distance tile, Q staging, per-query lists,
-// per-wave compaction scratch, item metadata.
-template <int R>
+// LDS carve (bytes): X staging / distance tile, Q staging, per-query top-k
+// lists (k keys each), per-query survivor buffers, item metadata.
 struct ScanSmem {
     static constexpr int kX = kBlockTiles * kDimChunk * kTile * 4;  // 32 KiB
     static constexpr int kQ = kDimChunk * kQT * 4;                  // 4 KiB
-    static constexpr int kLists = kQT * 64 * R * 8;
-    static constexpr int kScratch = (kScanThreads / 64) * kCT * 8;
-    static constexpr int kMeta = 64 * 4;
-    static constexpr int kTotal = kX + kQ + kLists + kScratch + kMeta;
+    static constexpr int kBuf = kQT * 64 * 8;                       // 16 KiB
+    static constexpr int kMeta = 128 * 4;
+    static int lists(int k) { return kQT * k * 8; }
+    static int total(int k) { return kX + kQ + kBuf + kMeta + lists(k); }
 };
+
+// Merge a row's survivor buffer (n keys) into its sorted k-list in LDS.
+template <int R>
+__device__ __forceinline__ void flush_row(u64 *L, const u64 *buf, int n, int k) {
+    const int lane = lane_id();
+    u64 lst[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        int e = r * 64 + lane;
+        lst[r] = e < k ? L[e] : kEmptyKey;
+    }
+    u64 batch = lane < n ? buf[lane] : kEmptyKey;
+    wave_merge_batch<R>(lst, batch);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        int e = r * 64 + lane;
+        if (e < k) L[e] = lst[r];
+    }
+    __builtin_amdgcn_wave_barrier();
+}
 
 template <int R, int METRIC>
 __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    typedef ScanSmem<R> S;
-    float *Xs = (float *)smem;                       // [4][32][64] (alias: dist [32][256])
-    float *Qs = (float *)(smem + S::kX);             // [32 dims][32 queries]
-    u64 *lists = (u64 *)(smem + S::kX + S::kQ);      // [32][64R]
-    u64 *scratch = (u64 *)(smem + S::kX + S::kQ + S::kLists);
-    int *meta = (int *)(smem + S::kX + S::kQ + S::kLists + S::kScratch);
-    constexpr int KP = 64 * R;
+    typedef ScanSmem S;
+    float *Xs = (float *)smem;                                   // [4][32][64] (alias: dist [32][256])
+    float *Qs = (float *)(smem + S::kX);                         // [32 dims][32 queries]
+    u64 *bufs = (u64 *)(smem + S::kX + S::kQ);                   // [32][64]
+    int *meta = (int *)(smem + S::kX + S::kQ + S::kBuf);         // [0..8) item, [8..40) pairs, [64..96) buffer fill
+    u64 *lists = (u64 *)(smem + S::kX + S::kQ + S::kBuf + S::kMeta);  // [32][k]
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int tx = tid & 31, ty = tid >> 5;
     const int k = a.k;
+    const float4 *Xg = (const float4 *)a.X;
 
     for (;;) {
         if (tid == 0) {
@@ -173,8 +241,10 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a) {
         const int p = meta[1], qb = meta[2], ch = meta[3];
         const int q0 = qb * kQT;
         const int nqb_valid = min(kQT, a.cnt[p] - q0);
-        if (tid < kQT) meta[8 + tid] = tid < nqb_valid ? a.qlist[a.qoff[p] + q0 + tid] : -1;
-        for (int i = tid; i < kQT * KP; i += kScanThreads) lists[i] = kEmptyKey;
+        if (tid < kQT) {
+            meta[8 + tid] = tid < nqb_valid ? a.qlist[a.qoff[p] + q0 + tid] : -1;
+            meta[64 + tid] = 0;
+        }
         __syncthreads();
 
         const int tile0 = a.tile_off[p];
@@ -186,8 +256,34 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a) {
         const int spair = meta[8 + sq];
         const float *qrow = spair >= 0 ? a.Q + (int64_t)(spair / a.nprobe) * a.d : nullptr;
 
+        // register-staged prefetch of one (block, dim-chunk): 8 float4 of X, 4 floats of Q
+        float4 px[8];
+        float pq[4];
+        auto fetch = [&](int tb, int jc) {
+            const int ntv = min(kBlockTiles, tb_end - tb);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int f = i * kScanThreads + tid;
+                const int t = f >> 9, off = f & 511;
+                px[i] = t < ntv ? Xg[((int64_t)(tile0 + tb + t) * a.dpad + jc) * (kTile / 4) + off]
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int j = jc + sj + u;
+                pq[u] = (qrow && j < a.d) ? qrow[j] : 0.0f;
+            }
+        };
+        fetch(tb_begin, 0);
+
         for (int tb = tb_begin; tb < tb_end; tb += kBlockTiles) {
             const int ntv = min(kBlockTiles, tb_end - tb);
+            int gid[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int c = lane * 4 + i;
+                gid[i] = (c >> 6) < ntv ? a.ids[(int64_t)(tile0 + tb) * kTile + c] : -1;
+            }
             float acc[4][8];
 #pragma unroll
             for (int u = 0; u < 4; ++u)
@@ -195,31 +291,25 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a) {
                 for (int v = 0; v < 8; ++v) acc[u][v] = 0.0f;
 
             for (int jc = 0; jc < a.dpad; jc += kDimChunk) {
-                __syncthreads();
-                {   // X chunk: tile t rows jc..jc+31 = 8 KiB contiguous in HBM and in LDS
-                    const float4 *src = (const float4 *)a.X;
-                    float4 *dst = (float4 *)Xs;
+                __syncthreads();  // previous compute / selection done with Xs, Qs
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        int f = i * kScanThreads + tid;
-                        int t = f >> 9, off = f & 511;
-                        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                        if (t < ntv)
-                            v = src[((int64_t)(tile0 + tb + t) * a.dpad + jc) * (kTile / 4) + off];
-                        dst[f] = v;
+                for (int i = 0; i < 8; ++i) ((float4 *)Xs)[i * kScanThreads + tid] = px[i];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) Qs[(sj + u) * kQT + sq] = pq[u];
+                __syncthreads();
+                {   // prefetch the next chunk (this block or the next) under the compute
+                    int njc = jc + kDimChunk, ntb = tb;
+                    if (njc >= a.dpad) {
+                        njc = 0;
+                        ntb = tb + kBlockTiles;
                     }
+                    if (ntb < tb_end) fetch(ntb, njc);
                 }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    int j = jc + sj + u;
-                    Qs[(sj + u) * kQT + sq] = (qrow && j < a.d) ? qrow[j] : 0.0f;
-                }
-                __syncthreads();
 #pragma unroll 4
                 for (int j = 0; j < kDimChunk; ++j) {
-                    float4 q4 = *(const float4 *)&Qs[j * kQT + ty * 4];
-                    float4 xa = *(const float4 *)&Xs[(tx >> 4) * (kDimChunk * kTile) + j * kTile + (tx & 15) * 4];
-                    float4 xb = *(const float4 *)&Xs[(2 + (tx >> 4)) * (kDimChunk * kTile) + j * kTile + (tx & 15) * 4];
+                    const float4 q4 = *(const float4 *)&Qs[j * kQT + ty * 4];
+                    const float4 xa = *(const float4 *)&Xs[(tx >> 4) * (kDimChunk * kTile) + j * kTile + (tx & 15) * 4];
+                    const float4 xb = *(const float4 *)&Xs[(2 + (tx >> 4)) * (kDimChunk * kTile) + j * kTile + (tx & 15) * 4];
                     const float qv[4] = {q4.x, q4.y, q4.z, q4.w};
                     const float xv[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
 #pragma unroll
@@ -247,61 +337,72 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a) {
             __syncthreads();
 
             // selection: wave w owns query rows 8w..8w+7; lane owns candidates 4*lane..+3
-            int gid[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                int c = lane * 4 + i;
-                gid[i] = (c >> 6) < ntv ? a.ids[(int64_t)(tile0 + tb) * kTile + c] : -1;
-            }
+            const bool first = tb == tb_begin;
             for (int rr = 0; rr < 8; ++rr) {
                 const int row = wave * 8 + rr;
                 if (meta[8 + row] < 0) continue;
-                u64 *L = lists + row * KP;
-                const u64 thr = L[k - 1];
+                u64 *L = lists + row * k;
                 const float4 d4 = *(const float4 *)&dist[row * kCT + lane * 4];
                 const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
-                u64 key[4], bal[4];
-                int tot = 0;
+                u64 key[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    key[i] = make_key(METRIC == LIRA_METRIC_IP ? -dv[i] : dv[i], gid[i]);
+                if (first) {  // the item's first 256 candidates: sort them outright
+                    wave_sort<4>(key);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int e = r * 64 + lane;
+                        if (e < k) L[e] = key[r];
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    continue;
+                }
+                const u64 thr = L[k - 1];
+                u64 bal[4];
+                int pos[4], tot = 0;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    float s = METRIC == LIRA_METRIC_IP ? -dv[i] : dv[i];
-                    key[i] = make_key(s, gid[i]);
                     bal[i] = __ballot(key[i] < thr);
+                    pos[i] = tot + mbcnt64(bal[i]);
                     tot += popc64(bal[i]);
                 }
                 if (tot == 0) continue;
-                u64 *sc = scratch + wave * kCT;
-                int base = 0;
+                u64 *buf = bufs + row * 64;
+                int bc = meta[64 + row];
+                int consumed = 0;
+                for (;;) {
+                    const int room = 64 - bc;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if ((bal[i] >> lane) & 1ull) sc[base + mbcnt64(bal[i])] = key[i];
-                    base += popc64(bal[i]);
+                    for (int i = 0; i < 4; ++i) {
+                        const int rel = pos[i] - consumed;
+                        if (((bal[i] >> lane) & 1ull) && rel >= 0 && rel < room) buf[bc + rel] = key[i];
+                    }
+                    const int placed = min(room, tot - consumed);
+                    bc += placed;
+                    consumed += placed;
+                    __builtin_amdgcn_wave_barrier();
+                    if (bc == 64) {
+                        flush_row<R>(L, buf, 64, k);
+                        bc = 0;
+                    }
+                    if (consumed >= tot) break;
                 }
-                __builtin_amdgcn_wave_barrier();
-                u64 lst[R];
-#pragma unroll
-                for (int r = 0; r < R; ++r) lst[r] = L[r * 64 + lane];
-                for (int b0 = 0; b0 < tot; b0 += 64) {
-                    u64 bk = (b0 + lane < tot) ? sc[b0 + lane] : kEmptyKey;
-                    wave_merge_batch<R>(lst, bk);
-                }
-#pragma unroll
-                for (int r = 0; r < R; ++r) L[r * 64 + lane] = lst[r];
+                if (lane == 0) meta[64 + row] = bc;
                 __builtin_amdgcn_wave_barrier();
             }
         }
 
-        // emit: each wave writes the k best of its own rows
+        // flush the survivor buffers, emit the k best of each row
         for (int rr = 0; rr < 8; ++rr) {
             const int row = wave * 8 + rr;
             const int pair = meta[8 + row];
             if (pair < 0) continue;
+            u64 *L = lists + row * k;
+            const int bc = meta[64 + row];
+            if (bc) flush_row<R>(L, bufs + row * 64, bc, k);
             u64 *dst = a.partial + ((int64_t)pair * a.nch_max + ch) * k;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                int e = r * 64 + lane;
-                if (e < k) dst[e] = lists[row * KP + e];
-            }
+            for (int e = lane; e < k; e += 64) dst[e] = L[e];
         }
         __syncthreads();
     }
@@ -427,10 +528,11 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
     if (a.ncand && lane == 0) a.ncand[q] = ncand;
 }
 
+
 // ------------------------------------------------------------------ host side
 
 struct ScanPlan {
-    int bpc = 1, nch_max = 1, grid = 1;
+    int bpc = 1, nch_max = 1, grid = 1, smem = 0;
     size_t off_cnt, off_cursor, off_qoff, off_item, off_nch, off_head, off_qlist, off_partial,
         total;
 };
@@ -468,7 +570,8 @@ static ScanPlan make_plan(const lira_index *idx, int64_t nq, int64_t nprobe, int
         pl.bpc = (int)std::max<int64_t>(1, (max_blocks + split - 1) / split);
     }
     pl.nch_max = (int)((max_blocks + pl.bpc - 1) / pl.bpc);
-    const int occ = scan_r(k) >= 4 ? 1 : 2;
+    pl.smem = ScanSmem::total((int)k);
+    const int occ = std::max(1, std::min(2, (160 * 1024) / pl.smem));
     pl.grid = ncu * occ;
     size_t o = 0;
     auto take = [&](size_t bytes) {
@@ -490,32 +593,21 @@ static ScanPlan make_plan(const lira_index *idx, int64_t nq, int64_t nprobe, int
 }
 
 template <int R, int M>
-static void launch_scan(const ScanArgs &a, int grid, hipStream_t st) {
-    hipLaunchKernelGGL((k_scan<R, M>), dim3(grid), dim3(kScanThreads), ScanSmem<R>::kTotal, st, a);
+static hipError_t launch_scan(const ScanArgs &a, const ScanPlan &pl, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void *)k_scan<R, M>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_scan<R, M>), dim3(pl.grid), dim3(kScanThreads), pl.smem, st, a);
+    return hipGetLastError();
 }
 
 template <int R>
 static void launch_merge(const MergeArgs &a, hipStream_t st) {
     hipLaunchKernelGGL((k_merge<R>), dim3((unsigned)((a.nq + 3) / 4)), dim3(256), 0, st, a);
-}
-
-static bool g_attr_done[3][2] = {{false}};
-
-template <int R, int M>
-static hipError_t set_smem_attr() {
-    return hipFuncSetAttribute((const void *)k_scan<R, M>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               ScanSmem<R>::kTotal);
-}
-
-static hipError_t ensure_attrs(int R, int M) {
-    int ri = R == 1 ? 0 : R == 2 ? 1 : 2;
-    if (g_attr_done[ri][M]) return hipSuccess;
-    hipError_t e = hipSuccess;
-    if (R == 1) e = M ? set_smem_attr<1, 1>() : set_smem_attr<1, 0>();
-    if (R == 2) e = M ? set_smem_attr<2, 1>() : set_smem_attr<2, 0>();
-    if (R == 4) e = M ? set_smem_attr<4, 1>() : set_smem_attr<4, 0>();
-    if (e == hipSuccess) g_attr_done[ri][M] = true;
-    return e;
 }
 
 int scan_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k,
@@ -538,8 +630,8 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
                     "k * max_replicas = " + std::to_string(k * idx->max_replicas) +
                         " exceeds the 512-key merge list");
     if (nq == 0) return LIRA_OK;
-    ScanPlan pl = make_plan(idx, nq, nprobe, k);
     if (nq * nprobe > INT32_MAX) return fail(LIRA_EUNSUPPORTED, "nq * nprobe_max must be < 2^31");
+    ScanPlan pl = make_plan(idx, nq, nprobe, k);
     if (!ws) {
         if (idx->ws_bytes < pl.total) {
             if (idx->ws) hipFree(idx->ws);
@@ -577,11 +669,14 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
     LIRA_HIP_TRY(hipMemsetAsync(w, 0, pl.off_qoff, st));
     const int64_t npairs = nq * nprobe;
     const int nl = (int)idx->n_lists;
-    const int eg = (int)std::min<int64_t>(4096, (npairs + 255) / 256);
-    hipLaunchKernelGGL(k_count, dim3(eg), dim3(256), 0, st, probe, npairs, nl, cnt, idx->err);
+    const unsigned pg = (unsigned)((npairs + kPairsPerBlock - 1) / kPairsPerBlock);
+    const size_t hc = nl <= kHistMax ? (size_t)nl * 4 : 0;
+    const size_t hf = nl <= kHistMax / 2 ? (size_t)nl * 8 : 0;
+    hipLaunchKernelGGL(k_count, dim3(pg), dim3(256), hc, st, probe, npairs, nl, cnt, idx->err);
     hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, pl.bpc, qoff,
                        item_off, nch, head);
-    hipLaunchKernelGGL(k_fill, dim3(eg), dim3(256), 0, st, probe, npairs, nl, qoff, cursor, qlist);
+    hipLaunchKernelGGL(k_fill, dim3(pg), dim3(256), hf, st, probe, npairs, nl, qoff, cursor, qlist);
+    LIRA_HIP_TRY(hipGetLastError());
 
     ScanArgs a;
     a.Q = q;
@@ -602,18 +697,15 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
     a.k = (int)k;
     a.bpc = pl.bpc;
     a.nch_max = pl.nch_max;
-    LIRA_HIP_TRY(ensure_attrs(R, idx->metric));
     if (ev[1]) LIRA_HIP_TRY(hipEventRecord(ev[1], st));
-    if (idx->metric == LIRA_METRIC_L2) {
-        if (R == 1) launch_scan<1, LIRA_METRIC_L2>(a, pl.grid, st);
-        else if (R == 2) launch_scan<2, LIRA_METRIC_L2>(a, pl.grid, st);
-        else launch_scan<4, LIRA_METRIC_L2>(a, pl.grid, st);
-    } else {
-        if (R == 1) launch_scan<1, LIRA_METRIC_IP>(a, pl.grid, st);
-        else if (R == 2) launch_scan<2, LIRA_METRIC_IP>(a, pl.grid, st);
-        else launch_scan<4, LIRA_METRIC_IP>(a, pl.grid, st);
-    }
-    LIRA_HIP_TRY(hipGetLastError());
+    hipError_t e;
+    if (idx->metric == LIRA_METRIC_L2)
+        e = R == 1 ? launch_scan<1, LIRA_METRIC_L2>(a, pl, st)
+            : R == 2 ? launch_scan<2, LIRA_METRIC_L2>(a, pl, st) : launch_scan<4, LIRA_METRIC_L2>(a, pl, st);
+    else
+        e = R == 1 ? launch_scan<1, LIRA_METRIC_IP>(a, pl, st)
+            : R == 2 ? launch_scan<2, LIRA_METRIC_IP>(a, pl, st) : launch_scan<4, LIRA_METRIC_IP>(a, pl, st);
+    if (e != hipSuccess) return fail(LIRA_EHIP, std::string("k_scan launch: ") + hipGetErrorString(e));
     if (ev[2]) LIRA_HIP_TRY(hipEventRecord(ev[2], st));
 
     MergeArgs m;
