@@ -137,6 +137,91 @@ __device__ __forceinline__ void wave_merge_batch(u64 (&list)[R], u64 batch) {
     wave_bitonic_merge<R>(list);
 }
 
+// ---- half-wave networks: lanes 0-31 and 32-63 each hold an independent
+// sequence of 32*R keys, element e = r*32 + (lane & 31).  Both halves run the
+// same instructions, so two query rows are sorted/merged at once.
+template <int R>
+__device__ __forceinline__ void half_sort(u64 (&v)[R]) {
+    const int hl = lane_id() & 31;
+#pragma unroll
+    for (int size = 2; size <= 32 * R; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            if (stride >= 32) {
+                const int rs = stride >> 5;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if ((r & rs) == 0) {
+                        const bool asc = ((r * 32) & size) == 0;
+                        u64 a = v[r], b = v[r | rs];
+                        v[r] = asc ? kmin(a, b) : kmax(a, b);
+                        v[r | rs] = asc ? kmax(a, b) : kmin(a, b);
+                    }
+                }
+            } else {
+                const bool lower = (hl & stride) == 0;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const bool asc = ((r * 32 + hl) & size) == 0;
+                    u64 o = shfl_xor64(v[r], stride);
+                    v[r] = (lower == asc) ? kmin(v[r], o) : kmax(v[r], o);
+                }
+            }
+        }
+    }
+}
+
+template <int R>
+__device__ __forceinline__ void half_bitonic_merge(u64 (&v)[R]) {
+    const int hl = lane_id() & 31;
+#pragma unroll
+    for (int rs = R / 2; rs >= 1; rs >>= 1) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if ((r & rs) == 0) {
+                u64 a = v[r], b = v[r | rs];
+                v[r] = kmin(a, b);
+                v[r | rs] = kmax(a, b);
+            }
+        }
+    }
+#pragma unroll
+    for (int stride = 16; stride > 0; stride >>= 1) {
+        const bool lower = (hl & stride) == 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            u64 o = shfl_xor64(v[r], stride);
+            v[r] = lower ? kmin(v[r], o) : kmax(v[r], o);
+        }
+    }
+}
+
+// Per half: list (sorted, 32*R >= 64 keys) <- the 32*R smallest of list U batch,
+// batch = 64 keys in any order (2 per lane).
+template <int R>
+__device__ __forceinline__ void half_merge_batch(u64 (&list)[R], u64 (&batch)[2]) {
+    static_assert(R >= 2, "half-wave lists hold at least 64 keys");
+    const int lane = lane_id();
+    half_sort<2>(batch);
+    const int src = (lane & 32) | (31 - (lane & 31));
+    const u64 rev0 = shfl64(batch[1], src), rev1 = shfl64(batch[0], src);
+    list[R - 2] = kmin(list[R - 2], rev0);
+    list[R - 1] = kmin(list[R - 1], rev1);
+    half_bitonic_merge<R>(list);
+}
+
+// Per half: list (sorted, 32*R keys) <- the 32*R smallest of list U batch,
+// batch = 32 keys in any order (1 per lane).
+template <int R>
+__device__ __forceinline__ void half_merge_batch1(u64 (&list)[R], u64 batch) {
+    const int lane = lane_id();
+    u64 b[1] = {batch};
+    half_sort<1>(b);
+    const u64 rev = shfl64(b[0], (lane & 32) | (31 - (lane & 31)));
+    list[R - 1] = kmin(list[R - 1], rev);
+    half_bitonic_merge<R>(list);
+}
+
 // Broadcast list element e (compile-time-unknown) to the whole wave.
 template <int R>
 __device__ __forceinline__ u64 wave_list_at(const u64 (&list)[R], int e) {

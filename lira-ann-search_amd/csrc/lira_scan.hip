@@ -14,11 +14,18 @@
 // (Makefile: -ffp-contract=off), i.e. bit-identical to search.cpp:253-269.
 // Top-k is exact over (score, gid) keys (lira_device.hpp).
 //
+// Staging.  X tiles reach LDS by LDS-DMA (global_load_lds_dwordx4) into a
+// 2-deep ring: the next 16-dim chunk streams in while the current one is
+// consumed, and no registers hold in-flight tile data.
+//
 // Selection.  Per query row the workgroup keeps its k best keys (LDS, sorted)
-// and a 64-key survivor buffer.  The first 256-candidate block of an item is
-// bitonic-sorted outright; afterwards a candidate below the row's k-th key is
-// appended to the buffer (ballot compaction), and only a full buffer costs a
-// sort + merge -- ~2.4 merges per row per 15.6k candidates instead of ~23.
+// and a 32-key survivor buffer.  A row's 256 candidates of a block sit in one
+// half-wave (8 per lane), so selection runs from the accumulators with no
+// distance tile and no barrier: a candidate whose score passes
+// the row's k-th key is appended to the buffer (ballot compaction), and only
+// a full buffer costs a sort + merge, a few per row per 15.6k candidates
+// instead of ~23 for merge-on-every-survivor.  Lists start empty, so an
+// item's first block fills them through the same path (8 merges).
 //
 // Kernels (one call = 5 launches + 1 memset, stream-ordered, no host sync):
 //   k_count  pairs per bucket (LDS histogram, one atomic per bucket per block)
@@ -37,6 +44,7 @@ namespace lira {
 static constexpr int kQT = 32;        // queries per work item
 static constexpr int kBlockTiles = 4; // tiles per candidate block
 static constexpr int kCT = kBlockTiles * kTile;  // 256 candidates per block
+static_assert(kCT == 256, "selection assumes 8 candidates per lane of a half-wave");
 static constexpr int kScanThreads = 256;
 static constexpr int kHistMax = 16384;  // buckets the LDS histograms handle
 static constexpr int kPairsPerBlock = 4096;
@@ -167,51 +175,68 @@ __global__ __launch_bounds__(256) void k_fill(const int32_t *probe, int64_t npai
     }
 }
 
-// LDS carve (bytes): X staging / distance tile, Q staging, per-query top-k
-// lists (k keys each), per-query survivor buffers, item metadata.
+// LDS carve (bytes): a 2-deep ring of X chunks (4 tiles x 16 dims, filled by
+// LDS-DMA), a 2-deep ring of Q chunks, per-query survivor buffers (32 keys),
+// item metadata, per-query top-k lists (k keys).
+static constexpr int kDK = 16;       // dims per staged chunk
+static constexpr int kBufCap = 32;   // survivor buffer per query row (1 key per lane of a half-wave)
 struct ScanSmem {
-    static constexpr int kX = kBlockTiles * kDimChunk * kTile * 4;  // 32 KiB
-    static constexpr int kQ = kDimChunk * kQT * 4;                  // 4 KiB
-    static constexpr int kBuf = kQT * 64 * 8;                       // 16 KiB
+    static constexpr int kXChunk = kBlockTiles * kDK * kTile * 4;  // 16 KiB
+    static constexpr int kQChunk = kDK * kQT * 4;                  // 2 KiB
+    static constexpr int kX = 2 * kXChunk;
+    static constexpr int kQ = 2 * kQChunk;
+    static constexpr int kBuf = kQT * kBufCap * 8;                 // 8 KiB
     static constexpr int kMeta = 128 * 4;
     static int lists(int k) { return kQT * k * 8; }
     static int total(int k) { return kX + kQ + kBuf + kMeta + lists(k); }
 };
 
-// Merge a row's survivor buffer (n keys) into its sorted k-list in LDS.
-template <int R>
-__device__ __forceinline__ void flush_row(u64 *L, const u64 *buf, int n, int k) {
-    const int lane = lane_id();
-    u64 lst[R];
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+
+// Both halves of the wave merge their row's survivor buffer (n keys, per
+// half) into the row's sorted k-list in LDS.  Rows without a query
+// (row_ok false) merge nothing and store nothing.
+template <int RL>
+__device__ __forceinline__ void flush_rows(u64 *L, const u64 *buf, int n, int k, bool row_ok) {
+    const int hl = lane_id() & 31;
+    u64 lst[RL];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        int e = r * 64 + lane;
-        lst[r] = e < k ? L[e] : kEmptyKey;
+    for (int r = 0; r < RL; ++r) {
+        const int e = r * 32 + hl;
+        lst[r] = (row_ok && e < k) ? L[e] : kEmptyKey;
     }
-    u64 batch = lane < n ? buf[lane] : kEmptyKey;
-    wave_merge_batch<R>(lst, batch);
+    const u64 b = (row_ok && hl < n) ? buf[hl] : kEmptyKey;
+    half_merge_batch1<RL>(lst, b);
+    if (row_ok) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        int e = r * 64 + lane;
-        if (e < k) L[e] = lst[r];
+        for (int r = 0; r < RL; ++r) {
+            const int e = r * 32 + hl;
+            if (e < k) L[e] = lst[r];
+        }
     }
     __builtin_amdgcn_wave_barrier();
 }
 
-template <int R, int METRIC>
-__global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a) {
+// RL: half-wave list registers, 32*RL >= k.  OCC: workgroups per CU the
+// register budget is built for.
+template <int RL, int METRIC, int OCC>
+__global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     typedef ScanSmem S;
-    float *Xs = (float *)smem;                                   // [4][32][64] (alias: dist [32][256])
-    float *Qs = (float *)(smem + S::kX);                         // [32 dims][32 queries]
-    u64 *bufs = (u64 *)(smem + S::kX + S::kQ);                   // [32][64]
-    int *meta = (int *)(smem + S::kX + S::kQ + S::kBuf);         // [0..8) item, [8..40) pairs, [64..96) buffer fill
-    u64 *lists = (u64 *)(smem + S::kX + S::kQ + S::kBuf + S::kMeta);  // [32][k]
+    float *Xs = (float *)smem;                                   // [2][4 tiles][16 dims][64]
+    float *Qs = (float *)(smem + S::kX);                         // [2][16 dims][32 queries]
+    u64 *bufs = (u64 *)(smem + S::kX + S::kQ);                   // [32 rows][32]
+    int *meta = (int *)(smem + S::kX + S::kQ + S::kBuf);         // [0..4) item, [8..40) pairs, [64..96) buffer fill
+    u64 *lists = (u64 *)(smem + S::kX + S::kQ + S::kBuf + S::kMeta);  // [32 rows][k]
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int tx = tid & 31, ty = tid >> 5;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tx = tid & 31, ty = tid >> 5;  // ty = 2*wave + half
     const int k = a.k;
     const float4 *Xg = (const float4 *)a.X;
+    const int tstride = (int)a.dpad * (kTile / 4);  // float4 per tile
+    const int nchunk = (int)(a.dpad / kDK);
 
     for (;;) {
         if (tid == 0) {
@@ -245,44 +270,57 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a) {
             meta[8 + tid] = tid < nqb_valid ? a.qlist[a.qoff[p] + q0 + tid] : -1;
             meta[64 + tid] = 0;
         }
+        for (int i = tid; i < kQT * k; i += kScanThreads) lists[i] = kEmptyKey;
         __syncthreads();
 
         const int tile0 = a.tile_off[p];
         const int ntl = a.tile_off[p + 1] - tile0;
         const int tb_begin = ch * a.bpc * kBlockTiles;
         const int tb_end = min(ntl, tb_begin + a.bpc * kBlockTiles);
-        // query staged by this thread: slot sq, dims (tid&7)*4 .. +3 of each chunk
-        const int sq = tid >> 3, sj = (tid & 7) * 4;
+        // Q staging: thread stages query slot sq, dims jj, jj+1 of each chunk;
+        // rows without a query stage row 0 (their results are never kept)
+        const int sq = tid & 31, jj = (tid >> 5) * 2;
         const int spair = meta[8 + sq];
-        const float *qrow = spair >= 0 ? a.Q + (int64_t)(spair / a.nprobe) * a.d : nullptr;
+        const float *qrow = a.Q + (spair >= 0 ? (int64_t)(spair / a.nprobe) * a.d : 0);
+        const int dlast = (int)a.d - 1;
+        bool row_ok[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) row_ok[u] = meta[8 + ty * 4 + u] >= 0;
 
-        // register-staged prefetch of one (block, dim-chunk): 8 float4 of X, 4 floats of Q
-        float4 px[8];
-        float pq[4];
-        auto fetch = [&](int tb, int jc) {
+        // Stage chunk (tb, jc) into ring slot `slot`: X by LDS-DMA (wave w moves
+        // bytes [1 KiB*w, 1 KiB*(w+1)) of each tile's 4 KiB chunk; tiles past the
+        // block's end re-read its last valid tile, masked later by gid -1), and
+        // this thread's two Q values into registers.  Query dims past d stage 0
+        // (the index pads X with zeros there).
+        float pq[2];
+        auto stage = [&](int tb, int jc, int slot) {
             const int ntv = min(kBlockTiles, tb_end - tb);
+            const float4 *src = Xg + (int64_t)(tile0 + tb) * tstride + jc * (kTile / 4) + tid;
+            float *dst = Xs + slot * (kBlockTiles * kDK * kTile) + wave * 256;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int f = i * kScanThreads + tid;
-                const int t = f >> 9, off = f & 511;
-                px[i] = t < ntv ? Xg[((int64_t)(tile0 + tb + t) * a.dpad + jc) * (kTile / 4) + off]
-                                : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
+            for (int i = 0; i < kBlockTiles; ++i)
+                __builtin_amdgcn_global_load_lds((gbl_void_t *)(src + min(i, ntv - 1) * tstride),
+                                                 (lds_void_t *)(dst + i * (kDK * kTile)), 16, 0, 0);
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int j = jc + sj + u;
-                pq[u] = (qrow && j < a.d) ? qrow[j] : 0.0f;
+            for (int u = 0; u < 2; ++u) {
+                const int j = jc + jj + u;
+                const float v = qrow[min(j, dlast)];
+                pq[u] = j <= dlast ? v : 0.0f;
             }
         };
-        fetch(tb_begin, 0);
+        int slot = 0;
+        stage(tb_begin, 0, 0);
 
         for (int tb = tb_begin; tb < tb_end; tb += kBlockTiles) {
             const int ntv = min(kBlockTiles, tb_end - tb);
-            int gid[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int c = lane * 4 + i;
-                gid[i] = (c >> 6) < ntv ? a.ids[(int64_t)(tile0 + tb) * kTile + c] : -1;
+            // this lane's candidates: c = tx*4+v (v<4) and 128+tx*4+(v-4)
+            int gid[8];
+            {
+                const int64_t base = (int64_t)(tile0 + tb) * kTile + tx * 4;
+                const int4 g0 = (tx >> 4) < ntv ? *(const int4 *)&a.ids[base] : make_int4(-1, -1, -1, -1);
+                const int4 g1 = 2 + (tx >> 4) < ntv ? *(const int4 *)&a.ids[base + 128] : make_int4(-1, -1, -1, -1);
+                gid[0] = g0.x; gid[1] = g0.y; gid[2] = g0.z; gid[3] = g0.w;
+                gid[4] = g1.x; gid[5] = g1.y; gid[6] = g1.z; gid[7] = g1.w;
             }
             float acc[4][8];
 #pragma unroll
@@ -290,26 +328,26 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a) {
 #pragma unroll
                 for (int v = 0; v < 8; ++v) acc[u][v] = 0.0f;
 
-            for (int jc = 0; jc < a.dpad; jc += kDimChunk) {
-                __syncthreads();  // previous compute / selection done with Xs, Qs
+            for (int c = 0; c < nchunk; ++c) {
+                float *Qc = Qs + slot * (kDK * kQT);
 #pragma unroll
-                for (int i = 0; i < 8; ++i) ((float4 *)Xs)[i * kScanThreads + tid] = px[i];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) Qs[(sj + u) * kQT + sq] = pq[u];
-                __syncthreads();
-                {   // prefetch the next chunk (this block or the next) under the compute
-                    int njc = jc + kDimChunk, ntb = tb;
-                    if (njc >= a.dpad) {
+                for (int u = 0; u < 2; ++u) Qc[(jj + u) * kQT + sq] = pq[u];
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA for the slot landed
+                __syncthreads();  // every wave's DMA landed; every wave is done with the other slot
+                {   // stage the next chunk (this block or the next) into the other slot
+                    int njc = (c + 1) * kDK, ntb = tb;
+                    if (c + 1 == nchunk) {
                         njc = 0;
                         ntb = tb + kBlockTiles;
                     }
-                    if (ntb < tb_end) fetch(ntb, njc);
+                    if (ntb < tb_end) stage(ntb, njc, slot ^ 1);
                 }
+                const float *Xc = Xs + slot * (kBlockTiles * kDK * kTile);
 #pragma unroll 4
-                for (int j = 0; j < kDimChunk; ++j) {
-                    const float4 q4 = *(const float4 *)&Qs[j * kQT + ty * 4];
-                    const float4 xa = *(const float4 *)&Xs[(tx >> 4) * (kDimChunk * kTile) + j * kTile + (tx & 15) * 4];
-                    const float4 xb = *(const float4 *)&Xs[(2 + (tx >> 4)) * (kDimChunk * kTile) + j * kTile + (tx & 15) * 4];
+                for (int j = 0; j < kDK; ++j) {
+                    const float4 q4 = *(const float4 *)&Qc[j * kQT + ty * 4];
+                    const float4 xa = *(const float4 *)&Xc[(tx >> 4) * (kDK * kTile) + j * kTile + (tx & 15) * 4];
+                    const float4 xb = *(const float4 *)&Xc[(2 + (tx >> 4)) * (kDK * kTile) + j * kTile + (tx & 15) * 4];
                     const float qv[4] = {q4.x, q4.y, q4.z, q4.w};
                     const float xv[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
 #pragma unroll
@@ -324,85 +362,76 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a) {
                             }
                         }
                 }
+                slot ^= 1;
             }
-            __syncthreads();
-            float *dist = Xs;  // [32 queries][256 candidates]
+
+            // ---- selection, per wave and per half-wave, straight from registers.
+            // Half h of wave w owns rows (2w+h)*4+u; lane tx holds 8 candidates of each.
+            // Fast filter: fp32 score against each row's k-th key (+inf while the
+            // list is not full, -inf for rows without a query).
+            float thf[4];
+            bool any = false;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                *(float4 *)&dist[(ty * 4 + u) * kCT + tx * 4] =
-                    make_float4(acc[u][0], acc[u][1], acc[u][2], acc[u][3]);
-                *(float4 *)&dist[(ty * 4 + u) * kCT + 128 + tx * 4] =
-                    make_float4(acc[u][4], acc[u][5], acc[u][6], acc[u][7]);
+                const u64 t = lists[(ty * 4 + u) * k + k - 1];
+                thf[u] = !row_ok[u] ? -__builtin_inff() : t == kEmptyKey ? __builtin_inff() : key_score(t);
+#pragma unroll
+                for (int v = 0; v < 8; ++v)
+                    any |= (METRIC == LIRA_METRIC_IP ? -acc[u][v] : acc[u][v]) <= thf[u];
             }
-            __syncthreads();
-
-            // selection: wave w owns query rows 8w..8w+7; lane owns candidates 4*lane..+3
-            const bool first = tb == tb_begin;
-            for (int rr = 0; rr < 8; ++rr) {
-                const int row = wave * 8 + rr;
-                if (meta[8 + row] < 0) continue;
-                u64 *L = lists + row * k;
-                const float4 d4 = *(const float4 *)&dist[row * kCT + lane * 4];
-                const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
-                u64 key[4];
+            if (!__any(any)) continue;
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    key[i] = make_key(METRIC == LIRA_METRIC_IP ? -dv[i] : dv[i], gid[i]);
-                if (first) {  // the item's first 256 candidates: sort them outright
-                    wave_sort<4>(key);
+            for (int u = 0; u < 4; ++u) {
+                const int row = ty * 4 + u;
+                const u64 thr = row_ok[u] ? lists[row * k + k - 1] : 0ull;
+                uint32_t hb[8];  // this half's survivor masks
+                int pos[8], tot = 0;
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int e = r * 64 + lane;
-                        if (e < k) L[e] = key[r];
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    continue;
+                for (int v = 0; v < 8; ++v) {
+                    const u64 key = make_key(METRIC == LIRA_METRIC_IP ? -acc[u][v] : acc[u][v], gid[v]);
+                    const u64 b = __ballot(key < thr);
+                    hb[v] = (lane & 32) ? (uint32_t)(b >> 32) : (uint32_t)b;
+                    pos[v] = tot + __popc(hb[v] & ((1u << tx) - 1u));
+                    tot += __popc(hb[v]);
                 }
-                const u64 thr = L[k - 1];
-                u64 bal[4];
-                int pos[4], tot = 0;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    bal[i] = __ballot(key[i] < thr);
-                    pos[i] = tot + mbcnt64(bal[i]);
-                    tot += popc64(bal[i]);
-                }
-                if (tot == 0) continue;
-                u64 *buf = bufs + row * 64;
+                if (!__any(tot > 0)) continue;
+                u64 *buf = bufs + row * kBufCap;
                 int bc = meta[64 + row];
                 int consumed = 0;
                 for (;;) {
-                    const int room = 64 - bc;
+                    const int room = kBufCap - bc;
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int rel = pos[i] - consumed;
-                        if (((bal[i] >> lane) & 1ull) && rel >= 0 && rel < room) buf[bc + rel] = key[i];
+                    for (int v = 0; v < 8; ++v) {
+                        const int rel = pos[v] - consumed;
+                        if (((hb[v] >> tx) & 1u) && rel >= 0 && rel < room)
+                            buf[bc + rel] = make_key(METRIC == LIRA_METRIC_IP ? -acc[u][v] : acc[u][v], gid[v]);
                     }
                     const int placed = min(room, tot - consumed);
                     bc += placed;
                     consumed += placed;
                     __builtin_amdgcn_wave_barrier();
-                    if (bc == 64) {
-                        flush_row<R>(L, buf, 64, k);
+                    if (__any(bc == kBufCap)) {  // a full buffer: merge both halves' buffers
+                        flush_rows<RL>(lists + row * k, buf, bc, k, row_ok[u]);
                         bc = 0;
                     }
-                    if (consumed >= tot) break;
+                    if (!__any(consumed < tot)) break;
                 }
-                if (lane == 0) meta[64 + row] = bc;
+                if (tx == 0) meta[64 + row] = bc;
                 __builtin_amdgcn_wave_barrier();
             }
         }
 
         // flush the survivor buffers, emit the k best of each row
-        for (int rr = 0; rr < 8; ++rr) {
-            const int row = wave * 8 + rr;
-            const int pair = meta[8 + row];
-            if (pair < 0) continue;
-            u64 *L = lists + row * k;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int row = ty * 4 + u;
             const int bc = meta[64 + row];
-            if (bc) flush_row<R>(L, bufs + row * 64, bc, k);
-            u64 *dst = a.partial + ((int64_t)pair * a.nch_max + ch) * k;
-            for (int e = lane; e < k; e += 64) dst[e] = L[e];
+            if (__any(bc > 0)) flush_rows<RL>(lists + row * k, bufs + row * kBufCap, bc, k, row_ok[u]);
+            const int pair = meta[8 + row];
+            if (pair >= 0) {
+                u64 *dst = a.partial + ((int64_t)pair * a.nch_max + ch) * k;
+                for (int e = tx; e < k; e += 32) dst[e] = lists[row * k + e];
+            }
         }
         __syncthreads();
     }
@@ -537,7 +566,13 @@ struct ScanPlan {
         total;
 };
 
-static int scan_r(int64_t k) { return k <= 64 ? 1 : k <= 128 ? 2 : 4; }
+// half-wave list registers for k, and the workgroups per CU each variant is built for
+static int scan_rl(int64_t k) { return k <= 32 ? 1 : k <= 64 ? 2 : k <= 128 ? 4 : 8; }
+template <int RL>
+struct ScanOcc {
+    static constexpr int value = RL == 1 ? 3 : RL == 8 ? 1 : 2;
+};
+static int scan_occ(int rl) { return rl == 1 ? 3 : rl == 8 ? 1 : 2; }
 
 static int merge_r(int64_t kp) {
     return kp <= 64 ? 1 : kp <= 128 ? 2 : kp <= 256 ? 4 : kp <= 512 ? 8 : -1;
@@ -571,7 +606,7 @@ static ScanPlan make_plan(const lira_index *idx, int64_t nq, int64_t nprobe, int
     }
     pl.nch_max = (int)((max_blocks + pl.bpc - 1) / pl.bpc);
     pl.smem = ScanSmem::total((int)k);
-    const int occ = std::max(1, std::min(2, (160 * 1024) / pl.smem));
+    const int occ = std::max(1, std::min(scan_occ(scan_rl(k)), (160 * 1024) / pl.smem));
     pl.grid = ncu * occ;
     size_t o = 0;
     auto take = [&](size_t bytes) {
@@ -592,16 +627,17 @@ static ScanPlan make_plan(const lira_index *idx, int64_t nq, int64_t nprobe, int
     return pl;
 }
 
-template <int R, int M>
+template <int RL, int M>
 static hipError_t launch_scan(const ScanArgs &a, const ScanPlan &pl, hipStream_t st) {
+    constexpr int OCC = ScanOcc<RL>::value;
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void *)k_scan<R, M>,
+        hipError_t e = hipFuncSetAttribute((const void *)k_scan<RL, M, OCC>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((k_scan<R, M>), dim3(pl.grid), dim3(kScanThreads), pl.smem, st, a);
+    hipLaunchKernelGGL((k_scan<RL, M, OCC>), dim3(pl.grid), dim3(kScanThreads), pl.smem, st, a);
     return hipGetLastError();
 }
 
@@ -622,7 +658,7 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
               void *ws, size_t ws_bytes, hipStream_t st) {
     const bool dedup = (flags & LIRA_SCAN_DEDUP) != 0;
     const bool per_part = (flags & LIRA_SCAN_PER_PARTITION) != 0;
-    const int R = scan_r(k);
+    const int RL = scan_rl(k);
     int64_t kpm = std::max<int64_t>(64, per_part ? k : (dedup ? k * std::max(1, idx->max_replicas) : k));
     int Rm = merge_r(kpm);
     if (Rm < 0)
@@ -700,11 +736,13 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
     if (ev[1]) LIRA_HIP_TRY(hipEventRecord(ev[1], st));
     hipError_t e;
     if (idx->metric == LIRA_METRIC_L2)
-        e = R == 1 ? launch_scan<1, LIRA_METRIC_L2>(a, pl, st)
-            : R == 2 ? launch_scan<2, LIRA_METRIC_L2>(a, pl, st) : launch_scan<4, LIRA_METRIC_L2>(a, pl, st);
+        e = RL == 1 ? launch_scan<1, LIRA_METRIC_L2>(a, pl, st)
+            : RL == 2 ? launch_scan<2, LIRA_METRIC_L2>(a, pl, st)
+            : RL == 4 ? launch_scan<4, LIRA_METRIC_L2>(a, pl, st) : launch_scan<8, LIRA_METRIC_L2>(a, pl, st);
     else
-        e = R == 1 ? launch_scan<1, LIRA_METRIC_IP>(a, pl, st)
-            : R == 2 ? launch_scan<2, LIRA_METRIC_IP>(a, pl, st) : launch_scan<4, LIRA_METRIC_IP>(a, pl, st);
+        e = RL == 1 ? launch_scan<1, LIRA_METRIC_IP>(a, pl, st)
+            : RL == 2 ? launch_scan<2, LIRA_METRIC_IP>(a, pl, st)
+            : RL == 4 ? launch_scan<4, LIRA_METRIC_IP>(a, pl, st) : launch_scan<8, LIRA_METRIC_IP>(a, pl, st);
     if (e != hipSuccess) return fail(LIRA_EHIP, std::string("k_scan launch: ") + hipGetErrorString(e));
     if (ev[2]) LIRA_HIP_TRY(hipEventRecord(ev[2], st));
 
