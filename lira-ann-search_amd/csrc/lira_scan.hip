@@ -343,24 +343,52 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
                     if (ntb < tb_end) stage(ntb, njc, slot ^ 1);
                 }
                 const float *Xc = Xs + slot * (kBlockTiles * kDK * kTile);
-#pragma unroll 4
+                const float *qp = Qc + ty * 4;
+                const float *xpa = Xc + (tx >> 4) * (kDK * kTile) + (tx & 15) * 4;
+                const float *xpb = xpa + 2 * (kDK * kTile);
+                // software-pipelined: LDS reads of dim j+1 are in flight while dim j
+                // runs as three phases of 16 independent packed ops (sub, mul, add),
+                // pinned by sched_barrier so no dependent pair sits back to back
+                float4 q4 = *(const float4 *)qp, xa = *(const float4 *)xpa, xb = *(const float4 *)xpb;
+#pragma unroll 2
                 for (int j = 0; j < kDK; ++j) {
-                    const float4 q4 = *(const float4 *)&Qc[j * kQT + ty * 4];
-                    const float4 xa = *(const float4 *)&Xc[(tx >> 4) * (kDK * kTile) + j * kTile + (tx & 15) * 4];
-                    const float4 xb = *(const float4 *)&Xc[(2 + (tx >> 4)) * (kDK * kTile) + j * kTile + (tx & 15) * 4];
                     const float qv[4] = {q4.x, q4.y, q4.z, q4.w};
                     const float xv[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+                    // (at j = 15 this reads past the chunk, still inside the
+                    // workgroup's LDS allocation; the values are never used)
+                    q4 = *(const float4 *)(qp + (j + 1) * kQT);
+                    xa = *(const float4 *)(xpa + (j + 1) * kTile);
+                    xb = *(const float4 *)(xpb + (j + 1) * kTile);
+                    if (METRIC == LIRA_METRIC_L2) {
+                        float df[4][8];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u)
+                        for (int u = 0; u < 4; ++u)
 #pragma unroll
-                        for (int v = 0; v < 8; ++v) {
-                            if (METRIC == LIRA_METRIC_L2) {
-                                float df = qv[u] - xv[v];
-                                acc[u][v] = acc[u][v] + df * df;
-                            } else {
-                                acc[u][v] = acc[u][v] + qv[u] * xv[v];
-                            }
-                        }
+                            for (int v = 0; v < 8; ++v) df[u][v] = qv[u] - xv[v];
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+#pragma unroll
+                            for (int v = 0; v < 8; ++v) df[u][v] = df[u][v] * df[u][v];
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+#pragma unroll
+                            for (int v = 0; v < 8; ++v) acc[u][v] = acc[u][v] + df[u][v];
+                        __builtin_amdgcn_sched_barrier(0);
+                    } else {
+                        float pr[4][8];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+#pragma unroll
+                            for (int v = 0; v < 8; ++v) pr[u][v] = qv[u] * xv[v];
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+#pragma unroll
+                            for (int v = 0; v < 8; ++v) acc[u][v] = acc[u][v] + pr[u][v];
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
                 }
                 slot ^= 1;
             }
