@@ -1,0 +1,155 @@
+"""End-to-end artifact search on the GPU: the search.cpp pipeline
+(search.cpp:278-558) with the hot path on the HIP module.
+
+Per query batch (search.cpp:421-514, batched instead of one query at a time):
+    exact query->centroid distances + standardisation   lira_centroid_dist
+    probing MLP scores                                    PyTorch-ROCm (probing.py)
+    probe buckets with score >= thr, argmax fallback      lira_select_probes
+    scan the probed buckets, exact top-k                  lira_scan_topk
+then recall@k against the ground truth (search.cpp:519-528) and QPS =
+queries / wall time of the pipeline (search.cpp:540), per threshold of the
+sweep (search.cpp:413; integer steps instead of float accumulation).
+
+CLI, with search.cpp's flags (search.cpp:18-82):
+    python -m lira_amd.search --dataset sift --data_path /data/vector_datasets \
+        --artifacts_dir DIR --prefix NAME --k 10 --metric L2 [--t_min --t_max --t_step]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+from .index import PartitionedIndex, build_csr, centroid_dist, normalize_metric, select_probes
+from .io import load_artifacts, read_fvecs, read_ivecs
+from .probing import probe_scores
+
+
+def recall_at_k(I: np.ndarray, gt: np.ndarray, k: int) -> np.ndarray:
+    """search.cpp:519-528: |gt[:k] intersect found| / k for each query."""
+    out = np.empty(I.shape[0])
+    for i in range(I.shape[0]):
+        found = set(int(v) for v in I[i] if v >= 0)
+        out[i] = sum(int(g) in found for g in gt[i, :k]) / k
+    return out
+
+
+def thresholds(t_min: float, t_max: float, t_step: float, cpp_exact: bool = True) -> np.ndarray:
+    """The sweep of search.cpp:413.
+
+    cpp_exact (default) reproduces the reference's fp32 accumulation
+    `for (float thr = t_min; thr <= t_max + 1e-6f; thr += t_step)` value for
+    value, so a score equal to a threshold probes exactly as search.cpp does;
+    otherwise thresholds are t_min + i * t_step in float64, rounded once.
+    """
+    if not cpp_exact:
+        n = int(np.floor((t_max - t_min) / t_step + 1e-6)) + 1
+        return (t_min + t_step * np.arange(max(0, n))).astype(np.float32)
+    out = []
+    thr, lim, step = np.float32(t_min), np.float32(np.float32(t_max) + np.float32(1e-6)), np.float32(t_step)
+    while thr <= lim and len(out) < 1_000_000:
+        out.append(thr)
+        thr = np.float32(thr + step)
+    return np.array(out, dtype=np.float32)
+
+
+class SearchEngine:
+    """search.cpp's loaded state: inverted lists, centroids, scaler, model."""
+
+    def __init__(self, artifacts, metric: str = "L2", device: int = 0, dedup: bool = False):
+        if isinstance(artifacts, str):
+            artifacts = load_artifacts(artifacts, device=f"cuda:{device}")
+        self.device = torch.device("cuda", device)
+        self.metric = normalize_metric(metric)
+        dev = self.device
+        self.centroids = torch.from_numpy(artifacts["centroids"]).to(dev)
+        self.n_bkt, self.d = self.centroids.shape
+        self.mean = torch.from_numpy(artifacts["scaler_mean"]).to(dev)
+        self.scale = torch.from_numpy(artifacts["scaler_scale"]).to(dev)
+        self.model = artifacts["model"].to(dev).eval()
+        x = torch.from_numpy(np.ascontiguousarray(artifacts["x_d"])).to(dev)
+        d2b = torch.from_numpy(np.ascontiguousarray(artifacts["data_2_bkt"])).to(dev)
+        offsets, ids, rep = build_csr(d2b, self.n_bkt)
+        self.index = PartitionedIndex(self.d, self.metric, device)
+        self.index.add_lists(offsets, ids, x, rep)
+        del x
+        self.dedup = dedup  # search.cpp keeps replicated gids twice (Appendix A)
+
+    def scores(self, q: torch.Tensor) -> torch.Tensor:
+        dist = centroid_dist(q, self.centroids, self.mean, self.scale)
+        return probe_scores(self.model, dist, q)
+
+    def search(self, q, threshold: float, k: int, scores: torch.Tensor | None = None):
+        """One threshold: returns (D, I, nprobe, ncand) device tensors."""
+        q = q if isinstance(q, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(q))
+        q = q.to(self.device, torch.float32).contiguous()
+        if scores is None:
+            scores = self.scores(q)
+        probe, nprobe = select_probes(scores, "ge", self.n_bkt, threshold)
+        D, I, ncand = self.index.search(q, probe, k, dedup=self.dedup)
+        return D, I, nprobe, ncand
+
+    def sweep(self, q, gt, k: int, t_min=0.02, t_max=0.80, t_step=0.02, verbose=True):
+        """search.cpp:413-548 for a query set; one row per threshold."""
+        qt = torch.from_numpy(np.ascontiguousarray(q)).to(self.device)
+        k = min(k, gt.shape[1])  # search.cpp:357-360 clamps k to the gt width
+        rows = []
+        for thr in thresholds(t_min, t_max, t_step):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            D, I, nprobe, ncand = self.search(qt, float(thr), k)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            rec = recall_at_k(I.cpu().numpy(), gt, k)
+            row = {"threshold": float(thr), "avg_recall": float(rec.mean()),
+                   "avg_nprobe": float(nprobe.float().mean()), "avg_cmp": float(ncand.double().mean()),
+                   "avg_time": dt / len(q), "qps": len(q) / dt}
+            rows.append(row)
+            if verbose:
+                print(f"=== Threshold = {thr:g} ===\nThreshold    : {thr:g}\n"
+                      f"avg_recall   : {row['avg_recall']:g}\navg_nprobe   : {row['avg_nprobe']:g}\n"
+                      f"avg_cmp      : {row['avg_cmp']:g}\navg_time(q)  : {row['avg_time']:g} s\n"
+                      f"QPS          : {row['qps']:g} q/s\n----------------------------------------")
+        return rows
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description="LIRA end-to-end search on MI355X (search.cpp flags)")
+    ap.add_argument("--dataset", required=True)
+    ap.add_argument("--data_path", default="/data/vector_datasets")
+    ap.add_argument("--artifacts_dir", default=".")
+    ap.add_argument("--prefix", required=True)
+    ap.add_argument("--metric", default="L2")
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--num_threads", type=int, default=32, help="accepted for compatibility")
+    ap.add_argument("--t_min", type=float, default=0.02)
+    ap.add_argument("--t_max", type=float, default=0.80)
+    ap.add_argument("--t_step", type=float, default=0.02)
+    ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--dedup", action="store_true", help="keep each gid once (search.cpp does not)")
+    a = ap.parse_args(argv)
+    try:
+        prefix = os.path.join(a.artifacts_dir, a.prefix)
+        eng = SearchEngine(prefix, a.metric, a.device, a.dedup)
+        ddir = os.path.join(a.data_path, a.dataset)
+        q = np.ascontiguousarray(read_fvecs(os.path.join(ddir, f"{a.dataset}_query.fvecs")))
+        gt = np.ascontiguousarray(read_ivecs(os.path.join(ddir, f"{a.dataset}_groundtruth.ivecs")))
+        if q.shape[1] != eng.d:
+            raise ValueError("query dim != base dim.")
+        if gt.shape[0] != q.shape[0]:
+            raise ValueError("groundtruth and queries count mismatch.")
+        print(f"Dataset      : {a.dataset}\nPrefix       : {prefix}\nMetric       : {a.metric}\nK            : {a.k}")
+        eng.sweep(q, gt, a.k, a.t_min, a.t_max, a.t_step)
+        print("Done.")
+    except Exception as e:  # search.cpp:552-555
+        print(f"[Error] {e}", file=sys.stderr)
+        return 1
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,213 @@
+"""LIRA's query-path helpers (utils.py, LIRA_smallscale.py) on the HIP module.
+
+Same names and argument meaning as the reference, so a driver written against
+LIRA's utils switches by import:
+
+    get_dist_cid            utils.py:98-118          query->centroid distances
+    scale_dist              utils.py:139-142, search.cpp:238-250 (StandardScaler.transform)
+    create_flat_indexes     utils.py:407-422         one flat index per bucket
+    create_inner_indexes    utils.py:424-429
+    get_cmp_recall          LIRA_smallscale.py:145-174   per-(query, bucket) top-k
+    get_knn_distr_redundancy utils.py:354-379        gt neighbours per bucket (host)
+    query_tuning            LIRA_smallscale.py:176-241   threshold sweep (host)
+
+Differences, all deliberate and documented in DESIGN.md:
+* distances are fp32 in search.cpp's sequential order (scipy's cdist works in
+  float64 and casts; the two agree to ~1 ulp of the float32 result);
+* get_cmp_recall runs ONE batched scan of every bucket for every query instead
+  of n_bkt x n_q single-query faiss calls; the per-(query, bucket) wall time it
+  returns is that batch's time apportioned by bucket size;
+* a bucket with fewer than k vectors yields -1 labels (the reference indexes
+  with -1 and wraps to the bucket's last id, LIRA_smallscale.py:169);
+* equal distances order by smaller id (faiss: heap order).
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+
+from .index import PartitionedIndex, centroid_dist, normalize_metric
+
+
+def _cuda(a, dtype=torch.float32):
+    if isinstance(a, torch.Tensor):
+        return a.to(device="cuda", dtype=dtype).contiguous()
+    return torch.from_numpy(np.ascontiguousarray(a)).to(device="cuda", dtype=dtype)
+
+
+def _centroids_of(kmeans):
+    return kmeans.centroids if hasattr(kmeans, "centroids") else kmeans
+
+
+def get_dist_cid(data, kmeans, n_bkt=None, batch_size: int = 1 << 20) -> np.ndarray:
+    """Euclidean distance of every row of `data` to every centroid, (n, B) float32.
+
+    `kmeans` is anything with ``.centroids`` (faiss.Kmeans) or the (B, d) array.
+    """
+    c = _cuda(_centroids_of(kmeans))
+    n = data.shape[0]
+    out = np.empty((n, c.shape[0]), dtype=np.float32)
+    for s in range(0, n, batch_size):
+        out[s:s + batch_size] = centroid_dist(_cuda(data[s:s + batch_size]), c).cpu().numpy()
+    return out
+
+
+def scale_dist(dist, mean, scale):
+    """StandardScaler.transform with saved mean_/scale_ ((d - mean) / scale, scale 0 -> 1)."""
+    s = np.where(np.asarray(scale) == 0, np.float32(1), np.asarray(scale, np.float32))
+    return ((np.asarray(dist, np.float32) - np.asarray(mean, np.float32)) / s).astype(np.float32)
+
+
+class BucketView:
+    """faiss-like handle on one bucket of a shared PartitionedIndex."""
+
+    def __init__(self, parent: "BucketIndexes", b: int):
+        self._p, self.b = parent, b
+        self.ntotal = int(parent.index.list_sizes[b])
+        self.d = parent.index.d
+
+    def search(self, x, k: int):
+        """Labels are positions within the bucket, as faiss returns for x_d[ids]."""
+        q = _cuda(x)
+        probe = torch.full((q.shape[0], 1), self.b, dtype=torch.int32, device=q.device)
+        D, I, _ = self._p.index.search(q, probe, k, dedup=False)
+        I = I.cpu().numpy()
+        pos = self._p.positions(self.b, I)
+        return D.cpu().numpy(), pos
+
+
+class BucketIndexes(list):
+    """What create_flat_indexes returns: a list of per-bucket indexes, backed by
+    ONE device-resident PartitionedIndex so bucket scans batch on the GPU."""
+
+    def __init__(self, index: PartitionedIndex, bucket_ids):
+        self.index = index
+        self._ids = [np.asarray(b, dtype=np.int64) for b in bucket_ids]
+        self._sorted = None
+        super().__init__(BucketView(self, b) for b in range(len(bucket_ids)))
+
+    def positions(self, b: int, gids: np.ndarray) -> np.ndarray:
+        """Global ids -> positions in bucket b's insertion order (-1 stays -1)."""
+        if self._sorted is None:
+            self._sorted = [(np.argsort(i, kind="stable"), np.sort(i, kind="stable")) for i in self._ids]
+        order, srt = self._sorted[b]
+        out = np.full(gids.shape, -1, dtype=np.int64)
+        ok = gids >= 0
+        if ok.any():
+            out[ok] = order[np.searchsorted(srt, gids[ok])]
+        return out
+
+
+def create_flat_indexes(x_d, xd_id_bkts, cfg=None, dis_metric: str = "L2") -> BucketIndexes:
+    metric = normalize_metric(dis_metric)
+    idx = PartitionedIndex.from_cluster_ids(_cuda(x_d), xd_id_bkts, metric)
+    return BucketIndexes(idx, xd_id_bkts)
+
+
+def create_inner_indexes(x_d, cluster_ids, cfg) -> BucketIndexes:
+    return create_flat_indexes(x_d, cluster_ids, cfg, dis_metric=getattr(cfg, "dis_metric", "L2"))
+
+
+def get_cmp_recall(inner_indexes: BucketIndexes, x_q, xd_id_bkt, cfg, query_batch: int = 4096):
+    """Top-k of every bucket for every query (LIRA_smallscale.py:145-174).
+
+    Returns (search_time (nq, B) seconds, cmp_distr_all (nq, B) int,
+    found_aknn_id (nq, B, k) int64 global ids, -1 where a bucket has < k rows).
+    """
+    index = inner_indexes.index
+    n_bkt, k = index.n_lists, int(cfg.k)
+    q = _cuda(x_q)
+    nq = q.shape[0]
+    sizes = np.asarray(index.list_sizes, dtype=np.int64)
+    found = np.full((nq, n_bkt, k), -1, dtype=np.int64)
+    probe_all = torch.arange(n_bkt, dtype=torch.int32, device=q.device)
+    elapsed = 0.0
+    for s in range(0, nq, query_batch):
+        qs = q[s:s + query_batch]
+        probe = probe_all.expand(qs.shape[0], n_bkt).contiguous()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        _, I, _ = index.search(qs, probe, k, dedup=False, per_partition=True)
+        torch.cuda.synchronize()
+        elapsed += time.perf_counter() - t0
+        found[s:s + qs.shape[0]] = I.cpu().numpy()
+    cmp_distr_all = np.broadcast_to(sizes, (nq, n_bkt)).astype(int)
+    per_cand = elapsed / max(1, int(sizes.sum()) * nq)
+    search_time = cmp_distr_all * per_cand
+    return search_time, cmp_distr_all, found
+
+
+def get_knn_distr_redundancy(knn, data_2_bkt, cfg):
+    """utils.py:354-379: per (query, bucket) the gt neighbour ids located there."""
+    knn = np.asarray(knn)
+    d2b = np.asarray(data_2_bkt)
+    if d2b.ndim == 1:
+        d2b = d2b[:, None]
+    n, kk = knn.shape
+    n_bkt = cfg.n_bkt
+    cnt = np.zeros((n, n_bkt), dtype=int)
+    ids = np.empty((n, n_bkt), dtype=object)
+    for i in range(n):
+        for j in range(n_bkt):
+            ids[i, j] = []
+        bk = d2b[knn[i]]  # (k, n_mul)
+        for gi in range(kk):
+            for b in bk[gi]:
+                if b >= 0:
+                    cnt[i, b] += 1
+                    ids[i, b].append(int(knn[i, gi]))
+    return cnt, ids
+
+
+def query_tuning(all_outputs, knn_distr_id, found_aknn_id, search_time, cmp_distr_all, cfg, fw=None,
+                 part: int = 0, thresholds=None):
+    """Threshold sweep (LIRA_smallscale.py:176-241): for t in 0.02..0.80, probe
+    buckets with score > t; recall = |U_b (gt-in-b intersect found-in-b)| / k,
+    QPS = 1 / mean_i sum_{b probed} t[i, b].  Returns a list of row dicts and,
+    when cfg has pth_log/file_name, writes the CSV the reference writes."""
+    scores = all_outputs.cpu().numpy() if isinstance(all_outputs, torch.Tensor) else np.asarray(all_outputs)
+    nq, n_bkt = scores.shape
+    k = int(cfg.k)
+    found = np.asarray(found_aknn_id)
+    # F[i, b, g] : gt id g of query i sits in bucket b and bucket b's top-k found it
+    gt_ids = [sorted({g for b in range(n_bkt) for g in knn_distr_id[i][b]}) for i in range(nq)]
+    width = max(1, max((len(g) for g in gt_ids), default=1))
+    F = np.zeros((nq, n_bkt, width), dtype=bool)
+    for i in range(nq):
+        pos = {g: j for j, g in enumerate(gt_ids[i])}
+        for b in range(n_bkt):
+            lst = knn_distr_id[i][b]
+            if not lst:
+                continue
+            fb = set(int(v) for v in found[i, b])
+            for g in set(lst):
+                if int(g) in fb:
+                    F[i, b, pos[g]] = True
+    rows = []
+    if thresholds is None:
+        thresholds = np.arange(0.02, 0.82, 0.02)
+    for t in thresholds:
+        probe = scores > t
+        rec = (F & probe[:, :, None]).any(1).sum(1) / k
+        tq = (search_time * probe).sum(1)
+        tm = float(tq.mean())
+        rows.append({"threshold": float(t), "nprobe": float(probe.sum(1).mean()),
+                     "Recall": float(rec.mean()), "Computations": float((cmp_distr_all * probe).sum(1).mean()),
+                     "QPS": 1.0 / tm if tm > 0 else 0.0})
+        msg = (f"threshold: {t:.3f}, nprobe: {rows[-1]['nprobe']:.2f}, Recall: {rows[-1]['Recall']:.4f}, "
+               f"Computations: {rows[-1]['Computations']:.0f}, QPS: {rows[-1]['QPS']:.2f}")
+        print(msg)
+        if fw is not None:
+            print(msg, file=fw)
+    pth, name = getattr(cfg, "pth_log", None), getattr(cfg, "file_name", None)
+    if pth and name:
+        import os
+
+        import pandas as pd
+        d = os.path.join(pth, name + "_tuning_threshold")
+        os.makedirs(d, exist_ok=True)
+        pd.DataFrame(rows).to_csv(os.path.join(d, f"{getattr(cfg, 'duplicate_type', 'None')}_{part}.csv"),
+                                  index=False)
+    return rows
