@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1024)
     ap.add_argument("--recall-sample", type=int, default=100)
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (default); gloo only to rehearse N>1 on one GPU")
     return ap.parse_args()
 
 
@@ -60,12 +62,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world != 1:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    gpu = local % max(1, ndev)  # gloo rehearsal: several ranks may share one GPU
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     N, d, B, nprobe, k, metric, nq_default = CONFIGS[args.config]
     nq = args.nq or nq_default
@@ -74,7 +81,7 @@ def main():
     x, centres = mixture_torch(N, d, B, args.seed, dev)
     assign = nearest_centre(x, centres)
     offsets, ids, rep = build_csr(assign[:, None], B)
-    index = PartitionedIndex(d, metric, local)
+    index = PartitionedIndex(d, metric, gpu)
     index.add_lists(offsets, ids, x, rep)
     # rank-specific queries (weak scaling: each rank owns a disjoint batch)
     q, _ = mixture_torch(nq, d, B, args.seed + 1 + 7919 * rank, dev, centres=centres)
@@ -87,15 +94,16 @@ def main():
     D = torch.empty((nq, k), dtype=torch.float32, device=dev)
     I = torch.empty((nq, k), dtype=torch.int64, device=dev)
     ncand = torch.empty(nq, dtype=torch.int64, device=dev)
-    gD = [torch.empty_like(D) for _ in range(world)] if world > 1 else None
-    gI = [torch.empty_like(I) for _ in range(world)] if world > 1 else None
+    gdev = dev if args.backend == "nccl" else torch.device("cpu")
+    gD = [torch.empty(D.shape, dtype=D.dtype, device=gdev) for _ in range(world)] if world > 1 else None
+    gI = [torch.empty(I.shape, dtype=I.dtype, device=gdev) for _ in range(world)] if world > 1 else None
 
     def step():
         rank_nearest(q, centres, nprobe, out=probe, workspace=ws)
         index.search(q, probe, k, dedup=True, out=(D, I, ncand))
-        if world > 1:
-            dist.all_gather(gD, D)
-            dist.all_gather(gI, I)
+        if world > 1:  # the per-rank top-k of the sharded batch, to every rank
+            dist.all_gather(gD, D.to(gdev))
+            dist.all_gather(gI, I.to(gdev))
 
     for _ in range(args.warmup):
         step()
@@ -115,7 +123,7 @@ def main():
     prof = index.profile_read()
     index.set_profiling(False)
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=gdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
