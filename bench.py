@@ -54,7 +54,6 @@ def log(*a):
 def main():
     args = parse()
     from lira_amd import PartitionedIndex, RankWorkspace, rank_nearest
-    from lira_amd.index import build_csr
     from lira_amd.synthetic import CONFIGS, mixture_torch, nearest_centre
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -80,9 +79,10 @@ def main():
     # ---- synthetic index (identical on every rank: same seed) ----------------
     x, centres = mixture_torch(N, d, B, args.seed, dev)
     assign = nearest_centre(x, centres)
-    offsets, ids, rep = build_csr(assign[:, None], B)
-    index = PartitionedIndex(d, metric, gpu)
-    index.add_lists(offsets, ids, x, rep)
+    index = PartitionedIndex(d, metric, gpu).build(assign[:, None], x, B)  # device CSR (search.cpp:366-404)
+    offsets = np.zeros(B + 1, dtype=np.int64)
+    offsets[1:] = np.cumsum(index.list_sizes)
+    rep = index.max_replicas
     # rank-specific queries (weak scaling: each rank owns a disjoint batch)
     q, _ = mixture_torch(nq, d, B, args.seed + 1 + 7919 * rank, dev, centres=centres)
     torch.cuda.synchronize()
@@ -157,7 +157,7 @@ def main():
         ns = min(args.recall_sample, nq)
         xs = x.cpu().numpy()
         off = np.asarray(offsets, dtype=np.int64)
-        ids_np = ids.cpu().numpy()
+        ids_np = np.concatenate([index.list_ids(b) for b in range(B)])
         vecs = xs[ids_np]
         qs = q[:ns].cpu().numpy()
         pr = probe[:ns].cpu().numpy()

@@ -87,6 +87,20 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
                               const int32_t *list_ids, const float *x, int64_t n_rows,
                               int32_t max_replicas, void *stream);
 
+/*
+ * Device-side inverted-list build + load in one call: search.cpp:366-404.
+ * data_2_bkt: device int32 (n, n_mul), -1 = empty slot; every valid bucket id
+ * of row i receives i, lists are sorted ascending and de-duplicated
+ * (search.cpp:371-385), then gathered like lira_index_add_partitions.
+ * max_replicas is derived (largest number of distinct buckets of a row).
+ * Returns LIRA_ERANGE for a bucket id >= n_lists (search.cpp:375-377).
+ * Synchronous w.r.t. the host on return.
+ */
+int lira_index_build(lira_index *idx, int64_t n_lists, const int32_t *data_2_bkt, int64_t n,
+                     int32_t n_mul, const float *x, void *stream);
+/* host copy of one bucket's row ids, in list order (ascending after lira_index_build) */
+int lira_index_list_ids(const lira_index *idx, int64_t list_no, int32_t *out_host, void *stream);
+
 /* sizes: ntotal = total rows incl. replicas (faiss .ntotal, LIRA_smallscale.py:171) */
 int lira_index_info(const lira_index *idx, int64_t *d, int *metric, int64_t *n_lists,
                     int64_t *ntotal, int64_t *max_list);

@@ -46,6 +46,8 @@ SIGNATURES = {
     "lira_index_create": (_INT, [_INT, _I64, _INT, ctypes.POINTER(_P)]),
     "lira_index_destroy": (_INT, [_P]),
     "lira_index_add_partitions": (_INT, [_P, _I64, _P, _P, _P, _I64, _I32, _P]),
+    "lira_index_build": (_INT, [_P, _I64, _P, _I64, _I32, _P, _P]),
+    "lira_index_list_ids": (_INT, [_P, _I64, _P, _P]),
     "lira_index_info": (_INT, [_P, ctypes.POINTER(_I64), ctypes.POINTER(_INT),
                                ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I64)]),
     "lira_index_list_size": (_INT, [_P, _I64, ctypes.POINTER(_I64)]),

@@ -117,14 +117,49 @@ class PartitionedIndex:
         self.max_replicas = int(max_replicas)
         return self
 
+    def build(self, data_2_bkt, x, n_lists: int):
+        """search.cpp:366-404 on the device (lira_index_build): lists from the
+        (N, n_mul) bucket assignment over base vectors x."""
+        d2b = _dev(data_2_bkt, torch.int32, self.device)
+        if d2b.dim() == 1:
+            d2b = d2b[:, None]
+        x = _dev(x, torch.float32, self.device)
+        if x.dim() != 2 or x.shape[1] != self.d or x.shape[0] != d2b.shape[0]:
+            raise ValueError(f"x must be (N, {self.d}) with N = data_2_bkt rows")
+        with torch.cuda.device(self.device):
+            _lib.call("lira_index_build", self._h, int(n_lists), _lib.ptr(d2b), d2b.shape[0],
+                      d2b.shape[1], _lib.ptr(x), _lib.stream_ptr())
+        sizes = np.empty(n_lists, dtype=np.int64)
+        v = ctypes.c_int64()
+        for b in range(n_lists):
+            _lib.call("lira_index_list_size", self._h, b, ctypes.byref(v))
+            sizes[b] = v.value
+        self.n_lists = n_lists
+        self.list_sizes = sizes
+        self.ntotal = int(sizes.sum())
+        self.max_replicas = self._info_replicas(d2b)
+        return self
+
+    def _info_replicas(self, d2b):
+        # the module derived it; mirror it host-side for dedup sizing checks
+        rows = torch.sort(d2b, dim=1).values
+        distinct = (rows >= 0) & torch.cat([torch.ones_like(rows[:, :1], dtype=torch.bool),
+                                            rows[:, 1:] != rows[:, :-1]], dim=1)
+        return max(1, int(distinct.sum(1).max())) if rows.numel() else 1
+
+    def list_ids(self, b: int) -> np.ndarray:
+        """Row ids of bucket b in list order (search.cpp's sorted bucket_ids[b])."""
+        out = np.empty(int(self.list_sizes[b]), dtype=np.int32)
+        with torch.cuda.device(self.device):
+            _lib.call("lira_index_list_ids", self._h, int(b), out.ctypes.data_as(ctypes.c_void_p),
+                      _lib.stream_ptr())
+        return out
+
     @classmethod
     def from_assignment(cls, x_d, data_2_bkt, n_bkt: int, metric: str = "L2", device=None):
         """search.cpp:366-404: lists from data_2_bkt (N, n_mul) over base vectors x_d."""
         idx = cls(x_d.shape[1], metric, device)
-        d2b = _dev(data_2_bkt, torch.int32, idx.device)
-        offsets, ids, rep = build_csr(d2b, n_bkt)
-        idx.add_lists(offsets, ids, x_d, rep)
-        return idx
+        return idx.build(data_2_bkt, x_d, n_bkt)
 
     @classmethod
     def from_cluster_ids(cls, x_d, cluster_ids, metric: str = "L2", device=None):

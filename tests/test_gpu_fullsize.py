@@ -11,16 +11,16 @@ pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 
 def build(cfg, nq, seed=1234, n_override=None):
     from lira_amd import PartitionedIndex
-    from lira_amd.index import build_csr
     from lira_amd.synthetic import CONFIGS, mixture_torch, nearest_centre
     N, d, B, nprobe, k, metric, _ = CONFIGS[cfg]
     N = n_override or N
     dev = torch.device("cuda", 0)
     x, c = mixture_torch(N, d, B, seed, dev)
     assign = nearest_centre(x, c)
-    off, ids, rep = build_csr(assign[:, None], B)
-    idx = PartitionedIndex(d, metric, 0)
-    idx.add_lists(off, ids, x, rep)
+    idx = PartitionedIndex(d, metric, 0).build(assign[:, None], x, B)
+    off = np.zeros(B + 1, dtype=np.int64)
+    off[1:] = np.cumsum(idx.list_sizes)
+    ids = torch.from_numpy(np.concatenate([idx.list_ids(b) for b in range(B)]))
     q, _ = mixture_torch(nq, d, B, seed + 1, dev, centres=c)
     return idx, x, c, q, off, ids, (N, d, B, nprobe, k, metric)
 

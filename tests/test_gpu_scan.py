@@ -151,3 +151,28 @@ def test_empty_batch_and_idempotence():
     for i in (0, 17, 63):
         Di, Ii, _ = run(idx, q[i:i + 1], probe[i:i + 1], 10)
         assert np.array_equal(Ii[0], a[1][i]) and np.array_equal(bits(Di[0]), bits(a[0][i]))
+
+
+def test_device_csr_builder_matches_search_cpp():
+    from lira_amd import LiraError, PartitionedIndex
+    rng = np.random.default_rng(21)
+    n, b = 20000, 37
+    x = rng.standard_normal((n, 12), dtype=np.float32)
+    d2b = rng.integers(-1, b, (n, 3)).astype(np.int32)
+    d2b[::7, 1] = d2b[::7, 0]  # a bucket repeated inside a row (search.cpp:384 uniques it)
+    idx = PartitionedIndex(12, "L2").build(torch.from_numpy(d2b).cuda(), torch.from_numpy(x).cuda(), b)
+    off, ids = oracle.build_csr(d2b, b)
+    assert np.array_equal(idx.list_sizes, np.diff(off))
+    for bb in range(b):
+        assert np.array_equal(idx.list_ids(bb), ids[off[bb]:off[bb + 1]])
+    distinct = max(len(set(r[r >= 0])) for r in d2b)
+    assert idx.max_replicas == distinct
+    q = rng.standard_normal((20, 12), dtype=np.float32)
+    probe = rng.integers(0, b, (20, 5)).astype(np.int32)
+    D, I, _ = run(idx, q, probe, 10)
+    Do, Io, _ = oracle.scan_topk(q, off, ids, x[ids], probe, 10, oracle.L2, distinct)
+    assert np.array_equal(I, Io) and np.array_equal(bits(D), bits(Do))
+    bad = d2b.copy()
+    bad[5, 0] = b
+    with pytest.raises(LiraError, match="out of range"):
+        PartitionedIndex(12, "L2").build(torch.from_numpy(bad).cuda(), torch.from_numpy(x).cuda(), b)
