@@ -34,6 +34,7 @@
 //   k_scan   persistent; pulls work items from an atomic head
 //   k_merge  per query: merge the per-(slot, chunk) top-k lists, dedup, emit
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 
 #include "lira_device.hpp"
@@ -192,7 +193,21 @@ struct ScanSmem {
 };
 
 typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) void gbl_void_t;
+
+// One LDS-DMA piece: 16 B per lane from `gsrc` into LDS at lds_addr + 16*lane
+// (lds_addr wave-uniform).  Inline asm, so hipcc does not treat it as an LDS
+// write it must drain (vmcnt(0)) before every later ds_read; the kernel waits
+// for it explicitly at the ring hand-off.  M0 is written and restored inside
+// the statement (it is compiler-reserved).
+__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_addr) {
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds_addr)
+        : "memory");
+}
 
 // Both halves of the wave merge their row's survivor buffer (n keys, per
 // half) into the row's sorted k-list in LDS.  Rows without a query
@@ -235,6 +250,7 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
     const int tx = tid & 31, ty = tid >> 5;  // ty = 2*wave + half
     const int k = a.k;
     const float4 *Xg = (const float4 *)a.X;
+    const uint32_t xs_lds = (uint32_t)(uintptr_t)(lds_void_t *)Xs;  // LDS byte address of the ring
     const int tstride = (int)a.dpad * (kTile / 4);  // float4 per tile
     const int nchunk = (int)(a.dpad / kDK);
 
@@ -296,17 +312,16 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
         auto stage = [&](int tb, int jc, int slot) {
             const int ntv = min(kBlockTiles, tb_end - tb);
             const float4 *src = Xg + (int64_t)(tile0 + tb) * tstride + jc * (kTile / 4) + tid;
-            float *dst = Xs + slot * (kBlockTiles * kDK * kTile) + wave * 256;
+            const uint32_t dst = __builtin_amdgcn_readfirstlane(
+                xs_lds + (uint32_t)(slot * (kBlockTiles * kDK * kTile) + wave * 256) * 4u);
 #pragma unroll
             for (int i = 0; i < kBlockTiles; ++i)
-                __builtin_amdgcn_global_load_lds((gbl_void_t *)(src + min(i, ntv - 1) * tstride),
-                                                 (lds_void_t *)(dst + i * (kDK * kTile)), 16, 0, 0);
+                glds16(src + min(i, ntv - 1) * tstride, dst + (uint32_t)(i * (kDK * kTile) * 4));
+            // raw loads only: the pad-dim select happens at the LDS store one
+            // chunk later, so nothing here waits on vmcnt (which would also
+            // wait for the DMA just issued)
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int j = jc + jj + u;
-                const float v = qrow[min(j, dlast)];
-                pq[u] = j <= dlast ? v : 0.0f;
-            }
+            for (int u = 0; u < 2; ++u) pq[u] = qrow[min(jc + jj + u, dlast)];
         };
         int slot = 0;
         stage(tb_begin, 0, 0);
@@ -331,8 +346,8 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
             for (int c = 0; c < nchunk; ++c) {
                 float *Qc = Qs + slot * (kDK * kQT);
 #pragma unroll
-                for (int u = 0; u < 2; ++u) Qc[(jj + u) * kQT + sq] = pq[u];
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA for the slot landed
+                for (int u = 0; u < 2; ++u) Qc[(jj + u) * kQT + sq] = c * kDK + jj + u <= dlast ? pq[u] : 0.0f;
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA (asm, uncounted by hipcc) landed
                 __syncthreads();  // every wave's DMA landed; every wave is done with the other slot
                 {   // stage the next chunk (this block or the next) into the other slot
                     int njc = (c + 1) * kDK, ntb = tb;
@@ -398,11 +413,54 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
             // Fast filter: fp32 score against each row's k-th key (+inf while the
             // list is not full, -inf for rows without a query).
             float thf[4];
-            bool any = false;
+            bool any = false, unfilled = false;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const u64 t = lists[(ty * 4 + u) * k + k - 1];
                 thf[u] = !row_ok[u] ? -__builtin_inff() : t == kEmptyKey ? __builtin_inff() : key_score(t);
+                unfilled |= thf[u] == __builtin_inff();
+            }
+            if (RL <= 2 && __any(unfilled)) {
+                // A row whose list is not yet full (an item's first block) gets a
+                // bound from the block itself: with t = RL, lane l's t-th smallest
+                // score m_l, and j = ceil(k/t), the j-th smallest m_l has j*t >= k
+                // real candidates at or below it, so nothing above it can be in
+                // the row's top k.  Keeps the first block from pushing all 256
+                // candidates through the survivor buffers.  (For k > 64 the bound
+                // is loose and measured no faster, so it is off there.)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    float sv[8];
+#pragma unroll
+                    for (int v = 0; v < 8; ++v) {
+                        const float sc = METRIC == LIRA_METRIC_IP ? -acc[u][v] : acc[u][v];
+                        sv[v] = gid[v] >= 0 && sc == sc ? sc : __builtin_inff();
+                    }
+                    float m;
+                    if (RL == 1) {
+                        m = sv[0];
+#pragma unroll
+                        for (int v = 1; v < 8; ++v) m = fminf(m, sv[v]);
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 8; ++i)
+#pragma unroll
+                            for (int v = 0; v + 1 < 8 - i; ++v) {
+                                const float lo = fminf(sv[v], sv[v + 1]), hi = fmaxf(sv[v], sv[v + 1]);
+                                sv[v] = lo;
+                                sv[v + 1] = hi;
+                            }
+                        m = sv[RL - 1];
+                    }
+                    u64 mk[1] = {((u64)f2ord(m) << 32) | (uint32_t)tx};
+                    half_sort<1>(mk);
+                    const int j = (k + RL - 1) / RL;  // <= 32
+                    const float bound = key_score(shfl64(mk[0], (lane & 32) + j - 1));
+                    thf[u] = fminf(thf[u], bound);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
 #pragma unroll
                 for (int v = 0; v < 8; ++v)
                     any |= (METRIC == LIRA_METRIC_IP ? -acc[u][v] : acc[u][v]) <= thf[u];
@@ -416,8 +474,8 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
                 int pos[8], tot = 0;
 #pragma unroll
                 for (int v = 0; v < 8; ++v) {
-                    const u64 key = make_key(METRIC == LIRA_METRIC_IP ? -acc[u][v] : acc[u][v], gid[v]);
-                    const u64 b = __ballot(key < thr);
+                    const float sc = METRIC == LIRA_METRIC_IP ? -acc[u][v] : acc[u][v];
+                    const u64 b = __ballot(make_key(sc, gid[v]) < thr && sc <= thf[u]);
                     hb[v] = (lane & 32) ? (uint32_t)(b >> 32) : (uint32_t)b;
                     pos[v] = tot + __popc(hb[v] & ((1u << tx) - 1u));
                     tot += __popc(hb[v]);
@@ -623,7 +681,17 @@ static ScanPlan make_plan(const lira_index *idx, int64_t nq, int64_t nprobe, int
     ScanPlan pl;
     const int64_t npairs = nq * nprobe;
     const int ncu = cu_count(idx->device);
-    const int64_t target = 4LL * ncu;
+    pl.smem = ScanSmem::total((int)k);
+    const int occ = std::max(1, std::min(scan_occ(scan_rl(k)), (160 * 1024) / pl.smem));
+    pl.grid = ncu * occ;
+    // Split buckets into chunks until the persistent grid sees ~`rounds` items
+    // per workgroup, so the last, partly filled round of items is a small
+    // fraction of the run (the tail); LIRA_SCAN_ROUNDS overrides (tuning).
+    static const int rounds = [] {
+        const char *e = getenv("LIRA_SCAN_ROUNDS");
+        return e && atoi(e) > 0 ? atoi(e) : 8;
+    }();
+    const int64_t target = (int64_t)rounds * pl.grid;
     const int64_t est_items = (npairs + kQT - 1) / kQT + std::min<int64_t>(idx->n_lists, npairs);
     const int64_t max_blocks = std::max<int64_t>(1, (idx->max_list_tiles + kBlockTiles - 1) / kBlockTiles);
     if (est_items >= target) {
@@ -633,9 +701,6 @@ static ScanPlan make_plan(const lira_index *idx, int64_t nq, int64_t nprobe, int
         pl.bpc = (int)std::max<int64_t>(1, (max_blocks + split - 1) / split);
     }
     pl.nch_max = (int)((max_blocks + pl.bpc - 1) / pl.bpc);
-    pl.smem = ScanSmem::total((int)k);
-    const int occ = std::max(1, std::min(scan_occ(scan_rl(k)), (160 * 1024) / pl.smem));
-    pl.grid = ncu * occ;
     size_t o = 0;
     auto take = [&](size_t bytes) {
         size_t at = o;
