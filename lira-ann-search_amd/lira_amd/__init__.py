@@ -9,6 +9,7 @@ liblira_hip.so), with the reference's Python-side interfaces on top:
 * ``utils``                  -- get_dist_cid / create_flat_indexes / get_cmp_recall /
                                 query_tuning (utils.py, LIRA_smallscale.py)
 * ``search``                 -- search.cpp's end-to-end artifact search
+* ``knn``                    -- compute_knn.cpp self-kNN, k-means (utils.py:222-330)
 """
 from ._lib import LiraError, load as load_library  # noqa: F401
 from .index import (PartitionedIndex, build_csr, centroid_dist, centroid_gemm,  # noqa: F401
