@@ -410,14 +410,30 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
 
             // ---- selection, per wave and per half-wave, straight from registers.
             // Half h of wave w owns rows (2w+h)*4+u; lane tx holds 8 candidates of each.
-            // Fast filter: fp32 score against each row's k-th key (+inf while the
-            // list is not full, -inf for rows without a query).
+            // A candidate survives when its fp32 score is <= the row's threshold:
+            // the score of the row's k-th key (+inf while the list is not full,
+            // NaN -- nothing passes -- for rows without a query).  A tie at the
+            // threshold with a larger id is admitted and then dropped by the merge.
+            // Padding candidates (gid -1: a bucket's partial last tile, tiles past
+            // its end) get a score that never passes.
+            {
+                bool pad = false;
+#pragma unroll
+                for (int v = 0; v < 8; ++v) pad |= gid[v] < 0;
+                if (__any(pad)) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+#pragma unroll
+                        for (int v = 0; v < 8; ++v)
+                            if (gid[v] < 0) acc[u][v] = METRIC == LIRA_METRIC_IP ? -__builtin_inff() : __builtin_inff();
+                }
+            }
             float thf[4];
-            bool any = false, unfilled = false;
+            bool unfilled = false;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const u64 t = lists[(ty * 4 + u) * k + k - 1];
-                thf[u] = !row_ok[u] ? -__builtin_inff() : t == kEmptyKey ? __builtin_inff() : key_score(t);
+                thf[u] = !row_ok[u] ? __builtin_nanf("") : t == kEmptyKey ? __builtin_inff() : key_score(t);
                 unfilled |= thf[u] == __builtin_inff();
             }
             if (RL <= 2 && __any(unfilled)) {
@@ -434,7 +450,7 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
 #pragma unroll
                     for (int v = 0; v < 8; ++v) {
                         const float sc = METRIC == LIRA_METRIC_IP ? -acc[u][v] : acc[u][v];
-                        sv[v] = gid[v] >= 0 && sc == sc ? sc : __builtin_inff();
+                        sv[v] = sc == sc ? sc : __builtin_inff();
                     }
                     float m;
                     if (RL == 1) {
@@ -456,31 +472,27 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
                     half_sort<1>(mk);
                     const int j = (k + RL - 1) / RL;  // <= 32
                     const float bound = key_score(shfl64(mk[0], (lane & 32) + j - 1));
-                    thf[u] = fminf(thf[u], bound);
+                    if (row_ok[u]) thf[u] = fminf(thf[u], bound);
                 }
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-#pragma unroll
-                for (int v = 0; v < 8; ++v)
-                    any |= (METRIC == LIRA_METRIC_IP ? -acc[u][v] : acc[u][v]) <= thf[u];
-            }
-            if (!__any(any)) continue;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
                 const int row = ty * 4 + u;
-                const u64 thr = row_ok[u] ? lists[row * k + k - 1] : 0ull;
+                u64 b[8], ball = 0;
+#pragma unroll
+                for (int v = 0; v < 8; ++v) {
+                    b[v] = __ballot((METRIC == LIRA_METRIC_IP ? -acc[u][v] : acc[u][v]) <= thf[u]);
+                    ball |= b[v];
+                }
+                if (!ball) continue;  // wave-uniform: no survivor in either half's row
                 uint32_t hb[8];  // this half's survivor masks
                 int pos[8], tot = 0;
 #pragma unroll
                 for (int v = 0; v < 8; ++v) {
-                    const float sc = METRIC == LIRA_METRIC_IP ? -acc[u][v] : acc[u][v];
-                    const u64 b = __ballot(make_key(sc, gid[v]) < thr && sc <= thf[u]);
-                    hb[v] = (lane & 32) ? (uint32_t)(b >> 32) : (uint32_t)b;
+                    hb[v] = (lane & 32) ? (uint32_t)(b[v] >> 32) : (uint32_t)b[v];
                     pos[v] = tot + __popc(hb[v] & ((1u << tx) - 1u));
                     tot += __popc(hb[v]);
                 }
-                if (!__any(tot > 0)) continue;
                 u64 *buf = bufs + row * kBufCap;
                 int bc = meta[64 + row];
                 int consumed = 0;
