@@ -58,6 +58,7 @@ struct ScanArgs {
     const int32_t *cnt, *qoff, *qlist, *item_off, *nch;
     int32_t *head;        // [0] = next item, [1] = n_items
     u64 *partial;         // [pair][nch_max][k]
+    uint32_t *qbound;     // [nq] f2ord(k-th score) published per query, ~0 = none; NULL = off
     int64_t d, dpad;
     int n_lists, nprobe, k, bpc, nch_max;
 };
@@ -302,6 +303,19 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
         bool row_ok[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) row_ok[u] = meta[8 + ty * 4 + u] >= 0;
+        // lane tx keeps the query of row ty*4 + (tx & 3) (its pruning bound slot)
+        const int my_pair = meta[8 + ty * 4 + (tx & 3)];
+        const int my_q = my_pair >= 0 ? my_pair / a.nprobe : -1;
+        // Cross-item pruning: a full k-list of any item of query q holds k
+        // distinct ids scoring <= its k-th score, so that score bounds q's final
+        // k-th; every item of q filters against the smallest one published so
+        // far (a stale value is still a valid bound; ties pass, the filter is <=).
+        auto publish = [&](int u) {
+            if (a.qbound && row_ok[u] && tx == 0) {
+                const u64 t = lists[(ty * 4 + u) * k + k - 1];
+                if (t != kEmptyKey) atomicMin(a.qbound + meta[8 + ty * 4 + u] / a.nprobe, (uint32_t)(t >> 32));
+            }
+        };
 
         // Stage chunk (tb, jc) into ring slot `slot`: X by LDS-DMA (wave w moves
         // bytes [1 KiB*w, 1 KiB*(w+1)) of each tile's 4 KiB chunk; tiles past the
@@ -337,6 +351,8 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
                 gid[0] = g0.x; gid[1] = g0.y; gid[2] = g0.z; gid[3] = g0.w;
                 gid[4] = g1.x; gid[5] = g1.y; gid[6] = g1.z; gid[7] = g1.w;
             }
+            const uint32_t my_bound = a.qbound && my_q >= 0
+                ? __hip_atomic_load(a.qbound + my_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
             float acc[4][8];
 #pragma unroll
             for (int u = 0; u < 4; ++u)
@@ -434,6 +450,8 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
             for (int u = 0; u < 4; ++u) {
                 const u64 t = lists[(ty * 4 + u) * k + k - 1];
                 thf[u] = !row_ok[u] ? __builtin_nanf("") : t == kEmptyKey ? __builtin_inff() : key_score(t);
+                const uint32_t gb = (uint32_t)__shfl((int)my_bound, (lane & 32) + u);
+                if (row_ok[u] && gb != ~0u) thf[u] = fminf(thf[u], ord2f(gb));
                 unfilled |= thf[u] == __builtin_inff();
             }
             if (RL <= 2 && __any(unfilled)) {
@@ -510,6 +528,7 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
                     __builtin_amdgcn_wave_barrier();
                     if (__any(bc == kBufCap)) {  // a full buffer: merge both halves' buffers
                         flush_rows<RL>(lists + row * k, buf, bc, k, row_ok[u]);
+                        publish(u);
                         bc = 0;
                     }
                     if (!__any(consumed < tot)) break;
@@ -524,7 +543,10 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
         for (int u = 0; u < 4; ++u) {
             const int row = ty * 4 + u;
             const int bc = meta[64 + row];
-            if (__any(bc > 0)) flush_rows<RL>(lists + row * k, bufs + row * kBufCap, bc, k, row_ok[u]);
+            if (__any(bc > 0)) {
+                flush_rows<RL>(lists + row * k, bufs + row * kBufCap, bc, k, row_ok[u]);
+                publish(u);
+            }
             const int pair = meta[8 + row];
             if (pair >= 0) {
                 u64 *dst = a.partial + ((int64_t)pair * a.nch_max + ch) * k;
@@ -660,7 +682,7 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
 
 struct ScanPlan {
     int bpc = 1, nch_max = 1, grid = 1, smem = 0;
-    size_t off_cnt, off_cursor, off_qoff, off_item, off_nch, off_head, off_qlist, off_partial,
+    size_t off_cnt, off_cursor, off_qoff, off_item, off_nch, off_head, off_qlist, off_partial, off_qbound,
         total;
 };
 
@@ -728,6 +750,7 @@ static ScanPlan make_plan(const lira_index *idx, int64_t nq, int64_t nprobe, int
     pl.off_nch = take(nl * 4);
     pl.off_qlist = take((size_t)npairs * 4);
     pl.off_partial = take((size_t)npairs * pl.nch_max * (size_t)k * 8);
+    pl.off_qbound = take((size_t)nq * 4);
     pl.total = o;
     return pl;
 }
@@ -794,6 +817,7 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
     int32_t *nch = (int32_t *)(w + pl.off_nch);
     int32_t *qlist = (int32_t *)(w + pl.off_qlist);
     u64 *partial = (u64 *)(w + pl.off_partial);
+    uint32_t *qbound = per_part ? nullptr : (uint32_t *)(w + pl.off_qbound);
 
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     if (idx->profiling) {
@@ -808,6 +832,7 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
     }
     // cnt, cursor and head are contiguous at the start of the workspace
     LIRA_HIP_TRY(hipMemsetAsync(w, 0, pl.off_qoff, st));
+    if (qbound) LIRA_HIP_TRY(hipMemsetAsync(qbound, 0xff, (size_t)nq * 4, st));
     const int64_t npairs = nq * nprobe;
     const int nl = (int)idx->n_lists;
     const unsigned pg = (unsigned)((npairs + kPairsPerBlock - 1) / kPairsPerBlock);
@@ -831,6 +856,7 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
     a.nch = nch;
     a.head = head;
     a.partial = partial;
+    a.qbound = qbound;
     a.d = idx->d;
     a.dpad = idx->dpad;
     a.n_lists = nl;
