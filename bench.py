@@ -29,6 +29,7 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_F32_PEAK_TOPS = 78.64   # non-FMA fp32 lane ops/s: 157.3 TFLOP/s counts an FMA as 2
+MFMA_F32_PEAK_TFLOPS = 157.3  # v_mfma_f32_32x32x2_f32 dense peak (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -53,7 +54,7 @@ def log(*a):
 
 def main():
     args = parse()
-    from lira_amd import PartitionedIndex, RankWorkspace, rank_nearest
+    from lira_amd import PartitionedIndex, RankWorkspace, centroid_gemm, rank_nearest
     from lira_amd.synthetic import CONFIGS, mixture_torch, nearest_centre
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -126,6 +127,23 @@ def main():
         t = torch.tensor([elapsed], device=gdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    # ---- the ranking GEMM alone (MFMA utilisation), outside the timed region ---
+    def event_ms(fn, reps=20):
+        s = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        fn()
+        torch.cuda.synchronize()
+        e0.record(s)
+        for _ in range(reps):
+            fn()
+        e1.record(s)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    gemm_ms = event_ms(lambda: centroid_gemm(q, centres))
+    rank_ms = event_ms(lambda: rank_nearest(q, centres, nprobe, out=probe, workspace=ws))
+    gemm_tflops = 2.0 * nq * B * d / (gemm_ms * 1e-3) / 1e12
 
     # ---- per-launch algorithmic figures -----------------------
     cand = int(ncand.sum().item())  # candidates scanned in one launch (this rank)
@@ -228,7 +246,14 @@ def main():
                                  "(frac > 1) while actual HBM traffic stays far below it. The "
                                  "binding bound is the fp32 VALU (exact search.cpp arithmetic: "
                                  "3 unfused ops per candidate-dim); see DESIGN.md"},
-            "kernels_ms_per_step": {"plan": plan_ms, "scan": scan_ms, "merge": merge_ms},
+            "kernels_ms_per_step": {"plan": plan_ms, "scan": scan_ms, "merge": merge_ms,
+                                    "rank_nearest": rank_ms},
+            "rank_gemm": {"kernel": "k_centroid_gemm (v_mfma_f32_32x32x2_f32)", "ms": gemm_ms,
+                          "achieved": gemm_tflops, "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                          "frac": gemm_tflops / MFMA_F32_PEAK_TFLOPS,
+                          "flops": 2 * nq * B * d,
+                          "note": "query x centroid GEMM of the ranking step (2*nq*B*d); "
+                                  "rank_nearest adds the exact re-check + top-nprobe select"},
             "cpu_baseline": cpu,
             "candidates_per_query": cand / nq,
             **extra,

@@ -100,16 +100,20 @@ __global__ __launch_bounds__(256) void k_centroid_gemm(const float *__restrict__
     const float ebound = 8.0f * (float)(d + 8) * 5.9604645e-08f;
     const int col = lane & 31;
     const int cb = c0 + wc * 32 + col;
+    // the bound grows with ||c||^2: one atomic per query row with the wave's
+    // largest in-range column norm (not one per element)
+    float mx = cb < nb ? nrm[64 + wc * 32 + col] : 0.0f;
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         int64_t qr = q0 + wr * 32 + row;
         float nq_ = nrm[wr * 32 + row], nc_ = nrm[64 + wc * 32 + col];
         float v = (nq_ + nc_) - 2.0f * acc[r];
-        if (qr < nq && cb < nb) {
-            out_sq[qr * nb + cb] = v;
-            if (out_err) atomicMax((unsigned int *)&out_err[qr], __float_as_uint(ebound * (nq_ + nc_) + 1e-30f));
-        }
+        if (qr < nq && cb < nb) out_sq[qr * nb + cb] = v;
+        if (out_err && col == 0 && qr < nq)
+            atomicMax((unsigned int *)&out_err[qr], __float_as_uint(ebound * (nq_ + mx) + 1e-30f));
     }
 }
 

@@ -1,0 +1,52 @@
+"""Turn a tools/profile_box.sh summary into the per-config record bench.py
+reads (profiles/pmc_scan_<config>.json) and copy the evidence into profiles/.
+
+usage: python tools/pmc_to_profile.py <config> <gpurun_out/prof_TAG> <round tag, e.g. r01>
+"""
+import json
+import os
+import shutil
+import sys
+
+WORKLOADS = {
+    "sift1m": "sift1m (N=1M d=128 B=64 nprobe=8 k=10 L2, 10k queries)",
+    "gist1m": "gist1m (N=1M d=960 B=128 nprobe=16 k=10 L2, 1k queries)",
+    "deep10m": "deep10m (N=10M d=96 B=256 nprobe=32 k=100 IP, 10k queries)",
+    "bigann100m": "bigann100m (N=100M d=128 B=1024 nprobe=32 k=10 L2, 10k queries)",
+}
+
+
+def main(cfg, src, tag):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    summ = json.load(open(os.path.join(src, "summary.json")))
+    scan = [(k, v) for k, v in summ.items() if k.startswith("lira::k_scan")]
+    if not scan:
+        raise SystemExit("no k_scan entry in summary")
+    name, e = max(scan, key=lambda kv: kv[1].get("trace", {}).get("calls", 0))
+    p = e.get("pmc", {})
+    rec = {
+        "kernel": name,
+        "workload": WORKLOADS.get(cfg, cfg),
+        "hbm_bytes_per_launch": e.get("hbm_bytes_per_launch"),
+        "avg_ns_trace": e.get("trace", {}).get("avg_ns"),
+        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes with "
+                  "--kernel-trace; bytes = (2*FETCH_SIZE + WRITE_SIZE) KiB (gfx950 FETCH_SIZE "
+                  "counts half of 16-B/lane streaming reads incl. LDS-DMA loads, "
+                  "MI355X_MICROARCH.md HBM section)",
+        "FETCH_SIZE_KiB": p.get("FETCH_SIZE"),
+        "WRITE_SIZE_KiB": p.get("WRITE_SIZE"),
+        "SQ_INSTS_VALU": p.get("SQ_INSTS_VALU"),
+        "wave_cycle_split": e.get("wave_cycle_split"),
+        "source": f"profiles/{tag}_{cfg}_pmc_summary.json",
+    }
+    out = os.path.join(root, "profiles")
+    json.dump(rec, open(os.path.join(out, f"pmc_scan_{cfg}.json"), "w"), indent=1)
+    shutil.copy(os.path.join(src, "summary.json"), os.path.join(out, f"{tag}_{cfg}_pmc_summary.json"))
+    st = os.path.join(src, "trace", "run_kernel_stats.csv")
+    if os.path.exists(st):
+        shutil.copy(st, os.path.join(out, f"{tag}_{cfg}_kernel_stats.csv"))
+    print(json.dumps(rec, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])
