@@ -65,8 +65,11 @@ struct ScanArgs {
 
 // Pairs per bucket.  With an LDS histogram each block issues one global
 // atomic per touched bucket (80k pairs on 64 buckets: 128 us -> ~5 us).
+// Pairs with probe slot in [slo, shi) only (the two scan phases); every pair
+// is range-checked once, in the phase that owns it.
 __global__ __launch_bounds__(256) void k_count(const int32_t *probe, int64_t npairs, int n_lists,
-                                               int32_t *cnt, int32_t *err) {
+                                               int nprobe, int slo, int shi, int32_t *cnt,
+                                               int32_t *err) {
     extern __shared__ int32_t hist[];
     const bool lds = n_lists <= kHistMax;
     const int64_t s = (int64_t)blockIdx.x * kPairsPerBlock;
@@ -76,6 +79,8 @@ __global__ __launch_bounds__(256) void k_count(const int32_t *probe, int64_t npa
         __syncthreads();
     }
     for (int64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
+        const int sl = (int)(i % nprobe);
+        if (sl < slo || sl >= shi) continue;
         int p = probe[i];
         if (p >= n_lists) {
             atomicOr(err, 1);
@@ -143,8 +148,8 @@ __global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t
 // (global atomic), then places its pairs by LDS-atomic rank.  The order inside
 // a bucket's list is arbitrary; results do not depend on it.
 __global__ __launch_bounds__(256) void k_fill(const int32_t *probe, int64_t npairs, int n_lists,
-                                              const int32_t *qoff, int32_t *cursor,
-                                              int32_t *qlist) {
+                                              int nprobe, int slo, int shi, const int32_t *qoff,
+                                              int32_t *cursor, int32_t *qlist) {
     extern __shared__ int32_t sh[];
     const bool lds = n_lists <= kHistMax / 2;
     int32_t *hist = sh, *base = sh + (lds ? n_lists : 0);
@@ -152,8 +157,9 @@ __global__ __launch_bounds__(256) void k_fill(const int32_t *probe, int64_t npai
     const int64_t e = min<int64_t>(npairs, s + kPairsPerBlock);
     if (!lds) {
         for (int64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
+            const int sl = (int)(i % nprobe);
             int p = probe[i];
-            if (p < 0 || p >= n_lists) continue;
+            if (sl < slo || sl >= shi || p < 0 || p >= n_lists) continue;
             qlist[qoff[p] + atomicAdd(&cursor[p], 1)] = (int32_t)i;
         }
         return;
@@ -161,8 +167,9 @@ __global__ __launch_bounds__(256) void k_fill(const int32_t *probe, int64_t npai
     for (int b = threadIdx.x; b < n_lists; b += blockDim.x) hist[b] = 0;
     __syncthreads();
     for (int64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
+        const int sl = (int)(i % nprobe);
         int p = probe[i];
-        if (p >= 0 && p < n_lists) atomicAdd(&hist[p], 1);
+        if (sl >= slo && sl < shi && p >= 0 && p < n_lists) atomicAdd(&hist[p], 1);
     }
     __syncthreads();
     for (int b = threadIdx.x; b < n_lists; b += blockDim.x) {
@@ -171,8 +178,9 @@ __global__ __launch_bounds__(256) void k_fill(const int32_t *probe, int64_t npai
     }
     __syncthreads();
     for (int64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
+        const int sl = (int)(i % nprobe);
         int p = probe[i];
-        if (p < 0 || p >= n_lists) continue;
+        if (sl < slo || sl >= shi || p < 0 || p >= n_lists) continue;
         qlist[base[p] + atomicAdd(&hist[p], 1)] = (int32_t)i;
     }
 }
@@ -838,11 +846,6 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
     const unsigned pg = (unsigned)((npairs + kPairsPerBlock - 1) / kPairsPerBlock);
     const size_t hc = nl <= kHistMax ? (size_t)nl * 4 : 0;
     const size_t hf = nl <= kHistMax / 2 ? (size_t)nl * 8 : 0;
-    hipLaunchKernelGGL(k_count, dim3(pg), dim3(256), hc, st, probe, npairs, nl, cnt, idx->err);
-    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, pl.bpc, qoff,
-                       item_off, nch, head);
-    hipLaunchKernelGGL(k_fill, dim3(pg), dim3(256), hf, st, probe, npairs, nl, qoff, cursor, qlist);
-    LIRA_HIP_TRY(hipGetLastError());
 
     ScanArgs a;
     a.Q = q;
@@ -864,16 +867,43 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
     a.k = (int)k;
     a.bpc = pl.bpc;
     a.nch_max = pl.nch_max;
-    if (ev[1]) LIRA_HIP_TRY(hipEventRecord(ev[1], st));
-    hipError_t e;
-    if (idx->metric == LIRA_METRIC_L2)
-        e = RL == 1 ? launch_scan<1, LIRA_METRIC_L2>(a, pl, st)
-            : RL == 2 ? launch_scan<2, LIRA_METRIC_L2>(a, pl, st)
-            : RL == 4 ? launch_scan<4, LIRA_METRIC_L2>(a, pl, st) : launch_scan<8, LIRA_METRIC_L2>(a, pl, st);
-    else
-        e = RL == 1 ? launch_scan<1, LIRA_METRIC_IP>(a, pl, st)
-            : RL == 2 ? launch_scan<2, LIRA_METRIC_IP>(a, pl, st)
-            : RL == 4 ? launch_scan<4, LIRA_METRIC_IP>(a, pl, st) : launch_scan<8, LIRA_METRIC_IP>(a, pl, st);
+    // Two phases when the pruning bound is on: every query's first m probe
+    // slots (its nearest partitions, where most of its top-k lives) are scanned
+    // first and publish tight bounds; the other slots then admit few survivors.
+    // m = ceil(32 * n_lists / nq) would keep phase 1's 32-query blocks full on
+    // average; only m = 1 measured faster (SIFT1M +1%, DEEP10M +7%; GIST1M
+    // with m = 5 -18%, BIGANN with m = 4 -4%: partly filled blocks and a
+    // second tail cost more than the pruning saves where selection is cheap).
+    // Each pair is planned and scanned in exactly one phase; the partial lists
+    // and chunk counts are the same as one pass, so the merge is unchanged.
+    static const bool two_phase_env = [] {
+        const char *e = getenv("LIRA_SCAN_TWO_PHASE");
+        return !(e && e[0] == '0');
+    }();
+    const int64_t m1 = (kQT * (int64_t)nl + nq - 1) / nq;
+    const bool two = qbound && two_phase_env && m1 == 1 && nprobe >= 2;
+    hipError_t e = hipSuccess;
+    for (int ph = 0; ph < (two ? 2 : 1) && e == hipSuccess; ++ph) {
+        const int slo = two && ph == 1 ? (int)m1 : 0;
+        const int shi = two && ph == 0 ? (int)m1 : (int)nprobe;
+        if (ph > 0) LIRA_HIP_TRY(hipMemsetAsync(w, 0, pl.off_qoff, st));
+        hipLaunchKernelGGL(k_count, dim3(pg), dim3(256), hc, st, probe, npairs, nl, (int)nprobe, slo, shi,
+                           cnt, idx->err);
+        hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, pl.bpc, qoff,
+                           item_off, nch, head);
+        hipLaunchKernelGGL(k_fill, dim3(pg), dim3(256), hf, st, probe, npairs, nl, (int)nprobe, slo, shi,
+                           qoff, cursor, qlist);
+        LIRA_HIP_TRY(hipGetLastError());
+        if (ph == 0 && ev[1]) LIRA_HIP_TRY(hipEventRecord(ev[1], st));  // scan_ms includes phase 2's plan
+        if (idx->metric == LIRA_METRIC_L2)
+            e = RL == 1 ? launch_scan<1, LIRA_METRIC_L2>(a, pl, st)
+                : RL == 2 ? launch_scan<2, LIRA_METRIC_L2>(a, pl, st)
+                : RL == 4 ? launch_scan<4, LIRA_METRIC_L2>(a, pl, st) : launch_scan<8, LIRA_METRIC_L2>(a, pl, st);
+        else
+            e = RL == 1 ? launch_scan<1, LIRA_METRIC_IP>(a, pl, st)
+                : RL == 2 ? launch_scan<2, LIRA_METRIC_IP>(a, pl, st)
+                : RL == 4 ? launch_scan<4, LIRA_METRIC_IP>(a, pl, st) : launch_scan<8, LIRA_METRIC_IP>(a, pl, st);
+    }
     if (e != hipSuccess) return fail(LIRA_EHIP, std::string("k_scan launch: ") + hipGetErrorString(e));
     if (ev[2]) LIRA_HIP_TRY(hipEventRecord(ev[2], st));
 

@@ -176,3 +176,18 @@ def test_device_csr_builder_matches_search_cpp():
     bad[5, 0] = b
     with pytest.raises(LiraError, match="out of range"):
         PartitionedIndex(12, "L2").build(torch.from_numpy(bad).cuda(), torch.from_numpy(x).cuda(), b)
+
+
+@pytest.mark.parametrize("metric,k,red", [("L2", 10, 0.3), ("inner_product", 100, 0.3), ("L2", 64, 0.0)])
+def test_two_phase_pruned_scan(metric, k, red):
+    # >= 32 queries per partition: the scan runs the first probe slot as its own
+    # phase and prunes the rest against the published per-query bounds
+    x, q, d2b, probe = random_case(300 + k, 20000, 40, 6, 600, 4, metric, red=red)
+    check_vs_oracle(x, q, d2b, probe, 6, k, metric, dedup=True)
+    check_vs_oracle(x, q, d2b, probe, 6, k, metric, dedup=False)
+    idx = make_index(x, d2b, 6, metric)
+    off, ids = oracle.build_csr(d2b, 6)
+    met = oracle.IP if metric == "inner_product" else oracle.L2
+    Dp, Ip, _ = oracle.scan_per_partition(q, off, ids, oracle.gather_lists(x, off, ids), probe, k, met)
+    D, I, _ = run(idx, q, probe, k, per_partition=True, dedup=False)
+    assert np.array_equal(I, Ip) and np.array_equal(bits(D), bits(Dp))
