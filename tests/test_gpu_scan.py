@@ -188,6 +188,6 @@ def test_two_phase_pruned_scan(metric, k, red):
     idx = make_index(x, d2b, 6, metric)
     off, ids = oracle.build_csr(d2b, 6)
     met = oracle.IP if metric == "inner_product" else oracle.L2
-    Dp, Ip, _ = oracle.scan_per_partition(q, off, ids, oracle.gather_lists(x, off, ids), probe, k, met)
+    Dp, Ip = oracle.scan_per_partition(q, off, ids, oracle.gather_lists(x, off, ids), probe, k, met)
     D, I, _ = run(idx, q, probe, k, per_partition=True, dedup=False)
     assert np.array_equal(I, Ip) and np.array_equal(bits(D), bits(Dp))
