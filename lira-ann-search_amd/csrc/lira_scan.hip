@@ -60,55 +60,64 @@ struct ScanArgs {
     u64 *partial;         // [pair][nch_max][k]
     uint32_t *qbound;     // [nq] f2ord(k-th score) published per query, ~0 = none; NULL = off
     int64_t d, dpad;
-    int n_lists, nprobe, k, bpc, nch_max;
+    int n_lists, n_virt, nprobe, k, bpc, nch_max;
 };
+
+// Work is planned over "virtual partitions" v = group * n_lists + p: with two
+// groups, pairs whose probe slot is < split (each query's nearest partitions)
+// form group 0 and are queued first.  Group of a pair:
+__device__ __forceinline__ int virt_of(int64_t pair, int p, int nprobe, int split, int groups,
+                                       int n_lists) {
+    return groups == 2 && (int)(pair % nprobe) >= split ? n_lists + p : p;
+}
 
 // Pairs per bucket.  With an LDS histogram each block issues one global
 // atomic per touched bucket (80k pairs on 64 buckets: 128 us -> ~5 us).
-// Pairs with probe slot in [slo, shi) only (the two scan phases); every pair
-// is range-checked once, in the phase that owns it.
+// Pairs per virtual partition.
 __global__ __launch_bounds__(256) void k_count(const int32_t *probe, int64_t npairs, int n_lists,
-                                               int nprobe, int slo, int shi, int32_t *cnt,
+                                               int nprobe, int split, int groups, int32_t *cnt,
                                                int32_t *err) {
     extern __shared__ int32_t hist[];
-    const bool lds = n_lists <= kHistMax;
+    const int n_virt = groups * n_lists;
+    const bool lds = n_virt <= kHistMax;
     const int64_t s = (int64_t)blockIdx.x * kPairsPerBlock;
     const int64_t e = min<int64_t>(npairs, s + kPairsPerBlock);
     if (lds) {
-        for (int b = threadIdx.x; b < n_lists; b += blockDim.x) hist[b] = 0;
+        for (int b = threadIdx.x; b < n_virt; b += blockDim.x) hist[b] = 0;
         __syncthreads();
     }
     for (int64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
-        const int sl = (int)(i % nprobe);
-        if (sl < slo || sl >= shi) continue;
         int p = probe[i];
         if (p >= n_lists) {
             atomicOr(err, 1);
             continue;
         }
-        if (p >= 0) atomicAdd(lds ? &hist[p] : &cnt[p], 1);
+        if (p < 0) continue;
+        const int v = virt_of(i, p, nprobe, split, groups, n_lists);
+        atomicAdd(lds ? &hist[v] : &cnt[v], 1);
     }
     if (lds) {
         __syncthreads();
-        for (int b = threadIdx.x; b < n_lists; b += blockDim.x)
+        for (int b = threadIdx.x; b < n_virt; b += blockDim.x)
             if (hist[b]) atomicAdd(&cnt[b], hist[b]);
     }
 }
 
 // One workgroup of 1024 threads: exclusive scans over the buckets.
 __global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t *tile_off,
-                                               int n_lists, int bpc, int32_t *qoff,
+                                               int n_lists, int n_virt, int bpc, int32_t *qoff,
                                                int32_t *item_off, int32_t *nch, int32_t *head) {
     __shared__ int32_t s_a[1024], s_b[1024];
     __shared__ int32_t carry_a, carry_b;
     if (threadIdx.x == 0) carry_a = carry_b = 0;
     __syncthreads();
-    for (int base = 0; base < n_lists; base += 1024) {
+    for (int base = 0; base < n_virt; base += 1024) {
         int p = base + threadIdx.x;
         int c = 0, items = 0;
-        if (p < n_lists) {
+        if (p < n_virt) {
             c = cnt[p];
-            int ntl = tile_off[p + 1] - tile_off[p];
+            const int pp = p >= n_lists ? p - n_lists : p;
+            int ntl = tile_off[pp + 1] - tile_off[pp];
             int nblk = (ntl + kBlockTiles - 1) / kBlockTiles;
             int nc = (nblk + bpc - 1) / bpc;
             nch[p] = nc;
@@ -125,7 +134,7 @@ __global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t
             s_b[threadIdx.x] += vb;
             __syncthreads();
         }
-        if (p < n_lists) {
+        if (p < n_virt) {
             qoff[p] = carry_a + s_a[threadIdx.x] - c;
             item_off[p] = carry_b + s_b[threadIdx.x] - items;
         }
@@ -137,8 +146,8 @@ __global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        qoff[n_lists] = carry_a;
-        item_off[n_lists] = carry_b;
+        qoff[n_virt] = carry_a;
+        item_off[n_virt] = carry_b;
         head[0] = 0;
         head[1] = carry_b;
     }
@@ -148,40 +157,40 @@ __global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t
 // (global atomic), then places its pairs by LDS-atomic rank.  The order inside
 // a bucket's list is arbitrary; results do not depend on it.
 __global__ __launch_bounds__(256) void k_fill(const int32_t *probe, int64_t npairs, int n_lists,
-                                              int nprobe, int slo, int shi, const int32_t *qoff,
+                                              int nprobe, int split, int groups, const int32_t *qoff,
                                               int32_t *cursor, int32_t *qlist) {
     extern __shared__ int32_t sh[];
-    const bool lds = n_lists <= kHistMax / 2;
-    int32_t *hist = sh, *base = sh + (lds ? n_lists : 0);
+    const int n_virt = groups * n_lists;
+    const bool lds = n_virt <= kHistMax / 2;
+    int32_t *hist = sh, *base = sh + (lds ? n_virt : 0);
     const int64_t s = (int64_t)blockIdx.x * kPairsPerBlock;
     const int64_t e = min<int64_t>(npairs, s + kPairsPerBlock);
     if (!lds) {
         for (int64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
-            const int sl = (int)(i % nprobe);
             int p = probe[i];
-            if (sl < slo || sl >= shi || p < 0 || p >= n_lists) continue;
-            qlist[qoff[p] + atomicAdd(&cursor[p], 1)] = (int32_t)i;
+            if (p < 0 || p >= n_lists) continue;
+            const int v = virt_of(i, p, nprobe, split, groups, n_lists);
+            qlist[qoff[v] + atomicAdd(&cursor[v], 1)] = (int32_t)i;
         }
         return;
     }
-    for (int b = threadIdx.x; b < n_lists; b += blockDim.x) hist[b] = 0;
+    for (int b = threadIdx.x; b < n_virt; b += blockDim.x) hist[b] = 0;
     __syncthreads();
     for (int64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
-        const int sl = (int)(i % nprobe);
         int p = probe[i];
-        if (sl >= slo && sl < shi && p >= 0 && p < n_lists) atomicAdd(&hist[p], 1);
+        if (p >= 0 && p < n_lists) atomicAdd(&hist[virt_of(i, p, nprobe, split, groups, n_lists)], 1);
     }
     __syncthreads();
-    for (int b = threadIdx.x; b < n_lists; b += blockDim.x) {
+    for (int b = threadIdx.x; b < n_virt; b += blockDim.x) {
         base[b] = hist[b] ? qoff[b] + atomicAdd(&cursor[b], hist[b]) : 0;
         hist[b] = 0;
     }
     __syncthreads();
     for (int64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
-        const int sl = (int)(i % nprobe);
         int p = probe[i];
-        if (sl < slo || sl >= shi || p < 0 || p >= n_lists) continue;
-        qlist[base[p] + atomicAdd(&hist[p], 1)] = (int32_t)i;
+        if (p < 0 || p >= n_lists) continue;
+        const int v = virt_of(i, p, nprobe, split, groups, n_lists);
+        qlist[base[v] + atomicAdd(&hist[v], 1)] = (int32_t)i;
     }
 }
 
@@ -270,7 +279,7 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
             int ok = item < n_items;
             int p = 0, qb = 0, ch = 0;
             if (ok) {
-                int lo = 0, hi = a.n_lists - 1;  // last p with item_off[p] <= item
+                int lo = 0, hi = a.n_virt - 1;  // last virtual partition with item_off <= item
                 while (lo < hi) {
                     int mid = (lo + hi + 1) >> 1;
                     if (a.item_off[mid] <= item) lo = mid; else hi = mid - 1;
@@ -288,11 +297,12 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
         }
         __syncthreads();
         if (!meta[0]) break;
-        const int p = meta[1], qb = meta[2], ch = meta[3];
+        const int v = meta[1], qb = meta[2], ch = meta[3];
+        const int p = v >= a.n_lists ? v - a.n_lists : v;  // the partition itself
         const int q0 = qb * kQT;
-        const int nqb_valid = min(kQT, a.cnt[p] - q0);
+        const int nqb_valid = min(kQT, a.cnt[v] - q0);
         if (tid < kQT) {
-            meta[8 + tid] = tid < nqb_valid ? a.qlist[a.qoff[p] + q0 + tid] : -1;
+            meta[8 + tid] = tid < nqb_valid ? a.qlist[a.qoff[v] + q0 + tid] : -1;
             meta[64 + tid] = 0;
         }
         for (int i = tid; i < kQT * k; i += kScanThreads) lists[i] = kEmptyKey;
@@ -749,13 +759,13 @@ static ScanPlan make_plan(const lira_index *idx, int64_t nq, int64_t nprobe, int
         o += (bytes + 255) & ~size_t(255);
         return at;
     };
-    const size_t nl = (size_t)idx->n_lists;
-    pl.off_cnt = take(nl * 4);
-    pl.off_cursor = take(nl * 4);
+    const size_t nv = 2 * (size_t)idx->n_lists;  // virtual partitions (two groups)
+    pl.off_cnt = take(nv * 4);
+    pl.off_cursor = take(nv * 4);
     pl.off_head = take(16);
-    pl.off_qoff = take((nl + 1) * 4);
-    pl.off_item = take((nl + 1) * 4);
-    pl.off_nch = take(nl * 4);
+    pl.off_qoff = take((nv + 1) * 4);
+    pl.off_item = take((nv + 1) * 4);
+    pl.off_nch = take(nv * 4);
     pl.off_qlist = take((size_t)npairs * 4);
     pl.off_partial = take((size_t)npairs * pl.nch_max * (size_t)k * 8);
     pl.off_qbound = take((size_t)nq * 4);
@@ -843,9 +853,31 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
     if (qbound) LIRA_HIP_TRY(hipMemsetAsync(qbound, 0xff, (size_t)nq * 4, st));
     const int64_t npairs = nq * nprobe;
     const int nl = (int)idx->n_lists;
+    // Two groups when the pruning bound is on and partitions get >= 32 queries:
+    // every query's first probe slot (its nearest partition, where most of its
+    // top-k lives) is queued ahead of the other slots, so those start with a
+    // tight published bound (measured: they then admit almost no survivors).
+    // One launch, so there is no tail between the groups.  With m = ceil(32 *
+    // n_lists / nq) > 1 first-slot blocks would be part-filled; measured slower
+    // there (GIST1M, BIGANN), so one group.
+    static const bool two_group_env = [] {
+        const char *e = getenv("LIRA_SCAN_TWO_PHASE");
+        return !(e && e[0] == '0');
+    }();
+    const int64_t m1 = (kQT * (int64_t)nl + nq - 1) / nq;
+    const int groups = qbound && two_group_env && m1 == 1 && nprobe >= 2 ? 2 : 1;
+    const int split = 1;
+    const int nv = groups * nl;
     const unsigned pg = (unsigned)((npairs + kPairsPerBlock - 1) / kPairsPerBlock);
-    const size_t hc = nl <= kHistMax ? (size_t)nl * 4 : 0;
-    const size_t hf = nl <= kHistMax / 2 ? (size_t)nl * 8 : 0;
+    const size_t hc = nv <= kHistMax ? (size_t)nv * 4 : 0;
+    const size_t hf = nv <= kHistMax / 2 ? (size_t)nv * 8 : 0;
+    hipLaunchKernelGGL(k_count, dim3(pg), dim3(256), hc, st, probe, npairs, nl, (int)nprobe, split, groups,
+                       cnt, idx->err);
+    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, nv, pl.bpc, qoff,
+                       item_off, nch, head);
+    hipLaunchKernelGGL(k_fill, dim3(pg), dim3(256), hf, st, probe, npairs, nl, (int)nprobe, split, groups,
+                       qoff, cursor, qlist);
+    LIRA_HIP_TRY(hipGetLastError());
 
     ScanArgs a;
     a.Q = q;
@@ -863,47 +895,21 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
     a.d = idx->d;
     a.dpad = idx->dpad;
     a.n_lists = nl;
+    a.n_virt = nv;
     a.nprobe = (int)nprobe;
     a.k = (int)k;
     a.bpc = pl.bpc;
     a.nch_max = pl.nch_max;
-    // Two phases when the pruning bound is on: every query's first m probe
-    // slots (its nearest partitions, where most of its top-k lives) are scanned
-    // first and publish tight bounds; the other slots then admit few survivors.
-    // m = ceil(32 * n_lists / nq) would keep phase 1's 32-query blocks full on
-    // average; only m = 1 measured faster (SIFT1M +1%, DEEP10M +7%; GIST1M
-    // with m = 5 -18%, BIGANN with m = 4 -4%: partly filled blocks and a
-    // second tail cost more than the pruning saves where selection is cheap).
-    // Each pair is planned and scanned in exactly one phase; the partial lists
-    // and chunk counts are the same as one pass, so the merge is unchanged.
-    static const bool two_phase_env = [] {
-        const char *e = getenv("LIRA_SCAN_TWO_PHASE");
-        return !(e && e[0] == '0');
-    }();
-    const int64_t m1 = (kQT * (int64_t)nl + nq - 1) / nq;
-    const bool two = qbound && two_phase_env && m1 == 1 && nprobe >= 2;
-    hipError_t e = hipSuccess;
-    for (int ph = 0; ph < (two ? 2 : 1) && e == hipSuccess; ++ph) {
-        const int slo = two && ph == 1 ? (int)m1 : 0;
-        const int shi = two && ph == 0 ? (int)m1 : (int)nprobe;
-        if (ph > 0) LIRA_HIP_TRY(hipMemsetAsync(w, 0, pl.off_qoff, st));
-        hipLaunchKernelGGL(k_count, dim3(pg), dim3(256), hc, st, probe, npairs, nl, (int)nprobe, slo, shi,
-                           cnt, idx->err);
-        hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, pl.bpc, qoff,
-                           item_off, nch, head);
-        hipLaunchKernelGGL(k_fill, dim3(pg), dim3(256), hf, st, probe, npairs, nl, (int)nprobe, slo, shi,
-                           qoff, cursor, qlist);
-        LIRA_HIP_TRY(hipGetLastError());
-        if (ph == 0 && ev[1]) LIRA_HIP_TRY(hipEventRecord(ev[1], st));  // scan_ms includes phase 2's plan
-        if (idx->metric == LIRA_METRIC_L2)
-            e = RL == 1 ? launch_scan<1, LIRA_METRIC_L2>(a, pl, st)
-                : RL == 2 ? launch_scan<2, LIRA_METRIC_L2>(a, pl, st)
-                : RL == 4 ? launch_scan<4, LIRA_METRIC_L2>(a, pl, st) : launch_scan<8, LIRA_METRIC_L2>(a, pl, st);
-        else
-            e = RL == 1 ? launch_scan<1, LIRA_METRIC_IP>(a, pl, st)
-                : RL == 2 ? launch_scan<2, LIRA_METRIC_IP>(a, pl, st)
-                : RL == 4 ? launch_scan<4, LIRA_METRIC_IP>(a, pl, st) : launch_scan<8, LIRA_METRIC_IP>(a, pl, st);
-    }
+    if (ev[1]) LIRA_HIP_TRY(hipEventRecord(ev[1], st));
+    hipError_t e;
+    if (idx->metric == LIRA_METRIC_L2)
+        e = RL == 1 ? launch_scan<1, LIRA_METRIC_L2>(a, pl, st)
+            : RL == 2 ? launch_scan<2, LIRA_METRIC_L2>(a, pl, st)
+            : RL == 4 ? launch_scan<4, LIRA_METRIC_L2>(a, pl, st) : launch_scan<8, LIRA_METRIC_L2>(a, pl, st);
+    else
+        e = RL == 1 ? launch_scan<1, LIRA_METRIC_IP>(a, pl, st)
+            : RL == 2 ? launch_scan<2, LIRA_METRIC_IP>(a, pl, st)
+            : RL == 4 ? launch_scan<4, LIRA_METRIC_IP>(a, pl, st) : launch_scan<8, LIRA_METRIC_IP>(a, pl, st);
     if (e != hipSuccess) return fail(LIRA_EHIP, std::string("k_scan launch: ") + hipGetErrorString(e));
     if (ev[2]) LIRA_HIP_TRY(hipEventRecord(ev[2], st));
 
