@@ -45,6 +45,8 @@ extern "C" {
 /* lira_scan_topk flags */
 #define LIRA_SCAN_DEDUP 1u         /* keep each gid once (search.cpp:496-514 does not: Appendix A) */
 #define LIRA_SCAN_PER_PARTITION 2u /* k best of every probed slot on its own (LIRA_smallscale.py:145-174) */
+#define LIRA_SCAN_FMA 4u           /* fused multiply-add accumulation: fewer ops, NOT bit-exact (SURVEY 7
+                                      "tolerance fallback": 1e-4 relative, ties may order differently) */
 
 /* lira_select_probes modes */
 #define LIRA_PROBE_NEAREST 0      /* nprobe smallest values, ties -> smaller bucket (IVF nprobe) */
@@ -166,12 +168,13 @@ int lira_select_probes(const float *scores, int64_t n, int64_t n_centroids, int 
  *   q          device fp32 (nq, d)
  *   probe      device int32 (nq, nprobe_max), -1 = unused slot
  *   k          1..256
- *   flags      LIRA_SCAN_DEDUP | LIRA_SCAN_PER_PARTITION
+ *   flags      LIRA_SCAN_DEDUP | LIRA_SCAN_PER_PARTITION | LIRA_SCAN_FMA
  *   out_D      device fp32  (nq, k)  or (nq, nprobe_max, k) with PER_PARTITION
  *   out_I      device int64 (nq, k)  or (nq, nprobe_max, k) with PER_PARTITION
  *   out_ncand  device int64 (nq) or NULL: search.cpp's cmp_for_query
  *              (candidates scanned, replicas included, search.cpp:468-477)
- * Distances are bit-identical to search.cpp's sequential fp32 l2_sq / ip.
+ * Distances are bit-identical to search.cpp's sequential fp32 l2_sq / ip
+ * (without LIRA_SCAN_FMA; with it, fma(q-x, q-x, acc) / fma(q, x, acc)).
  * Order: faiss convention -- L2 ascending squared distance, IP descending
  * inner product; ties -> smaller gid; pads (+inf, -1) for L2, (-inf, -1) IP.
  * workspace: device, >= lira_scan_workspace_size() bytes, or NULL to use a

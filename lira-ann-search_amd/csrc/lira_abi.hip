@@ -284,7 +284,7 @@ int lira_scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *p
     if (idx->n_lists == 0) return fail(LIRA_ESTATE, "index has no lists (add_partitions first)");
     if (nq < 0 || nprobe_max <= 0) return fail(LIRA_EINVAL, "need nq >= 0 and nprobe_max > 0");
     if (k <= 0 || k > 256) return fail(LIRA_EUNSUPPORTED, "k must be in [1, 256]");
-    if (flags & ~(LIRA_SCAN_DEDUP | LIRA_SCAN_PER_PARTITION)) return fail(LIRA_EINVAL, "unknown flags");
+    if (flags & ~(LIRA_SCAN_DEDUP | LIRA_SCAN_PER_PARTITION | LIRA_SCAN_FMA)) return fail(LIRA_EINVAL, "unknown flags");
     if (nq > 0 && (!q || !probe || !out_D || !out_I)) return fail(LIRA_EINVAL, "NULL buffer");
     DeviceGuard g(idx->device);
     return scan_topk(idx, q, nq, probe, nprobe_max, k, flags, out_D, out_I, out_ncand, workspace,

@@ -252,8 +252,8 @@ __device__ __forceinline__ void flush_rows(u64 *L, const u64 *buf, int n, int k,
 }
 
 // RL: half-wave list registers, 32*RL >= k.  OCC: workgroups per CU the
-// register budget is built for.
-template <int RL, int METRIC, int OCC>
+// register budget is built for.  FMA: LIRA_SCAN_FMA accumulation (not exact).
+template <int RL, int METRIC, int OCC, bool FMA>
 __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     typedef ScanSmem S;
@@ -408,7 +408,19 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
                     q4 = *(const float4 *)(qp + (j + 1) * kQT);
                     xa = *(const float4 *)(xpa + (j + 1) * kTile);
                     xb = *(const float4 *)(xpb + (j + 1) * kTile);
-                    if (METRIC == LIRA_METRIC_L2) {
+                    if (METRIC == LIRA_METRIC_L2 && FMA) {
+                        float df[4][8];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+#pragma unroll
+                            for (int v = 0; v < 8; ++v) df[u][v] = qv[u] - xv[v];
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+#pragma unroll
+                            for (int v = 0; v < 8; ++v) acc[u][v] = __builtin_fmaf(df[u][v], df[u][v], acc[u][v]);
+                        __builtin_amdgcn_sched_barrier(0);
+                    } else if (METRIC == LIRA_METRIC_L2) {
                         float df[4][8];
 #pragma unroll
                         for (int u = 0; u < 4; ++u)
@@ -424,6 +436,12 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
                         for (int u = 0; u < 4; ++u)
 #pragma unroll
                             for (int v = 0; v < 8; ++v) acc[u][v] = acc[u][v] + df[u][v];
+                        __builtin_amdgcn_sched_barrier(0);
+                    } else if (FMA) {
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+#pragma unroll
+                            for (int v = 0; v < 8; ++v) acc[u][v] = __builtin_fmaf(qv[u], xv[v], acc[u][v]);
                         __builtin_amdgcn_sched_barrier(0);
                     } else {
                         float pr[4][8];
@@ -773,18 +791,25 @@ static ScanPlan make_plan(const lira_index *idx, int64_t nq, int64_t nprobe, int
     return pl;
 }
 
-template <int RL, int M>
+template <int RL, int M, bool FMA>
 static hipError_t launch_scan(const ScanArgs &a, const ScanPlan &pl, hipStream_t st) {
     constexpr int OCC = ScanOcc<RL>::value;
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void *)k_scan<RL, M, OCC>,
+        hipError_t e = hipFuncSetAttribute((const void *)k_scan<RL, M, OCC, FMA>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((k_scan<RL, M, OCC>), dim3(pl.grid), dim3(kScanThreads), pl.smem, st, a);
+    hipLaunchKernelGGL((k_scan<RL, M, OCC, FMA>), dim3(pl.grid), dim3(kScanThreads), pl.smem, st, a);
     return hipGetLastError();
+}
+
+template <int M, bool FMA>
+static hipError_t launch_scan_rl(int RL, const ScanArgs &a, const ScanPlan &pl, hipStream_t st) {
+    return RL == 1 ? launch_scan<1, M, FMA>(a, pl, st)
+           : RL == 2 ? launch_scan<2, M, FMA>(a, pl, st)
+           : RL == 4 ? launch_scan<4, M, FMA>(a, pl, st) : launch_scan<8, M, FMA>(a, pl, st);
 }
 
 template <int R>
@@ -901,15 +926,14 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
     a.bpc = pl.bpc;
     a.nch_max = pl.nch_max;
     if (ev[1]) LIRA_HIP_TRY(hipEventRecord(ev[1], st));
+    const bool fma = (flags & LIRA_SCAN_FMA) != 0;
     hipError_t e;
     if (idx->metric == LIRA_METRIC_L2)
-        e = RL == 1 ? launch_scan<1, LIRA_METRIC_L2>(a, pl, st)
-            : RL == 2 ? launch_scan<2, LIRA_METRIC_L2>(a, pl, st)
-            : RL == 4 ? launch_scan<4, LIRA_METRIC_L2>(a, pl, st) : launch_scan<8, LIRA_METRIC_L2>(a, pl, st);
+        e = fma ? launch_scan_rl<LIRA_METRIC_L2, true>(RL, a, pl, st)
+                : launch_scan_rl<LIRA_METRIC_L2, false>(RL, a, pl, st);
     else
-        e = RL == 1 ? launch_scan<1, LIRA_METRIC_IP>(a, pl, st)
-            : RL == 2 ? launch_scan<2, LIRA_METRIC_IP>(a, pl, st)
-            : RL == 4 ? launch_scan<4, LIRA_METRIC_IP>(a, pl, st) : launch_scan<8, LIRA_METRIC_IP>(a, pl, st);
+        e = fma ? launch_scan_rl<LIRA_METRIC_IP, true>(RL, a, pl, st)
+                : launch_scan_rl<LIRA_METRIC_IP, false>(RL, a, pl, st);
     if (e != hipSuccess) return fail(LIRA_EHIP, std::string("k_scan launch: ") + hipGetErrorString(e));
     if (ev[2]) LIRA_HIP_TRY(hipEventRecord(ev[2], st));
 

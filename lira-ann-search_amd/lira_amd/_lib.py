@@ -19,6 +19,7 @@ LIRA_METRIC_L2 = 0
 LIRA_METRIC_IP = 1
 LIRA_SCAN_DEDUP = 1
 LIRA_SCAN_PER_PARTITION = 2
+LIRA_SCAN_FMA = 4
 LIRA_PROBE_NEAREST = 0
 LIRA_PROBE_THRESHOLD_GE = 1
 LIRA_PROBE_THRESHOLD_GT = 2

@@ -176,13 +176,16 @@ class PartitionedIndex:
 
     # --------------------------------------------------------------- search
     def search(self, q: torch.Tensor, probe: torch.Tensor, k: int, dedup: bool = True,
-               per_partition: bool = False, out=None, stream=None):
+               per_partition: bool = False, out=None, stream=None, fma: bool = False):
         """Scan the probed lists of every query; exact top-k.
 
         q (nq, d) fp32, probe (nq, nprobe_max) int32 (-1 = unused slot).
         Returns (D, I, ncand) device tensors: D/I (nq, k) -- or
         (nq, nprobe_max, k) with per_partition -- and ncand (nq,) int64, the
         candidates scanned per query (search.cpp's cmp_for_query).
+        Distances are search.cpp's sequential fp32 sums bit for bit; fma=True
+        accumulates with fused multiply-adds instead (LIRA_SCAN_FMA: fewer
+        operations, ~1e-6 relative difference, near-ties may order differently).
         """
         q = _dev(q, torch.float32, self.device)
         probe = _dev(probe, torch.int32, self.device)
@@ -202,7 +205,8 @@ class PartitionedIndex:
         else:
             D, I, ncand = out
         flags = (_lib.LIRA_SCAN_DEDUP if dedup else 0) | \
-            (_lib.LIRA_SCAN_PER_PARTITION if per_partition else 0)
+            (_lib.LIRA_SCAN_PER_PARTITION if per_partition else 0) | \
+            (_lib.LIRA_SCAN_FMA if fma else 0)
         with torch.cuda.device(self.device):
             _lib.call("lira_scan_topk", self._h, _lib.ptr(q), nq, _lib.ptr(probe), npm, int(k),
                       flags, _lib.ptr(D), _lib.ptr(I), _lib.ptr(ncand), None, 0,

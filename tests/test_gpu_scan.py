@@ -191,3 +191,32 @@ def test_two_phase_pruned_scan(metric, k, red):
     Dp, Ip = oracle.scan_per_partition(q, off, ids, oracle.gather_lists(x, off, ids), probe, k, met)
     D, I, _ = run(idx, q, probe, k, per_partition=True, dedup=False)
     assert np.array_equal(I, Ip) and np.array_equal(bits(D), bits(Dp))
+
+
+@pytest.mark.parametrize("metric,k", [("L2", 10), ("inner_product", 10), ("L2", 100), ("inner_product", 100)])
+def test_fma_variant_within_tolerance(metric, k):
+    # LIRA_SCAN_FMA (SURVEY 7 tolerance fallback): distances within 1e-4
+    # relative of search.cpp's; every returned id is a valid top-k member up to
+    # that tolerance (tie-aware), and ids agree wherever the oracle's distances
+    # are not near-tied.
+    x, q, d2b, probe = random_case(400 + k, 20000, 96, 8, 300, 4, metric, red=0.1)
+    idx = make_index(x, d2b, 8, metric)
+    off, ids = oracle.build_csr(d2b, 8)
+    met = oracle.IP if metric == "inner_product" else oracle.L2
+    Do, Io, nco = oracle.scan_topk(q, off, ids, oracle.gather_lists(x, off, ids), probe, k, met, idx.max_replicas)
+    Dk1 = oracle.scan_topk(q, off, ids, oracle.gather_lists(x, off, ids), probe, k + 1, met, idx.max_replicas)[0]
+    D, I, nc = run(idx, q, probe, k, fma=True)
+    assert np.array_equal(nc, nco)
+    tol = 1e-4
+    assert np.all(np.abs(D - Do) <= tol * np.maximum(np.abs(Do), 1e-6))
+    sign = -1.0 if metric == "inner_product" else 1.0
+    for r in range(q.shape[0]):
+        kth = sign * Do[r, -1]
+        assert len(set(I[r])) == k
+        # exact distance of each returned id (oracle arithmetic) within tolerance of the k-th
+        ex = oracle.scan_topk(q[r:r + 1], np.array([0, len(I[r])], np.int64), I[r].astype(np.int32),
+                              x[I[r]], np.zeros((1, 1), np.int32), k, met, 0)[0][0]
+        assert np.all(sign * ex <= kth + tol * abs(kth) + 1e-6)
+        gap = np.abs(np.diff(Dk1[r])) > tol * np.maximum(np.abs(Dk1[r, 1:]), 1e-6)
+        if gap.all():  # no near-tie inside the top k nor at its boundary
+            assert np.array_equal(I[r], Io[r])
