@@ -759,7 +759,7 @@ static ScanPlan make_plan(const lira_index *idx, int64_t nq, int64_t nprobe, int
     // fraction of the run (the tail); LIRA_SCAN_ROUNDS overrides (tuning).
     static const int rounds = [] {
         const char *e = getenv("LIRA_SCAN_ROUNDS");
-        return e && atoi(e) > 0 ? atoi(e) : 8;
+        return e && atoi(e) > 0 ? atoi(e) : 16;
     }();
     const int64_t target = (int64_t)rounds * pl.grid;
     const int64_t est_items = (npairs + kQT - 1) / kQT + std::min<int64_t>(idx->n_lists, npairs);
