@@ -52,50 +52,91 @@ __global__ __launch_bounds__(256) void k_centroid_dist(const float *__restrict__
 // Workgroup = 4 waves = 64 queries x 64 centroids; wave (wr, wc) owns a 32x32
 // accumulator of v_mfma_f32_32x32x2_f32 (A: lane -> row lane&31, k lane>>5;
 // B: k lane>>5, col lane&31; C: col lane&31, row (r&3)+8(r>>2)+4(lane>>5)).
-// Operands are staged through LDS in 32-dim chunks (padded rows, no conflicts).
+// Operands go through LDS in 64-dim chunks, loaded as coalesced float4 (16
+// lanes per 256-B row segment; VEC = d % 4 == 0, else scalar loads).  The
+// squared norms are accumulated in registers from the same loads (each thread
+// owns 4 query rows and 4 centroid rows x 4 dims of a chunk) and reduced over
+// the 16 lanes of a row at the end -- no serial pass over LDS.
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+static constexpr int kGK = 64;        // dims per LDS chunk
+static constexpr int kGLd = kGK + 2;  // padded row: the MFMA reads (32 rows x 2 dims) hit 64 banks
 
+template <bool VEC>
 __global__ __launch_bounds__(256) void k_centroid_gemm(const float *__restrict__ q, int64_t nq,
                                                        const float *__restrict__ cent, int nb,
                                                        int64_t d, float *out_sq, float *out_err) {
-    __shared__ float Qs[64][33];
-    __shared__ float Cs[64][33];
+    __shared__ __attribute__((aligned(16))) float Qs[64 * kGLd];
+    __shared__ __attribute__((aligned(16))) float Cs[64 * kGLd];  // 8-B aligned rows
     __shared__ float nrm[128];  // [0,64) query norms, [64,128) centroid norms
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wr = w >> 1, wc = w & 1;
     const int64_t q0 = (int64_t)blockIdx.x * 64;
     const int c0 = blockIdx.y * 64;
+    const int lr = tid >> 4, l4 = (tid & 15) * 4;  // load role: rows lr + 16 i, dims l4..l4+3
     f32x16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
-    float nacc = 0.0f;  // thread t<128 accumulates norm of row t
-    for (int64_t k0 = 0; k0 < d; k0 += 32) {
-        __syncthreads();
-        for (int i = tid; i < 64 * 32; i += 256) {
-            int r = i >> 5, kk = i & 31;
-            int64_t k = k0 + kk;
-            int64_t qr = q0 + r;
-            int cr = c0 + r;
-            Qs[r][kk] = (qr < nq && k < d) ? q[qr * d + k] : 0.0f;
-            Cs[r][kk] = (cr < nb && k < d) ? cent[(int64_t)cr * d + k] : 0.0f;
-        }
-        __syncthreads();
-        if (tid < 128) {
-            const float *row = tid < 64 ? Qs[tid] : Cs[tid - 64];
-#pragma unroll 8
-            for (int kk = 0; kk < 32; ++kk) nacc = fmaf(row[kk], row[kk], nacc);
-        }
+    float nq_acc[4] = {0.f, 0.f, 0.f, 0.f}, nc_acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t k0 = 0; k0 < d; k0 += kGK) {
+        float4 vq[4], vc[4];
 #pragma unroll
-        for (int kk = 0; kk < 32; kk += 2) {
-            float a = Qs[wr * 32 + (lane & 31)][kk + (lane >> 5)];
-            float b = Cs[wc * 32 + (lane & 31)][kk + (lane >> 5)];
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+        for (int i = 0; i < 4; ++i) {
+            const int r = lr + 16 * i;
+            const int64_t qr = q0 + r, kk = k0 + l4;
+            const int cr = c0 + r;
+            if (VEC) {
+                vq[i] = qr < nq && kk < d ? *(const float4 *)(q + qr * d + kk) : make_float4(0.f, 0.f, 0.f, 0.f);
+                vc[i] = cr < nb && kk < d ? *(const float4 *)(cent + (int64_t)cr * d + kk)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+            } else {
+                float t[4], u[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    t[e] = qr < nq && kk + e < d ? q[qr * d + kk + e] : 0.f;
+                    u[e] = cr < nb && kk + e < d ? cent[(int64_t)cr * d + kk + e] : 0.f;
+                }
+                vq[i] = make_float4(t[0], t[1], t[2], t[3]);
+                vc[i] = make_float4(u[0], u[1], u[2], u[3]);
+            }
+        }
+        __syncthreads();  // the previous chunk's MFMA reads are done
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = lr + 16 * i;
+            *(float2 *)&Qs[r * kGLd + l4] = make_float2(vq[i].x, vq[i].y);
+            *(float2 *)&Qs[r * kGLd + l4 + 2] = make_float2(vq[i].z, vq[i].w);
+            *(float2 *)&Cs[r * kGLd + l4] = make_float2(vc[i].x, vc[i].y);
+            *(float2 *)&Cs[r * kGLd + l4 + 2] = make_float2(vc[i].z, vc[i].w);
+            nq_acc[i] = fmaf(vq[i].x, vq[i].x, fmaf(vq[i].y, vq[i].y, fmaf(vq[i].z, vq[i].z, fmaf(vq[i].w, vq[i].w, nq_acc[i]))));
+            nc_acc[i] = fmaf(vc[i].x, vc[i].x, fmaf(vc[i].y, vc[i].y, fmaf(vc[i].z, vc[i].z, fmaf(vc[i].w, vc[i].w, nc_acc[i]))));
+        }
+        __syncthreads();
+        const float *qa = Qs + (wr * 32 + (lane & 31)) * kGLd + (lane >> 5);
+        const float *cb_ = Cs + (wc * 32 + (lane & 31)) * kGLd + (lane >> 5);
+#pragma unroll
+        for (int kk = 0; kk < kGK; kk += 2)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qa[kk], cb_[kk], acc, 0, 0, 0);
+    }
+    // row norms: reduce over the 16 lanes that loaded a row
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            nq_acc[i] += __shfl_xor(nq_acc[i], o);
+            nc_acc[i] += __shfl_xor(nc_acc[i], o);
         }
     }
-    if (tid < 128) nrm[tid] = nacc;
+    if ((tid & 15) == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            nrm[lr + 16 * i] = nq_acc[i];
+            nrm[64 + lr + 16 * i] = nc_acc[i];
+        }
+    }
     __syncthreads();
     // |A - R| <= (2 gamma_d + 4u)(nq + nc) and |E - R| <= 2 gamma_{d+3}(nq + nc)
-    // (R real, E = search.cpp's sequential sum), so |A - E| <= (4d + 10)u(nq + nc);
+    // (R real, E = search.cpp's sequential sum; any summation order of the
+    // norms and the dot stays within gamma_d), so |A - E| <= (4d + 10)u(nq + nc);
     // 8(d+8)u leaves room for sqrt() merging nearby E values into one float.
     const float ebound = 8.0f * (float)(d + 8) * 5.9604645e-08f;
     const int col = lane & 31;
@@ -277,8 +318,12 @@ int lira_centroid_gemm(const float *q, int64_t nq, const float *centroids, int64
     hipStream_t st = (hipStream_t)stream;
     if (out_err) LIRA_HIP_TRY(hipMemsetAsync(out_err, 0, nq * 4, st));
     dim3 grid((unsigned)((nq + 63) / 64), (unsigned)((n_centroids + 63) / 64));
-    hipLaunchKernelGGL(k_centroid_gemm, grid, dim3(256), 0, st, q, nq, centroids,
-                       (int)n_centroids, d, out_sq, out_err);
+    if (d % 4 == 0 && ((uintptr_t)q & 15) == 0 && ((uintptr_t)centroids & 15) == 0)
+        hipLaunchKernelGGL(k_centroid_gemm<true>, grid, dim3(256), 0, st, q, nq, centroids,
+                           (int)n_centroids, d, out_sq, out_err);
+    else
+        hipLaunchKernelGGL(k_centroid_gemm<false>, grid, dim3(256), 0, st, q, nq, centroids,
+                           (int)n_centroids, d, out_sq, out_err);
     LIRA_HIP_TRY(hipGetLastError());
     return LIRA_OK;
 }
