@@ -47,6 +47,8 @@ extern "C" {
 #define LIRA_SCAN_PER_PARTITION 2u /* k best of every probed slot on its own (LIRA_smallscale.py:145-174) */
 #define LIRA_SCAN_FMA 4u           /* fused multiply-add accumulation: fewer ops, NOT bit-exact (SURVEY 7
                                       "tolerance fallback": 1e-4 relative, ties may order differently) */
+#define LIRA_SCAN_NO_PRUNE 8u      /* L2: compute every candidate to the last dim (no early abandon of
+                                      pairs already past the k-th score); same results, for A/B */
 
 /* lira_select_probes modes */
 #define LIRA_PROBE_NEAREST 0      /* nprobe smallest values, ties -> smaller bucket (IVF nprobe) */
@@ -168,7 +170,7 @@ int lira_select_probes(const float *scores, int64_t n, int64_t n_centroids, int 
  *   q          device fp32 (nq, d)
  *   probe      device int32 (nq, nprobe_max), -1 = unused slot
  *   k          1..256
- *   flags      LIRA_SCAN_DEDUP | LIRA_SCAN_PER_PARTITION | LIRA_SCAN_FMA
+ *   flags      LIRA_SCAN_DEDUP | LIRA_SCAN_PER_PARTITION | LIRA_SCAN_FMA | LIRA_SCAN_NO_PRUNE
  *   out_D      device fp32  (nq, k)  or (nq, nprobe_max, k) with PER_PARTITION
  *   out_I      device int64 (nq, k)  or (nq, nprobe_max, k) with PER_PARTITION
  *   out_ncand  device int64 (nq) or NULL: search.cpp's cmp_for_query
@@ -196,6 +198,17 @@ int lira_scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *p
 int lira_index_set_profiling(lira_index *idx, int enable);
 int lira_index_profile_read(lira_index *idx, double *plan_ms, double *scan_ms, double *merge_ms,
                             int64_t *calls);
+
+/*
+ * Scan work counters, for measuring what the L2 early abandon skips.  While
+ * enabled, every k_scan wave adds per candidate block: the 16-dim chunks it
+ * computed, the chunks a full scan computes, and (once per block) the block
+ * and whether the workgroup dropped it.  lira_index_stats_read synchronises
+ * the device, returns the four sums {computed, nominal, blocks, dropped} and
+ * resets them.  Costs a few atomics per block: keep it off when timing.
+ */
+int lira_index_set_stats(lira_index *idx, int enable);
+int lira_index_stats_read(lira_index *idx, uint64_t *out4);
 
 /*
  * Device-side error word of the last scan/select on this handle (e.g. a probe

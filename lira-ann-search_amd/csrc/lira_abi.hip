@@ -132,6 +132,7 @@ int lira_index_destroy(lira_index *idx) {
     if (idx->err) hipFree(idx->err);
     if (idx->ws) hipFree(idx->ws);
     for (hipEvent_t e : idx->ev_pool) hipEventDestroy(e);
+    if (idx->stats) hipFree(idx->stats);
     delete idx;
     return LIRA_OK;
 }
@@ -284,7 +285,7 @@ int lira_scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *p
     if (idx->n_lists == 0) return fail(LIRA_ESTATE, "index has no lists (add_partitions first)");
     if (nq < 0 || nprobe_max <= 0) return fail(LIRA_EINVAL, "need nq >= 0 and nprobe_max > 0");
     if (k <= 0 || k > 256) return fail(LIRA_EUNSUPPORTED, "k must be in [1, 256]");
-    if (flags & ~(LIRA_SCAN_DEDUP | LIRA_SCAN_PER_PARTITION | LIRA_SCAN_FMA)) return fail(LIRA_EINVAL, "unknown flags");
+    if (flags & ~(LIRA_SCAN_DEDUP | LIRA_SCAN_PER_PARTITION | LIRA_SCAN_FMA | LIRA_SCAN_NO_PRUNE)) return fail(LIRA_EINVAL, "unknown flags");
     if (nq > 0 && (!q || !probe || !out_D || !out_I)) return fail(LIRA_EINVAL, "NULL buffer");
     DeviceGuard g(idx->device);
     return scan_topk(idx, q, nq, probe, nprobe_max, k, flags, out_D, out_I, out_ncand, workspace,
@@ -295,6 +296,29 @@ int lira_index_set_profiling(lira_index *idx, int enable) {
     if (!idx) return fail(LIRA_EINVAL, "index is NULL");
     idx->profiling = enable != 0;
     idx->ev_used = 0;
+    return LIRA_OK;
+}
+
+int lira_index_set_stats(lira_index *idx, int enable) {
+    if (!idx) return fail(LIRA_EINVAL, "index is NULL");
+    DeviceGuard g(idx->device);
+    if (enable && !idx->stats) LIRA_HIP_TRY(hipMalloc(&idx->stats, 4 * sizeof(uint64_t)));
+    if (enable) {
+        LIRA_HIP_TRY(hipDeviceSynchronize());
+        LIRA_HIP_TRY(hipMemset(idx->stats, 0, 4 * sizeof(uint64_t)));
+    }
+    idx->stats_on = enable != 0;
+    return LIRA_OK;
+}
+
+int lira_index_stats_read(lira_index *idx, uint64_t *out4) {
+    if (!idx || !out4) return fail(LIRA_EINVAL, "index or out is NULL");
+    DeviceGuard g(idx->device);
+    for (int i = 0; i < 4; ++i) out4[i] = 0;
+    if (!idx->stats) return LIRA_OK;
+    LIRA_HIP_TRY(hipDeviceSynchronize());
+    LIRA_HIP_TRY(hipMemcpy(out4, idx->stats, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    LIRA_HIP_TRY(hipMemset(idx->stats, 0, 4 * sizeof(uint64_t)));
     return LIRA_OK;
 }
 

@@ -48,6 +48,9 @@ struct lira_index_impl {
     bool profiling = false;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
+    // scan work counters (lira_index_set_stats): 4 u64 on the device
+    bool stats_on = false;
+    uint64_t *stats = nullptr;
 };
 
 int64_t round_up(int64_t x, int64_t m);

@@ -61,6 +61,9 @@ struct ScanArgs {
     uint32_t *qbound;     // [nq] f2ord(k-th score) published per query, ~0 = none; NULL = off
     int64_t d, dpad;
     int n_lists, n_virt, nprobe, k, bpc, nch_max;
+    int prune;            // L2 early abandon (off: LIRA_SCAN_NO_PRUNE, or env LIRA_SCAN_PRUNE=0)
+    unsigned long long *stats;  // NULL, or work counters (lira_index_set_stats): wave-chunks
+                                // computed, wave-chunks nominal, blocks, blocks dropped
 };
 
 // Work is planned over "virtual partitions" v = group * n_lists + p: with two
@@ -205,7 +208,7 @@ struct ScanSmem {
     static constexpr int kX = 2 * kXChunk;
     static constexpr int kQ = 2 * kQChunk;
     static constexpr int kBuf = kQT * kBufCap * 8;                 // 8 KiB
-    static constexpr int kMeta = 128 * 4;
+    static constexpr int kMeta = 160 * 4;  // ints; [128, 160) = per-row thresholds (float)
     static int lists(int k) { return kQT * k * 8; }
     static int total(int k) { return kX + kQ + kBuf + kMeta + lists(k); }
 };
@@ -255,6 +258,7 @@ __device__ __forceinline__ void flush_rows(u64 *L, const u64 *buf, int n, int k,
 // register budget is built for.  FMA: LIRA_SCAN_FMA accumulation (not exact).
 template <int RL, int METRIC, int OCC, bool FMA>
 __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
+    const bool PRUNE = METRIC == LIRA_METRIC_L2 && a.prune;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     typedef ScanSmem S;
     float *Xs = (float *)smem;                                   // [2][4 tiles][16 dims][64]
@@ -262,6 +266,7 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
     u64 *bufs = (u64 *)(smem + S::kX + S::kQ);                   // [32 rows][32]
     int *meta = (int *)(smem + S::kX + S::kQ + S::kBuf);         // [0..4) item, [8..40) pairs, [64..96) buffer fill
     u64 *lists = (u64 *)(smem + S::kX + S::kQ + S::kBuf + S::kMeta);  // [32 rows][k]
+    float *thr_s = (float *)(meta + 128);                         // [32 rows] early-abandon thresholds
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -324,6 +329,7 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
         // lane tx keeps the query of row ty*4 + (tx & 3) (its pruning bound slot)
         const int my_pair = meta[8 + ty * 4 + (tx & 3)];
         const int my_q = my_pair >= 0 ? my_pair / a.nprobe : -1;
+        const bool row_ok_lane = my_pair >= 0;
         // Cross-item pruning: a full k-list of any item of query q holds k
         // distinct ids scoring <= its k-th score, so that score bounds q's final
         // k-th; every item of q filters against the smallest one published so
@@ -371,25 +377,53 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
             }
             const uint32_t my_bound = a.qbound && my_q >= 0
                 ? __hip_atomic_load(a.qbound + my_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
+            // Row thresholds for the early abandon below, in LDS (registers are
+            // at the occupancy limit): lane tx < 4 of each half publishes row
+            // ty*4 + tx's.  Only this wave's selection changes these rows'
+            // lists, so they hold for the whole block.
+            if (tx < 4) {
+                const u64 t = lists[(ty * 4 + tx) * k + k - 1];
+                float th = !row_ok_lane ? __builtin_nanf("") : t == kEmptyKey ? __builtin_inff() : key_score(t);
+                if (row_ok_lane && my_bound != ~0u) th = fminf(th, ord2f(my_bound));
+                thr_s[ty * 4 + tx] = th;
+            }
+            __builtin_amdgcn_wave_barrier();
             float acc[4][8];
 #pragma unroll
             for (int u = 0; u < 4; ++u)
 #pragma unroll
                 for (int v = 0; v < 8; ++v) acc[u][v] = 0.0f;
 
-            for (int c = 0; c < nchunk; ++c) {
+            // Early abandon (L2 only).  The L2 sum adds non-negative rounded
+            // squares, and fp32 round-to-nearest is monotone, so every partial
+            // sum is <= the final distance: once a pair's partial sum exceeds
+            // its row threshold it can never be selected.  A wave whose 2048
+            // pairs are all past their thresholds stops computing (wdead); when
+            // all four waves are, the workgroup drops the rest of the block's
+            // chunks (flags in meta[96..104), double-buffered by chunk parity).
+            bool wdead = false;
+            int c = 0, ncomp = 0;
+            for (; c < nchunk; ++c) {
                 float *Qc = Qs + slot * (kDK * kQT);
 #pragma unroll
                 for (int u = 0; u < 2; ++u) Qc[(jj + u) * kQT + sq] = c * kDK + jj + u <= dlast ? pq[u] : 0.0f;
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA (asm, uncounted by hipcc) landed
                 __syncthreads();  // every wave's DMA landed; every wave is done with the other slot
-                {   // stage the next chunk (this block or the next) into the other slot
+                // workgroup-uniform: every wave was dead after chunk c-1
+                const int *fl = meta + 96 + ((c - 1) & 1) * 4;
+                const bool drop = PRUNE && c > 0 && !(fl[0] | fl[1] | fl[2] | fl[3]);
+                {   // stage the next chunk (this block, or the next block's first
+                    // when this one ends or is dropped) into the other slot
                     int njc = (c + 1) * kDK, ntb = tb;
-                    if (c + 1 == nchunk) {
+                    if (drop || c + 1 == nchunk) {
                         njc = 0;
                         ntb = tb + kBlockTiles;
                     }
                     if (ntb < tb_end) stage(ntb, njc, slot ^ 1);
+                }
+                if (drop) {  // chunk c's data (in `slot`) goes unused
+                    slot ^= 1;
+                    break;
                 }
                 const float *Xc = Xs + slot * (kBlockTiles * kDK * kTile);
                 const float *qp = Qc + ty * 4;
@@ -398,6 +432,8 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
                 // software-pipelined: LDS reads of dim j+1 are in flight while dim j
                 // runs as three phases of 16 independent packed ops (sub, mul, add),
                 // pinned by sched_barrier so no dependent pair sits back to back
+                if (!wdead) {
+                ++ncomp;
                 float4 q4 = *(const float4 *)qp, xa = *(const float4 *)xpa, xb = *(const float4 *)xpb;
 #pragma unroll 2
                 for (int j = 0; j < kDK; ++j) {
@@ -457,8 +493,32 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
                         __builtin_amdgcn_sched_barrier(0);
                     }
                 }
+                if (PRUNE) {
+                    const float4 t4 = *(const float4 *)&thr_s[ty * 4];
+                    const float thv[4] = {t4.x, t4.y, t4.z, t4.w};
+                    bool live = false;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        float m = acc[u][0];
+#pragma unroll
+                        for (int v = 1; v < 8; ++v) m = fminf(m, acc[u][v]);
+                        live |= m <= thv[u];
+                    }
+                    wdead = !__any(live);
+                }
+                }
+                if (PRUNE && lane == 0) meta[96 + (c & 1) * 4 + wave] = !wdead;
                 slot ^= 1;
             }
+            if (a.stats && lane == 0) {
+                atomicAdd(a.stats + 0, (unsigned long long)ncomp);
+                atomicAdd(a.stats + 1, (unsigned long long)nchunk);
+                if (wave == 0) {
+                    atomicAdd(a.stats + 2, 1ull);
+                    if (c < nchunk) atomicAdd(a.stats + 3, 1ull);
+                }
+            }
+            if (c < nchunk || wdead) continue;  // no pair of the block (c < nchunk) / wave can pass
 
             // ---- selection, per wave and per half-wave, straight from registers.
             // Half h of wave w owns rows (2w+h)*4+u; lane tx holds 8 candidates of each.
@@ -885,12 +945,18 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
     // One launch, so there is no tail between the groups.  With m = ceil(32 *
     // n_lists / nq) > 1 first-slot blocks would be part-filled; measured slower
     // there (GIST1M, BIGANN), so one group.
-    static const bool two_group_env = [] {
+    static const int prune_env = [] {
+        const char *e = getenv("LIRA_SCAN_PRUNE");
+        return e && e[0] == '0' ? 0 : 1;
+    }();
+    static const int two_group_env = [] {
         const char *e = getenv("LIRA_SCAN_TWO_PHASE");
-        return !(e && e[0] == '0');
+        return e ? atoi(e) : 1;
     }();
     const int64_t m1 = (kQT * (int64_t)nl + nq - 1) / nq;
-    const int groups = qbound && two_group_env && m1 == 1 && nprobe >= 2 ? 2 : 1;
+    const bool l2_prune = idx->metric == LIRA_METRIC_L2 && prune_env && !(flags & LIRA_SCAN_NO_PRUNE);
+    const int groups = qbound && two_group_env && (m1 == 1 || l2_prune || two_group_env == 2) && nprobe >= 2
+                           ? 2 : 1;
     const int split = 1;
     const int nv = groups * nl;
     const unsigned pg = (unsigned)((npairs + kPairsPerBlock - 1) / kPairsPerBlock);
@@ -925,6 +991,8 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
     a.k = (int)k;
     a.bpc = pl.bpc;
     a.nch_max = pl.nch_max;
+    a.prune = prune_env && !(flags & LIRA_SCAN_NO_PRUNE);
+    a.stats = idx->stats_on ? (unsigned long long *)idx->stats : nullptr;
     if (ev[1]) LIRA_HIP_TRY(hipEventRecord(ev[1], st));
     const bool fma = (flags & LIRA_SCAN_FMA) != 0;
     hipError_t e;

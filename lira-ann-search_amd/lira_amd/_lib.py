@@ -20,6 +20,7 @@ LIRA_METRIC_IP = 1
 LIRA_SCAN_DEDUP = 1
 LIRA_SCAN_PER_PARTITION = 2
 LIRA_SCAN_FMA = 4
+LIRA_SCAN_NO_PRUNE = 8
 LIRA_PROBE_NEAREST = 0
 LIRA_PROBE_THRESHOLD_GE = 1
 LIRA_PROBE_THRESHOLD_GT = 2
@@ -62,6 +63,8 @@ SIGNATURES = {
     "lira_scan_topk": (_INT, [_P, _P, _I64, _P, _I64, _I64, ctypes.c_uint, _P, _P, _P, _P, _SZ, _P]),
     "lira_index_check": (_INT, [_P, _P]),
     "lira_index_set_profiling": (_INT, [_P, _INT]),
+    "lira_index_set_stats": (_INT, [_P, _INT]),
+    "lira_index_stats_read": (_INT, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     "lira_index_profile_read": (_INT, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64)]),
 }

@@ -176,7 +176,8 @@ class PartitionedIndex:
 
     # --------------------------------------------------------------- search
     def search(self, q: torch.Tensor, probe: torch.Tensor, k: int, dedup: bool = True,
-               per_partition: bool = False, out=None, stream=None, fma: bool = False):
+               per_partition: bool = False, out=None, stream=None, fma: bool = False,
+               prune: bool = True):
         """Scan the probed lists of every query; exact top-k.
 
         q (nq, d) fp32, probe (nq, nprobe_max) int32 (-1 = unused slot).
@@ -186,6 +187,7 @@ class PartitionedIndex:
         Distances are search.cpp's sequential fp32 sums bit for bit; fma=True
         accumulates with fused multiply-adds instead (LIRA_SCAN_FMA: fewer
         operations, ~1e-6 relative difference, near-ties may order differently).
+        prune=False turns off the L2 early abandon (same results; for A/B).
         """
         q = _dev(q, torch.float32, self.device)
         probe = _dev(probe, torch.int32, self.device)
@@ -206,7 +208,8 @@ class PartitionedIndex:
             D, I, ncand = out
         flags = (_lib.LIRA_SCAN_DEDUP if dedup else 0) | \
             (_lib.LIRA_SCAN_PER_PARTITION if per_partition else 0) | \
-            (_lib.LIRA_SCAN_FMA if fma else 0)
+            (_lib.LIRA_SCAN_FMA if fma else 0) | \
+            (0 if prune else _lib.LIRA_SCAN_NO_PRUNE)
         with torch.cuda.device(self.device):
             _lib.call("lira_scan_topk", self._h, _lib.ptr(q), nq, _lib.ptr(probe), npm, int(k),
                       flags, _lib.ptr(D), _lib.ptr(I), _lib.ptr(ncand), None, 0,
@@ -230,6 +233,18 @@ class PartitionedIndex:
             _lib.call("lira_index_profile_read", self._h, ctypes.byref(a), ctypes.byref(b),
                       ctypes.byref(c), ctypes.byref(n))
         return {"plan_ms": a.value, "scan_ms": b.value, "merge_ms": c.value, "calls": n.value}
+
+    def set_stats(self, enable: bool = True):
+        """Count scan work (16-dim chunks computed vs a full scan; see stats_read)."""
+        _lib.call("lira_index_set_stats", self._h, int(bool(enable)))
+
+    def stats_read(self) -> dict:
+        """Work counters since the last read: wave-chunks computed / nominal,
+        candidate blocks, blocks the workgroup dropped (L2 early abandon)."""
+        v = (ctypes.c_uint64 * 4)()
+        with torch.cuda.device(self.device):
+            _lib.call("lira_index_stats_read", self._h, v)
+        return {"chunks_computed": v[0], "chunks_nominal": v[1], "blocks": v[2], "blocks_dropped": v[3]}
 
     def memory_bytes(self) -> int:
         v = ctypes.c_int64()

@@ -220,3 +220,41 @@ def test_fma_variant_within_tolerance(metric, k):
         gap = np.abs(np.diff(Dk1[r])) > tol * np.maximum(np.abs(Dk1[r, 1:]), 1e-6)
         if gap.all():  # no near-tie inside the top k nor at its boundary
             assert np.array_equal(I[r], Io[r])
+
+
+def clustered_case(seed, n, d, b, nq, nprobe, spread=3.0, sigma=0.35, ints=False):
+    # well-separated clusters: pairs outside a query's own cluster pass its k-th
+    # score within a few dims, so the L2 early abandon drops whole blocks
+    rng = np.random.default_rng(seed)
+    c = spread * rng.standard_normal((b, d), dtype=np.float32)
+    lab = rng.integers(0, b, n)
+    x = (c[lab] + sigma * rng.standard_normal((n, d), dtype=np.float32)).astype(np.float32)
+    ql = rng.integers(0, b, nq)
+    q = (c[ql] + sigma * rng.standard_normal((nq, d), dtype=np.float32)).astype(np.float32)
+    if ints:  # small integers: many exactly tied distances at the k-th score
+        x, q = np.round(x).astype(np.float32), np.round(q).astype(np.float32)
+    d2b = lab.astype(np.int32)[:, None]
+    cd = oracle.centroid_dist(q, c)
+    probe = oracle.probe_nearest(cd, nprobe)
+    return x, q, d2b, probe
+
+
+@pytest.mark.parametrize("d,k,nq,ints", [(16, 10, 600, False), (100, 1, 600, False), (128, 10, 40, True),
+                                          (960, 100, 64, False), (33, 65, 300, True)])
+def test_early_abandon_exact(d, k, nq, ints):
+    # L2 early abandon (partial sums are monotone, so a pair past its row's
+    # threshold is dropped): identical to the unpruned scan and to the oracle,
+    # including exact ties at the k-th score (integer data), per-partition lists
+    # and both probe-ordering schedules (nq >= / < 32 queries per partition)
+    b = 8
+    x, q, d2b, probe = clustered_case(500 + d, 12000, d, b, nq, 4, ints=ints)
+    idx = check_vs_oracle(x, q, d2b, probe, b, k, "L2")
+    Dp, Ip, _ = run(idx, q, probe, k)
+    Dn, In, _ = run(idx, q, probe, k, prune=False)
+    assert np.array_equal(Ip, In) and np.array_equal(bits(Dp), bits(Dn))
+    Dp, Ip, _ = run(idx, q, probe, k, per_partition=True, dedup=False)
+    Dn, In, _ = run(idx, q, probe, k, per_partition=True, dedup=False, prune=False)
+    assert np.array_equal(Ip, In) and np.array_equal(bits(Dp), bits(Dn))
+    off, ids = oracle.build_csr(d2b, b)
+    Dq, Iq = oracle.scan_per_partition(q, off, ids, oracle.gather_lists(x, off, ids), probe, k, oracle.L2)
+    assert np.array_equal(Ip, Iq) and np.array_equal(bits(Dp), bits(Dq))
