@@ -264,7 +264,10 @@ def main():
                                           "early abandon skips work"},
                          "work": {**work, "computed_frac": work["chunks_computed"] /
                                   max(1, work["chunks_nominal"]),
-                                  "dropped_block_frac": work["blocks_dropped"] / max(1, work["blocks"])},
+                                  "dropped_block_frac": work["blocks_dropped"] /
+                                  max(1, work["blocks"] + work["blocks_skipped"]),
+                                  "skipped_block_frac": work["blocks_skipped"] /
+                                  max(1, work["blocks"] + work["blocks_skipped"])},
                          "note": "SURVEY 8(d) algorithmic bytes = sum over queries of probed-bucket "
                                  "bytes; the partition-major scan reads a candidate tile once per "
                                  "32-query block and the exact L2 early abandon drops blocks whose "

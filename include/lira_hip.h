@@ -200,15 +200,19 @@ int lira_index_profile_read(lira_index *idx, double *plan_ms, double *scan_ms, d
                             int64_t *calls);
 
 /*
- * Scan work counters, for measuring what the L2 early abandon skips.  While
- * enabled, every k_scan wave adds per candidate block: the 16-dim chunks it
- * computed, the chunks a full scan computes, and (once per block) the block
- * and whether the workgroup dropped it.  lira_index_stats_read synchronises
- * the device, returns the four sums {computed, nominal, blocks, dropped} and
- * resets them.  Costs a few atomics per block: keep it off when timing.
+ * Scan work counters, for measuring what the exact L2 pruning skips.  While
+ * enabled, k_scan adds per candidate block (256 candidates x 32 query rows):
+ *   [0] 16-dim wave-chunks computed, [1] wave-chunks a full scan computes
+ *       (4 waves x dpad/16 per block, skipped blocks included),
+ *   [2] blocks entered, [3] blocks dropped by the early abandon,
+ *   [4] blocks skipped by the triangle-inequality test (never loaded),
+ *   [5..7] reserved (0).
+ * lira_index_stats_read synchronises the device, copies the 8 sums to `out8`
+ * (host) and resets them.  Costs a few atomics per block: keep it off when
+ * timing.
  */
 int lira_index_set_stats(lira_index *idx, int enable);
-int lira_index_stats_read(lira_index *idx, uint64_t *out4);
+int lira_index_stats_read(lira_index *idx, uint64_t *out8);
 
 /*
  * Device-side error word of the last scan/select on this handle (e.g. a probe

@@ -50,6 +50,58 @@ __global__ __launch_bounds__(256) void k_tile_gather(const float *x, int64_t d, 
     }
 }
 
+// Pivot of list b = mean of its rows (double sums; pad rows of X are zero).
+// One thread per (list, dim); rows read as float4 runs of a tile's dim row.
+__global__ __launch_bounds__(256) void k_list_pivot(const float *X, int64_t d, int64_t dpad,
+                                                    const int32_t *tile_off, const int64_t *list_off,
+                                                    float *pivot) {
+    const int b = blockIdx.x;
+    const int64_t j = (int64_t)blockIdx.y * blockDim.x + threadIdx.x;
+    if (j >= d) return;
+    double s = 0.0;
+    for (int t = tile_off[b]; t < tile_off[b + 1]; ++t) {
+        const float4 *row = (const float4 *)(X + ((int64_t)t * dpad + j) * kTile);
+#pragma unroll 4
+        for (int r = 0; r < kTile / 4; ++r) {
+            const float4 v = row[r];
+            s += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
+        }
+    }
+    const int64_t n = list_off[b + 1] - list_off[b];
+    pivot[(int64_t)b * d + j] = n > 0 ? (float)(s / (double)n) : 0.0f;
+}
+
+// Radius bounds of every tile: lane r of a wave = row r of the tile.
+// ||x - pivot|| in double, rounded outward to fp32 with a 2^-40 relative
+// margin (the double sum's error is ~d * 2^-53), min/max over the tile's real
+// rows (NaN rows are ignored by fminf/fmaxf; they are never selected either).
+// A tile without real rows gets (+inf, -inf).
+__global__ __launch_bounds__(256) void k_tile_stats(const float *X, const int32_t *ids, int64_t d,
+                                                    int64_t dpad, const int32_t *tile_list,
+                                                    const float *pivot, int64_t n_tiles,
+                                                    float2 *tstat) {
+    const int lane = threadIdx.x & 63;
+    const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= n_tiles) return;
+    const float *pv = pivot + (int64_t)tile_list[t] * d;
+    const float *x = X + t * dpad * kTile + lane;
+    double s = 0.0;
+    for (int64_t j = 0; j < d; ++j) {
+        const double df = (double)x[j * kTile] - (double)pv[j];
+        s = __builtin_fma(df, df, s);
+    }
+    const double R = __builtin_sqrt(s);
+    const bool real = ids[t * kTile + lane] >= 0;
+    float lo = real ? __double2float_rd(R * (1.0 - 0x1p-40)) : __builtin_inff();
+    float hi = real ? __double2float_ru(R * (1.0 + 0x1p-40)) : -__builtin_inff();
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        lo = fminf(lo, __shfl_xor(lo, m, 64));
+        hi = fmaxf(hi, __shfl_xor(hi, m, 64));
+    }
+    if (lane == 0) tstat[t] = make_float2(lo, hi);
+}
+
 __global__ void k_check_ids(const int32_t *ids, int64_t n, int64_t n_rows, int32_t *bad) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x)
@@ -61,6 +113,10 @@ static void free_storage(lira_index *idx) {
     if (idx->ids) hipFree(idx->ids);
     if (idx->tile_off) hipFree(idx->tile_off);
     if (idx->list_size) hipFree(idx->list_size);
+    if (idx->pivot) hipFree(idx->pivot);
+    if (idx->tstat) hipFree(idx->tstat);
+    idx->pivot = nullptr;
+    idx->tstat = nullptr;
     idx->X = nullptr;
     idx->ids = nullptr;
     idx->tile_off = nullptr;
@@ -226,6 +282,23 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
             rc = fail(LIRA_EHIP, std::string("tile gather failed: ") + hipGetErrorString(e));
             break;
         }
+        if (idx->metric == LIRA_METRIC_L2 && tiles > 0) {
+            if (hipMalloc(&idx->pivot, (size_t)n_lists * idx->d * 4) != hipSuccess ||
+                hipMalloc(&idx->tstat, (size_t)tiles * sizeof(float2)) != hipSuccess) {
+                rc = fail(LIRA_ENOMEM, "hipMalloc of the pivot / tile radius arrays failed");
+                break;
+            }
+            hipLaunchKernelGGL(k_list_pivot, dim3((unsigned)n_lists, (unsigned)((idx->d + 255) / 256)), dim3(256),
+                               0, st, idx->X, idx->d, idx->dpad, idx->tile_off, d_loff, idx->pivot);
+            hipLaunchKernelGGL(k_tile_stats, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, idx->X,
+                               idx->ids, idx->d, idx->dpad, d_tlist, idx->pivot, tiles, idx->tstat);
+            e = hipGetLastError();
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) {
+                rc = fail(LIRA_EHIP, std::string("pivot / tile radius build failed: ") + hipGetErrorString(e));
+                break;
+            }
+        }
     } while (0);
     if (d_loff) hipFree(d_loff);
     if (d_tlist) hipFree(d_tlist);
@@ -265,7 +338,8 @@ int lira_index_list_size(const lira_index *idx, int64_t list_no, int64_t *out) {
 
 int lira_index_memory(const lira_index *idx, int64_t *bytes) {
     if (!idx || !bytes) return fail(LIRA_EINVAL, "NULL argument");
-    *bytes = idx->n_tiles * idx->dpad * kTile * 4 + idx->n_tiles * kTile * 4 + idx->n_lists * 8;
+    *bytes = idx->n_tiles * idx->dpad * kTile * 4 + idx->n_tiles * kTile * 4 + idx->n_lists * 8 +
+             (idx->pivot ? idx->n_lists * idx->d * 4 + idx->n_tiles * 8 : 0);
     return LIRA_OK;
 }
 
@@ -302,23 +376,23 @@ int lira_index_set_profiling(lira_index *idx, int enable) {
 int lira_index_set_stats(lira_index *idx, int enable) {
     if (!idx) return fail(LIRA_EINVAL, "index is NULL");
     DeviceGuard g(idx->device);
-    if (enable && !idx->stats) LIRA_HIP_TRY(hipMalloc(&idx->stats, 4 * sizeof(uint64_t)));
+    if (enable && !idx->stats) LIRA_HIP_TRY(hipMalloc(&idx->stats, 8 * sizeof(uint64_t)));
     if (enable) {
         LIRA_HIP_TRY(hipDeviceSynchronize());
-        LIRA_HIP_TRY(hipMemset(idx->stats, 0, 4 * sizeof(uint64_t)));
+        LIRA_HIP_TRY(hipMemset(idx->stats, 0, 8 * sizeof(uint64_t)));
     }
     idx->stats_on = enable != 0;
     return LIRA_OK;
 }
 
-int lira_index_stats_read(lira_index *idx, uint64_t *out4) {
-    if (!idx || !out4) return fail(LIRA_EINVAL, "index or out is NULL");
+int lira_index_stats_read(lira_index *idx, uint64_t *out8) {
+    if (!idx || !out8) return fail(LIRA_EINVAL, "index or out is NULL");
     DeviceGuard g(idx->device);
-    for (int i = 0; i < 4; ++i) out4[i] = 0;
+    for (int i = 0; i < 8; ++i) out8[i] = 0;
     if (!idx->stats) return LIRA_OK;
     LIRA_HIP_TRY(hipDeviceSynchronize());
-    LIRA_HIP_TRY(hipMemcpy(out4, idx->stats, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-    LIRA_HIP_TRY(hipMemset(idx->stats, 0, 4 * sizeof(uint64_t)));
+    LIRA_HIP_TRY(hipMemcpy(out8, idx->stats, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    LIRA_HIP_TRY(hipMemset(idx->stats, 0, 8 * sizeof(uint64_t)));
     return LIRA_OK;
 }
 

@@ -41,6 +41,11 @@ struct lira_index_impl {
     int32_t *ids = nullptr;
     int32_t *tile_off = nullptr;   // n_lists+1 (int32: < 2^31 tiles)
     int32_t *list_size = nullptr;  // n_lists
+    // L2 only, for the scan's triangle-inequality block skip: per-list pivot
+    // (mean of its rows, fp32, n_lists x d) and per-tile radius bounds
+    // (lo, hi) with lo <= ||x - pivot|| <= hi for every real row of the tile.
+    float *pivot = nullptr;
+    float2 *tstat = nullptr;
     int32_t *err = nullptr;        // device error word
     void *ws = nullptr;            // cached scan workspace
     size_t ws_bytes = 0;
@@ -48,7 +53,7 @@ struct lira_index_impl {
     bool profiling = false;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
-    // scan work counters (lira_index_set_stats): 4 u64 on the device
+    // scan work counters (lira_index_set_stats): 8 u64 on the device
     bool stats_on = false;
     uint64_t *stats = nullptr;
 };

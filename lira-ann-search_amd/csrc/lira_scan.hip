@@ -62,8 +62,9 @@ struct ScanArgs {
     int64_t d, dpad;
     int n_lists, n_virt, nprobe, k, bpc, nch_max;
     int prune;            // L2 early abandon (off: LIRA_SCAN_NO_PRUNE, or env LIRA_SCAN_PRUNE=0)
-    unsigned long long *stats;  // NULL, or work counters (lira_index_set_stats): wave-chunks
-                                // computed, wave-chunks nominal, blocks, blocks dropped
+    unsigned long long *stats;  // NULL, or the work counters of lira_index_set_stats
+    const float *pivot;   // L2: per-list pivot (n_lists x d) and per-tile radius bounds
+    const float2 *tstat;  //     for the triangle-inequality block skip; NULL = off
 };
 
 // Work is planned over "virtual partitions" v = group * n_lists + p: with two
@@ -208,7 +209,10 @@ struct ScanSmem {
     static constexpr int kX = 2 * kXChunk;
     static constexpr int kQ = 2 * kQChunk;
     static constexpr int kBuf = kQT * kBufCap * 8;                 // 8 KiB
-    static constexpr int kMeta = 160 * 4;  // ints; [128, 160) = per-row thresholds (float)
+    // meta bytes: [0, 512) ints (item, pairs, buffer fill, abandon flags),
+    // [512, 640) per-row thresholds, [640, 1152) per-row block-skip radii (A, B)
+    // x 2 parities, [1152, 1664) per-row query-pivot distance (lo, hi) doubles
+    static constexpr int kMeta = 1664;
     static int lists(int k) { return kQT * k * 8; }
     static int total(int k) { return kX + kQ + kBuf + kMeta + lists(k); }
 };
@@ -259,6 +263,7 @@ __device__ __forceinline__ void flush_rows(u64 *L, const u64 *buf, int n, int k,
 template <int RL, int METRIC, int OCC, bool FMA>
 __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
     const bool PRUNE = METRIC == LIRA_METRIC_L2 && a.prune;
+    const bool TRI = PRUNE && a.tstat != nullptr;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     typedef ScanSmem S;
     float *Xs = (float *)smem;                                   // [2][4 tiles][16 dims][64]
@@ -267,6 +272,8 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
     int *meta = (int *)(smem + S::kX + S::kQ + S::kBuf);         // [0..4) item, [8..40) pairs, [64..96) buffer fill
     u64 *lists = (u64 *)(smem + S::kX + S::kQ + S::kBuf + S::kMeta);  // [32 rows][k]
     float *thr_s = (float *)(meta + 128);                         // [32 rows] early-abandon thresholds
+    float2 *tri_s = (float2 *)(meta + 160);                       // [2][32 rows] block-skip (A, B)
+    double *dq_s = (double *)(meta + 288);                        // [32 rows][lo, hi] ||q - pivot||
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -302,7 +309,9 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
         }
         __syncthreads();
         if (!meta[0]) break;
-        const int v = meta[1], qb = meta[2], ch = meta[3];
+        // item metadata is workgroup-uniform: keep it in SGPRs
+        const int v = __builtin_amdgcn_readfirstlane(meta[1]), qb = __builtin_amdgcn_readfirstlane(meta[2]),
+                  ch = __builtin_amdgcn_readfirstlane(meta[3]);
         const int p = v >= a.n_lists ? v - a.n_lists : v;  // the partition itself
         const int q0 = qb * kQT;
         const int nqb_valid = min(kQT, a.cnt[v] - q0);
@@ -313,8 +322,8 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
         for (int i = tid; i < kQT * k; i += kScanThreads) lists[i] = kEmptyKey;
         __syncthreads();
 
-        const int tile0 = a.tile_off[p];
-        const int ntl = a.tile_off[p + 1] - tile0;
+        const int tile0 = __builtin_amdgcn_readfirstlane(a.tile_off[p]);
+        const int ntl = __builtin_amdgcn_readfirstlane(a.tile_off[p + 1]) - tile0;
         const int tb_begin = ch * a.bpc * kBlockTiles;
         const int tb_end = min(ntl, tb_begin + a.bpc * kBlockTiles);
         // Q staging: thread stages query slot sq, dims jj, jj+1 of each chunk;
@@ -330,6 +339,100 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
         const int my_pair = meta[8 + ty * 4 + (tx & 3)];
         const int my_q = my_pair >= 0 ? my_pair / a.nprobe : -1;
         const bool row_ok_lane = my_pair >= 0;
+
+        // Triangle-inequality block skip (L2).  For a candidate x of list p with
+        // pivot c_p: ||q - x|| >= | ||q - c_p|| - ||x - c_p|| |.  The index keeps
+        // per tile bounds lo <= ||x - c_p|| <= hi (k_tile_stats), so a block whose
+        // radius range [lo, hi] sits farther than rad_r from ||q_r - c_p|| on
+        // either side cannot hold a pair scoring <= row r's threshold T_r, with
+        // rad_r = sqrt((T_r + d 2^-140) / (1 - (d+4) 2^-24)): search.cpp's fp32
+        // sum is >= the real squared distance times (1-2^-24)^(d+2) minus
+        // underflow (every term is a rounded non-negative square), so the fp32
+        // score is > T_r.  Per row: A = dq_lo - rad (rounded down), B = dq_hi +
+        // rad (rounded up); skip when hi < A or lo > B for every row.
+        if (TRI) {  // ||q_r - c_p|| in double for this half's 4 rows, 8 lanes per row
+            const int rrow = ty * 4 + (tx >> 3), part = tx & 7;
+            const int rp = meta[8 + rrow];
+            double sq = 0.0;
+            if (rp >= 0) {
+                const float *qr = a.Q + (int64_t)(rp / a.nprobe) * a.d;
+                const float *pv = a.pivot + (int64_t)p * a.d;
+                for (int j = part; j < (int)a.d; j += 8) {
+                    const double df = (double)qr[j] - (double)pv[j];
+                    sq = __builtin_fma(df, df, sq);
+                }
+            }
+            sq += __shfl_xor(sq, 1, 64);
+            sq += __shfl_xor(sq, 2, 64);
+            sq += __shfl_xor(sq, 4, 64);
+            if (part == 0) {
+                const double dq = __builtin_sqrt(sq), m = (double)(a.d + 8) * 0x1p-50;
+                dq_s[rrow * 2] = dq * (1.0 - m);
+                dq_s[rrow * 2 + 1] = dq * (1.0 + m);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        // Row thresholds (lane tx < 4 of each half: row ty*4 + tx): the row's
+        // k-th score or the query's published bound, +inf while neither exists,
+        // NaN for rows without a query.  thr_s feeds the early abandon (own
+        // rows only), tri_s[par] the block skip (read by every wave: two
+        // parities, so a wave refreshing the next block's never races one still
+        // testing with the current block's).
+        auto refresh = [&](int par) {
+            const uint32_t my_bound = a.qbound && my_q >= 0
+                ? __hip_atomic_load(a.qbound + my_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
+            if (tx < 4) {
+                const int row = ty * 4 + tx;
+                const u64 t = lists[row * k + k - 1];
+                float th = !row_ok_lane ? __builtin_nanf("") : t == kEmptyKey ? __builtin_inff() : key_score(t);
+                if (row_ok_lane && my_bound != ~0u) th = fminf(th, ord2f(my_bound));
+                thr_s[row] = th;
+                if (TRI) {
+                    float2 ab = make_float2(-__builtin_inff(), __builtin_inff());  // never skip
+                    const double F = 1.0 - (double)(a.d + 4) * 0x1p-24;
+                    if (!row_ok_lane) {
+                        ab = make_float2(__builtin_inff(), -__builtin_inff());      // no query: always
+                    } else if (th < __builtin_inff() && F > 0.5) {
+                        const double rad = __builtin_sqrt(((double)th + (double)a.d * 0x1p-140) / F) * (1.0 + 0x1p-40);
+                        double A = dq_s[row * 2] - rad, B = dq_s[row * 2 + 1] + rad;
+                        A -= __builtin_fabs(A) * 0x1p-50;
+                        B += __builtin_fabs(B) * 0x1p-50;
+                        ab = make_float2(__double2float_rd(A), __double2float_ru(B));
+                    }
+                    tri_s[par * 32 + row] = ab;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        };
+        // radius range of the block at tile tb (its tiles inside this item)
+        auto block_range = [&](int tb, float &lo, float &hi) {
+            const int ntv = min(kBlockTiles, tb_end - tb);
+            lo = __builtin_inff();
+            hi = -__builtin_inff();
+            for (int i = 0; i < ntv; ++i) {
+                const float2 st = a.tstat[tile0 + tb + i];
+                lo = fminf(lo, st.x);
+                hi = fmaxf(hi, st.y);
+            }
+        };
+        // first block at or after t that the skip test keeps (workgroup-uniform:
+        // every wave tests all 32 rows against the same LDS values)
+        auto skip_from = [&](int t, int par) {
+            if (TRI) {
+                const float2 ab = tri_s[par * 32 + (lane & 31)];
+                while (t < tb_end) {
+                    float lo, hi;
+                    block_range(t, lo, hi);
+                    if (!__all(hi < ab.x || lo > ab.y)) break;
+                    if (a.stats && tid == 0) {
+                        atomicAdd(a.stats + 4, 1ull);
+                        atomicAdd(a.stats + 1, (unsigned long long)(4 * nchunk));
+                    }
+                    t += kBlockTiles;
+                }
+            }
+            return t;
+        };
         // Cross-item pruning: a full k-list of any item of query q holds k
         // distinct ids scoring <= its k-th score, so that score bounds q's final
         // k-th; every item of q filters against the smallest one published so
@@ -361,33 +464,19 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
 #pragma unroll
             for (int u = 0; u < 2; ++u) pq[u] = qrow[min(jc + jj + u, dlast)];
         };
-        int slot = 0;
-        stage(tb_begin, 0, 0);
+        int slot = 0, bi = 0;  // bi: blocks processed in this item (tri_s parity)
+        int tb = tb_begin;
+        if (TRI) {
+            refresh(1);
+            __syncthreads();
+            tb = skip_from(tb_begin, 1);
+        }
+        if (tb < tb_end) stage(tb, 0, 0);
 
-        for (int tb = tb_begin; tb < tb_end; tb += kBlockTiles) {
-            const int ntv = min(kBlockTiles, tb_end - tb);
-            // this lane's candidates: c = tx*4+v (v<4) and 128+tx*4+(v-4)
-            int gid[8];
-            {
-                const int64_t base = (int64_t)(tile0 + tb) * kTile + tx * 4;
-                const int4 g0 = (tx >> 4) < ntv ? *(const int4 *)&a.ids[base] : make_int4(-1, -1, -1, -1);
-                const int4 g1 = 2 + (tx >> 4) < ntv ? *(const int4 *)&a.ids[base + 128] : make_int4(-1, -1, -1, -1);
-                gid[0] = g0.x; gid[1] = g0.y; gid[2] = g0.z; gid[3] = g0.w;
-                gid[4] = g1.x; gid[5] = g1.y; gid[6] = g1.z; gid[7] = g1.w;
-            }
-            const uint32_t my_bound = a.qbound && my_q >= 0
-                ? __hip_atomic_load(a.qbound + my_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
-            // Row thresholds for the early abandon below, in LDS (registers are
-            // at the occupancy limit): lane tx < 4 of each half publishes row
-            // ty*4 + tx's.  Only this wave's selection changes these rows'
-            // lists, so they hold for the whole block.
-            if (tx < 4) {
-                const u64 t = lists[(ty * 4 + tx) * k + k - 1];
-                float th = !row_ok_lane ? __builtin_nanf("") : t == kEmptyKey ? __builtin_inff() : key_score(t);
-                if (row_ok_lane && my_bound != ~0u) th = fminf(th, ord2f(my_bound));
-                thr_s[ty * 4 + tx] = th;
-            }
-            __builtin_amdgcn_wave_barrier();
+        for (int next_tb = tb_end; tb < tb_end; tb = next_tb, ++bi) {
+            // thresholds for this block (only this wave's selection changes its
+            // rows' lists, so they hold for the whole block)
+            refresh(bi & 1);
             float acc[4][8];
 #pragma unroll
             for (int u = 0; u < 4; ++u)
@@ -402,6 +491,12 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
             // all four waves are, the workgroup drops the rest of the block's
             // chunks (flags in meta[96..104), double-buffered by chunk parity).
             bool wdead = false;
+            if (TRI) {  // this wave's 8 rows all skip the block: no compute
+                float lo, hi;
+                block_range(tb, lo, hi);
+                const float2 ab = tri_s[(bi & 1) * 32 + ty * 4 + (tx & 3)];
+                wdead = __all(hi < ab.x || lo > ab.y);
+            }
             int c = 0, ncomp = 0;
             for (; c < nchunk; ++c) {
                 float *Qc = Qs + slot * (kDK * kQT);
@@ -417,7 +512,8 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
                     int njc = (c + 1) * kDK, ntb = tb;
                     if (drop || c + 1 == nchunk) {
                         njc = 0;
-                        ntb = tb + kBlockTiles;
+                        ntb = skip_from(tb + kBlockTiles, bi & 1);
+                        next_tb = ntb;
                     }
                     if (ntb < tb_end) stage(ntb, njc, slot ^ 1);
                 }
@@ -520,6 +616,18 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
             }
             if (c < nchunk || wdead) continue;  // no pair of the block (c < nchunk) / wave can pass
 
+            // this lane's candidates: c = tx*4+v (v<4) and 128+tx*4+(v-4) (loaded
+            // here, not before the chunk loop, to keep 8 VGPRs free in it)
+            const int ntv = min(kBlockTiles, tb_end - tb);
+            int gid[8];
+            {
+                const int64_t base = (int64_t)(tile0 + tb) * kTile + tx * 4;
+                const int4 g0 = (tx >> 4) < ntv ? *(const int4 *)&a.ids[base] : make_int4(-1, -1, -1, -1);
+                const int4 g1 = 2 + (tx >> 4) < ntv ? *(const int4 *)&a.ids[base + 128] : make_int4(-1, -1, -1, -1);
+                gid[0] = g0.x; gid[1] = g0.y; gid[2] = g0.z; gid[3] = g0.w;
+                gid[4] = g1.x; gid[5] = g1.y; gid[6] = g1.z; gid[7] = g1.w;
+            }
+
             // ---- selection, per wave and per half-wave, straight from registers.
             // Half h of wave w owns rows (2w+h)*4+u; lane tx holds 8 candidates of each.
             // A candidate survives when its fp32 score is <= the row's threshold:
@@ -544,10 +652,7 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
             bool unfilled = false;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const u64 t = lists[(ty * 4 + u) * k + k - 1];
-                thf[u] = !row_ok[u] ? __builtin_nanf("") : t == kEmptyKey ? __builtin_inff() : key_score(t);
-                const uint32_t gb = (uint32_t)__shfl((int)my_bound, (lane & 32) + u);
-                if (row_ok[u] && gb != ~0u) thf[u] = fminf(thf[u], ord2f(gb));
+                thf[u] = thr_s[ty * 4 + u];  // refresh() at the block start (NaN: no query)
                 unfilled |= thf[u] == __builtin_inff();
             }
             if (RL <= 2 && __any(unfilled)) {
@@ -993,6 +1098,8 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
     a.nch_max = pl.nch_max;
     a.prune = prune_env && !(flags & LIRA_SCAN_NO_PRUNE);
     a.stats = idx->stats_on ? (unsigned long long *)idx->stats : nullptr;
+    a.pivot = idx->pivot;
+    a.tstat = idx->tstat;
     if (ev[1]) LIRA_HIP_TRY(hipEventRecord(ev[1], st));
     const bool fma = (flags & LIRA_SCAN_FMA) != 0;
     hipError_t e;

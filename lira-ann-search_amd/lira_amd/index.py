@@ -240,11 +240,13 @@ class PartitionedIndex:
 
     def stats_read(self) -> dict:
         """Work counters since the last read: wave-chunks computed / nominal,
-        candidate blocks, blocks the workgroup dropped (L2 early abandon)."""
-        v = (ctypes.c_uint64 * 4)()
+        candidate blocks entered, dropped by the L2 early abandon, skipped by
+        the triangle-inequality test (include/lira_hip.h)."""
+        v = (ctypes.c_uint64 * 8)()
         with torch.cuda.device(self.device):
             _lib.call("lira_index_stats_read", self._h, v)
-        return {"chunks_computed": v[0], "chunks_nominal": v[1], "blocks": v[2], "blocks_dropped": v[3]}
+        return {"chunks_computed": v[0], "chunks_nominal": v[1], "blocks": v[2], "blocks_dropped": v[3],
+                "blocks_skipped": v[4]}
 
     def memory_bytes(self) -> int:
         v = ctypes.c_int64()
