@@ -9,27 +9,30 @@ import oracle
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 
 
-def build(cfg, nq, seed=1234, n_override=None):
+def build(cfg, nq, seed=1234, n_override=None, data="mixture"):
     from lira_amd import PartitionedIndex
-    from lira_amd.synthetic import CONFIGS, mixture_torch, nearest_centre
+    from lira_amd.synthetic import CONFIGS, workload
     N, d, B, nprobe, k, metric, _ = CONFIGS[cfg]
     N = n_override or N
     dev = torch.device("cuda", 0)
-    x, c = mixture_torch(N, d, B, seed, dev)
-    assign = nearest_centre(x, c)
+    x, c, assign, make_queries = workload(cfg, seed, dev, data, n_override=N)
     idx = PartitionedIndex(d, metric, 0).build(assign[:, None], x, B)
     off = np.zeros(B + 1, dtype=np.int64)
     off[1:] = np.cumsum(idx.list_sizes)
     ids = torch.from_numpy(np.concatenate([idx.list_ids(b) for b in range(B)]))
-    q, _ = mixture_torch(nq, d, B, seed + 1, dev, centres=c)
+    q = make_queries(nq, seed + 1)
     return idx, x, c, q, off, ids, (N, d, B, nprobe, k, metric)
 
 
-@pytest.mark.parametrize("cfg,nq,n", [("sift1m", 10000, None), ("gist1m", 1000, 200_000),
-                                      ("deep10m", 2000, 1_000_000)])
-def test_fullsize(cfg, nq, n):
+# mixture: separated clusters, the pruning skips most blocks; latent: k-means
+# cells over a continuum, the pruning rarely fires (lira_amd/synthetic.py)
+@pytest.mark.parametrize("cfg,nq,n,data", [("sift1m", 10000, None, "mixture"), ("gist1m", 1000, 200_000, "mixture"),
+                                           ("deep10m", 2000, 1_000_000, "mixture"),
+                                           ("sift1m", 10000, None, "latent"), ("gist1m", 1000, 200_000, "latent"),
+                                           ("deep10m", 2000, 1_000_000, "latent")])
+def test_fullsize(cfg, nq, n, data):
     from lira_amd import rank_nearest
-    idx, x, c, q, off, ids, (N, d, B, nprobe, k, metric) = build(cfg, nq, n_override=n)
+    idx, x, c, q, off, ids, (N, d, B, nprobe, k, metric) = build(cfg, nq, n_override=n, data=data)
     probe = rank_nearest(q, c, nprobe)
     D, I, nc = idx.search(q, probe, k)
     torch.cuda.synchronize()
