@@ -49,6 +49,8 @@ extern "C" {
                                       "tolerance fallback": 1e-4 relative, ties may order differently) */
 #define LIRA_SCAN_NO_PRUNE 8u      /* L2: compute every candidate to the last dim (no early abandon of
                                       pairs already past the k-th score); same results, for A/B */
+#define LIRA_SCAN_EXACT 16u        /* use the all-exact scan (every candidate in search.cpp's arithmetic)
+                                      instead of the default FMA screen + exact re-check; same results */
 
 /* lira_select_probes modes */
 #define LIRA_PROBE_NEAREST 0      /* nprobe smallest values, ties -> smaller bucket (IVF nprobe) */
@@ -206,7 +208,11 @@ int lira_index_profile_read(lira_index *idx, double *plan_ms, double *scan_ms, d
  *       (4 waves x dpad/16 per block, skipped blocks included),
  *   [2] blocks entered, [3] blocks dropped by the early abandon,
  *   [4] blocks skipped by the triangle-inequality test (never loaded),
- *   [5..7] reserved (0).
+ *   [5] candidates re-computed exactly by the screened path's merge,
+ *   [6] chunks it re-scanned exactly (a screened list that may have dropped
+ *       a needed candidate), [7] screened survivors appended to row lists.
+ * The screened path (default) counts [2], [5], [6], [7]; the all-exact scan
+ * (LIRA_SCAN_EXACT) [0]..[4].
  * lira_index_stats_read synchronises the device, copies the 8 sums to `out8`
  * (host) and resets them.  Costs a few atomics per block: keep it off when
  * timing.

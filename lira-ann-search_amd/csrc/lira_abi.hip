@@ -102,6 +102,30 @@ __global__ __launch_bounds__(256) void k_tile_stats(const float *X, const int32_
     if (lane == 0) tstat[t] = make_float2(lo, hi);
 }
 
+// Screening constants of every storage row (lane = row of a tile): xadj and
+// the list's rmax (atomicMax on the bits of a non-negative float).  Norms in
+// double; sqrt rounded up with a 2^-40 relative margin.
+__global__ __launch_bounds__(256) void k_row_norms(const float *X, const int32_t *ids, int64_t d, int64_t dpad,
+                                                   const int32_t *tile_list, int64_t n_tiles, int metric,
+                                                   float *xadj, float *rmax) {
+    const int lane = threadIdx.x & 63;
+    const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= n_tiles) return;
+    const float *x = X + t * dpad * kTile + lane;
+    double s = 0.0;
+    for (int64_t j = 0; j < d; ++j) {
+        const double v = (double)x[j * kTile];
+        s = __builtin_fma(v, v, s);
+    }
+    const bool real = ids[t * kTile + lane] >= 0;
+    const float xn = (float)s;  // round to nearest
+    xadj[t * kTile + lane] = !real ? __builtin_inff() : metric == LIRA_METRIC_L2 ? xn * 0.5f : 0.0f;
+    float r = real ? __double2float_ru(__builtin_sqrt(s) * (1.0 + 0x1p-40)) : 0.0f;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) r = fmaxf(r, __shfl_xor(r, m, 64));
+    if (lane == 0 && r > 0.0f) atomicMax((unsigned int *)&rmax[tile_list[t]], __float_as_uint(r));
+}
+
 __global__ void k_check_ids(const int32_t *ids, int64_t n, int64_t n_rows, int32_t *bad) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x)
@@ -113,6 +137,10 @@ static void free_storage(lira_index *idx) {
     if (idx->ids) hipFree(idx->ids);
     if (idx->tile_off) hipFree(idx->tile_off);
     if (idx->list_size) hipFree(idx->list_size);
+    if (idx->xadj) hipFree(idx->xadj);
+    if (idx->rmax) hipFree(idx->rmax);
+    idx->xadj = nullptr;
+    idx->rmax = nullptr;
     if (idx->pivot) hipFree(idx->pivot);
     if (idx->tstat) hipFree(idx->tstat);
     idx->pivot = nullptr;
@@ -282,6 +310,25 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
             rc = fail(LIRA_EHIP, std::string("tile gather failed: ") + hipGetErrorString(e));
             break;
         }
+        if (tiles > 0) {
+            if (hipMalloc(&idx->xadj, (size_t)tiles * kTile * 4) != hipSuccess ||
+                hipMalloc(&idx->rmax, (size_t)n_lists * 4) != hipSuccess) {
+                rc = fail(LIRA_ENOMEM, "hipMalloc of the row-norm arrays failed");
+                break;
+            }
+            e = hipMemsetAsync(idx->rmax, 0, (size_t)n_lists * 4, st);
+            if (e == hipSuccess) {
+                hipLaunchKernelGGL(k_row_norms, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, idx->X,
+                                   idx->ids, idx->d, idx->dpad, d_tlist, tiles, idx->metric, idx->xadj,
+                                   idx->rmax);
+                e = hipGetLastError();
+            }
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) {
+                rc = fail(LIRA_EHIP, std::string("row norms failed: ") + hipGetErrorString(e));
+                break;
+            }
+        }
         if (idx->metric == LIRA_METRIC_L2 && tiles > 0) {
             if (hipMalloc(&idx->pivot, (size_t)n_lists * idx->d * 4) != hipSuccess ||
                 hipMalloc(&idx->tstat, (size_t)tiles * sizeof(float2)) != hipSuccess) {
@@ -339,7 +386,8 @@ int lira_index_list_size(const lira_index *idx, int64_t list_no, int64_t *out) {
 int lira_index_memory(const lira_index *idx, int64_t *bytes) {
     if (!idx || !bytes) return fail(LIRA_EINVAL, "NULL argument");
     *bytes = idx->n_tiles * idx->dpad * kTile * 4 + idx->n_tiles * kTile * 4 + idx->n_lists * 8 +
-             (idx->pivot ? idx->n_lists * idx->d * 4 + idx->n_tiles * 8 : 0);
+             (idx->pivot ? idx->n_lists * idx->d * 4 + idx->n_tiles * 8 : 0) +
+             (idx->xadj ? idx->n_tiles * kTile * 4 + idx->n_lists * 4 : 0);
     return LIRA_OK;
 }
 
@@ -359,7 +407,7 @@ int lira_scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *p
     if (idx->n_lists == 0) return fail(LIRA_ESTATE, "index has no lists (add_partitions first)");
     if (nq < 0 || nprobe_max <= 0) return fail(LIRA_EINVAL, "need nq >= 0 and nprobe_max > 0");
     if (k <= 0 || k > 256) return fail(LIRA_EUNSUPPORTED, "k must be in [1, 256]");
-    if (flags & ~(LIRA_SCAN_DEDUP | LIRA_SCAN_PER_PARTITION | LIRA_SCAN_FMA | LIRA_SCAN_NO_PRUNE)) return fail(LIRA_EINVAL, "unknown flags");
+    if (flags & ~(LIRA_SCAN_DEDUP | LIRA_SCAN_PER_PARTITION | LIRA_SCAN_FMA | LIRA_SCAN_NO_PRUNE | LIRA_SCAN_EXACT)) return fail(LIRA_EINVAL, "unknown flags");
     if (nq > 0 && (!q || !probe || !out_D || !out_I)) return fail(LIRA_EINVAL, "NULL buffer");
     DeviceGuard g(idx->device);
     return scan_topk(idx, q, nq, probe, nprobe_max, k, flags, out_D, out_I, out_ncand, workspace,

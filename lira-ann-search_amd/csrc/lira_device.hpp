@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "lira_hip.h"
+
 namespace lira {
 
 typedef unsigned long long u64;
@@ -236,6 +238,71 @@ __device__ __forceinline__ int popc64(u64 m) { return __popcll(m); }
 // number of set bits of m in lanes below this lane
 __device__ __forceinline__ int mbcnt64(u64 m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
+// ---- per-query merge helpers (k_merge, k_smerge) ----
+__device__ __forceinline__ void emit_key(u64 key, int metric, float *D, int64_t *I) {
+    if (key == kEmptyKey) {
+        *D = metric == LIRA_METRIC_IP ? -__builtin_inff() : __builtin_inff();
+        *I = -1;
+    } else {
+        float s = key_score(key);
+        *D = metric == LIRA_METRIC_IP ? -s : s;
+        *I = key_gid(key);
+    }
+}
+
+// Append the k keys of one partial list to the wave's batch, merging full batches.
+template <int R>
+__device__ __forceinline__ void merge_list(u64 (&lst)[R], u64 &batch, int &bc, const u64 *src,
+                                           int k) {
+    const int lane = lane_id();
+    for (int e0 = 0; e0 < k; e0 += 64) {
+        int n = min(64, k - e0);
+        if (bc + n > 64) {
+            u64 thr = wave_list_at<R>(lst, 64 * R - 1);
+            if (__ballot(batch < thr)) wave_merge_batch<R>(lst, batch);
+            batch = kEmptyKey;
+            bc = 0;
+        }
+        if (lane >= bc && lane < bc + n) batch = src[e0 + lane - bc];
+        bc += n;
+    }
+}
+
+template <int R>
+__device__ __forceinline__ void flush_batch(u64 (&lst)[R], u64 &batch, int &bc) {
+    if (bc) {
+        u64 thr = wave_list_at<R>(lst, 64 * R - 1);
+        if (__ballot(batch < thr)) wave_merge_batch<R>(lst, batch);
+    }
+    batch = kEmptyKey;
+    bc = 0;
+}
+
+// Write the first k keys of a sorted list, optionally skipping repeated keys
+// (a gid replicated across probed buckets has the same key in each).
+template <int R>
+__device__ __forceinline__ void emit_list(const u64 (&lst)[R], int k, int dedup, int metric,
+                                          float *D, int64_t *I) {
+    const int lane = lane_id();
+    int outpos = 0;
+    u64 prev_last = kEmptyKey;
+    bool have_prev = false;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        u64 up = shfl64(lst[r], lane == 0 ? 0 : lane - 1);
+        u64 prev = lane == 0 ? prev_last : up;
+        bool has_prev = lane == 0 ? have_prev : true;
+        bool keep = lst[r] != kEmptyKey && !(dedup && has_prev && prev == lst[r]);
+        u64 bal = __ballot(keep);
+        int pos = outpos + mbcnt64(bal);
+        if (keep && pos < k) emit_key(lst[r], metric, D + pos, I + pos);
+        outpos += popc64(bal);
+        prev_last = shfl64(lst[r], 63);
+        have_prev = true;
+    }
+    for (int e = outpos + lane; e < k; e += 64) emit_key(kEmptyKey, metric, D + e, I + e);
 }
 
 }  // namespace lira

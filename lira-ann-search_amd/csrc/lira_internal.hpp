@@ -46,6 +46,11 @@ struct lira_index_impl {
     // (lo, hi) with lo <= ||x - pivot|| <= hi for every real row of the tile.
     float *pivot = nullptr;
     float2 *tstat = nullptr;
+    // For the screened scan (lira_screen.hip): per storage row xadj = ||x||^2 / 2
+    // (L2, the fp32 rounding of the double sum, halved) or 0 (IP), +inf for
+    // padding rows; per list rmax >= max ||x|| over its rows (rounded up).
+    float *xadj = nullptr;
+    float *rmax = nullptr;
     int32_t *err = nullptr;        // device error word
     void *ws = nullptr;            // cached scan workspace
     size_t ws_bytes = 0;

@@ -108,16 +108,19 @@ __global__ __launch_bounds__(256) void k_count(const int32_t *probe, int64_t npa
 }
 
 // One workgroup of 1024 threads: exclusive scans over the buckets.
+// qr = queries per work item; qblk_off (optional) = exclusive scan of the
+// query blocks ceil(cnt / qr) per virtual partition.
 __global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t *tile_off,
-                                               int n_lists, int n_virt, int bpc, int32_t *qoff,
-                                               int32_t *item_off, int32_t *nch, int32_t *head) {
-    __shared__ int32_t s_a[1024], s_b[1024];
-    __shared__ int32_t carry_a, carry_b;
-    if (threadIdx.x == 0) carry_a = carry_b = 0;
+                                               int n_lists, int n_virt, int bpc, int qr, int32_t *qoff,
+                                               int32_t *item_off, int32_t *nch, int32_t *head,
+                                               int32_t *qblk_off) {
+    __shared__ int32_t s_a[1024], s_b[1024], s_c[1024];
+    __shared__ int32_t carry_a, carry_b, carry_c;
+    if (threadIdx.x == 0) carry_a = carry_b = carry_c = 0;
     __syncthreads();
     for (int base = 0; base < n_virt; base += 1024) {
         int p = base + threadIdx.x;
-        int c = 0, items = 0;
+        int c = 0, items = 0, nqb = 0;
         if (p < n_virt) {
             c = cnt[p];
             const int pp = p >= n_lists ? p - n_lists : p;
@@ -125,33 +128,40 @@ __global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t
             int nblk = (ntl + kBlockTiles - 1) / kBlockTiles;
             int nc = (nblk + bpc - 1) / bpc;
             nch[p] = nc;
-            items = ((c + kQT - 1) / kQT) * nc;
+            nqb = (c + qr - 1) / qr;
+            items = nqb * nc;
         }
         s_a[threadIdx.x] = c;
         s_b[threadIdx.x] = items;
+        s_c[threadIdx.x] = nqb;
         __syncthreads();
         for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
             int va = threadIdx.x >= off ? s_a[threadIdx.x - off] : 0;
             int vb = threadIdx.x >= off ? s_b[threadIdx.x - off] : 0;
+            int vc = threadIdx.x >= off ? s_c[threadIdx.x - off] : 0;
             __syncthreads();
             s_a[threadIdx.x] += va;
             s_b[threadIdx.x] += vb;
+            s_c[threadIdx.x] += vc;
             __syncthreads();
         }
         if (p < n_virt) {
             qoff[p] = carry_a + s_a[threadIdx.x] - c;
             item_off[p] = carry_b + s_b[threadIdx.x] - items;
+            if (qblk_off) qblk_off[p] = carry_c + s_c[threadIdx.x] - nqb;
         }
         __syncthreads();
         if (threadIdx.x == 1023) {
             carry_a += s_a[1023];
             carry_b += s_b[1023];
+            carry_c += s_c[1023];
         }
         __syncthreads();
     }
     if (threadIdx.x == 0) {
         qoff[n_virt] = carry_a;
         item_off[n_virt] = carry_b;
+        if (qblk_off) qblk_off[n_virt] = carry_c;
         head[0] = 0;
         head[1] = carry_b;
     }
@@ -768,70 +778,6 @@ struct MergeArgs {
     int n_lists, nprobe, k, nch_max, metric, dedup, per_partition;
 };
 
-__device__ __forceinline__ void emit_key(u64 key, int metric, float *D, int64_t *I) {
-    if (key == kEmptyKey) {
-        *D = metric == LIRA_METRIC_IP ? -__builtin_inff() : __builtin_inff();
-        *I = -1;
-    } else {
-        float s = key_score(key);
-        *D = metric == LIRA_METRIC_IP ? -s : s;
-        *I = key_gid(key);
-    }
-}
-
-// Append the k keys of one partial list to the wave's batch, merging full batches.
-template <int R>
-__device__ __forceinline__ void merge_list(u64 (&lst)[R], u64 &batch, int &bc, const u64 *src,
-                                           int k) {
-    const int lane = lane_id();
-    for (int e0 = 0; e0 < k; e0 += 64) {
-        int n = min(64, k - e0);
-        if (bc + n > 64) {
-            u64 thr = wave_list_at<R>(lst, 64 * R - 1);
-            if (__ballot(batch < thr)) wave_merge_batch<R>(lst, batch);
-            batch = kEmptyKey;
-            bc = 0;
-        }
-        if (lane >= bc && lane < bc + n) batch = src[e0 + lane - bc];
-        bc += n;
-    }
-}
-
-template <int R>
-__device__ __forceinline__ void flush_batch(u64 (&lst)[R], u64 &batch, int &bc) {
-    if (bc) {
-        u64 thr = wave_list_at<R>(lst, 64 * R - 1);
-        if (__ballot(batch < thr)) wave_merge_batch<R>(lst, batch);
-    }
-    batch = kEmptyKey;
-    bc = 0;
-}
-
-// Write the first k keys of a sorted list, optionally skipping repeated keys
-// (a gid replicated across probed buckets has the same key in each).
-template <int R>
-__device__ __forceinline__ void emit_list(const u64 (&lst)[R], int k, int dedup, int metric,
-                                          float *D, int64_t *I) {
-    const int lane = lane_id();
-    int outpos = 0;
-    u64 prev_last = kEmptyKey;
-    bool have_prev = false;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        u64 up = shfl64(lst[r], lane == 0 ? 0 : lane - 1);
-        u64 prev = lane == 0 ? prev_last : up;
-        bool has_prev = lane == 0 ? have_prev : true;
-        bool keep = lst[r] != kEmptyKey && !(dedup && has_prev && prev == lst[r]);
-        u64 bal = __ballot(keep);
-        int pos = outpos + mbcnt64(bal);
-        if (keep && pos < k) emit_key(lst[r], metric, D + pos, I + pos);
-        outpos += popc64(bal);
-        prev_last = shfl64(lst[r], 63);
-        have_prev = true;
-    }
-    for (int e = outpos + lane; e < k; e += 64) emit_key(kEmptyKey, metric, D + e, I + e);
-}
-
 template <int R>
 __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
     const int lane = threadIdx.x & 63;
@@ -982,10 +928,26 @@ static void launch_merge(const MergeArgs &a, hipStream_t st) {
     hipLaunchKernelGGL((k_merge<R>), dim3((unsigned)((a.nq + 3) / 4)), dim3(256), 0, st, a);
 }
 
+bool screen_supported(const lira_index *idx, int64_t k);
+size_t screen_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k);
+int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe, int64_t nprobe, int64_t k,
+                unsigned flags, int Rm, float *out_D, int64_t *out_I, int64_t *out_ncand, void *ws,
+                size_t ws_bytes, hipStream_t st, hipEvent_t *ev);
+
+// the screened scan (lira_screen.hip) is the default; LIRA_SCAN_EXACT,
+// LIRA_SCAN_FMA or env LIRA_SCAN_SCREEN=0 select the all-exact k_scan
+static bool use_screen(const lira_index *idx, int64_t k, unsigned flags) {
+    static const int env = [] {
+        const char *e = getenv("LIRA_SCAN_SCREEN");
+        return e && e[0] == '0' ? 0 : 1;
+    }();
+    return env && !(flags & (LIRA_SCAN_FMA | LIRA_SCAN_EXACT)) && screen_supported(idx, k);
+}
+
 int scan_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k,
                         size_t *bytes) {
     ScanPlan pl = make_plan(idx, nq, nprobe, k);
-    *bytes = pl.total;
+    *bytes = std::max(pl.total, screen_supported(idx, k) ? screen_workspace_size(idx, nq, nprobe, k) : 0);
     return LIRA_OK;
 }
 
@@ -1003,6 +965,18 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
                         " exceeds the 512-key merge list");
     if (nq == 0) return LIRA_OK;
     if (nq * nprobe > INT32_MAX) return fail(LIRA_EUNSUPPORTED, "nq * nprobe_max must be < 2^31");
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    if (idx->profiling) {
+        while (idx->ev_pool.size() < idx->ev_used + 4) {
+            hipEvent_t e;
+            LIRA_HIP_TRY(hipEventCreate(&e));
+            idx->ev_pool.push_back(e);
+        }
+        for (int i = 0; i < 4; ++i) ev[i] = idx->ev_pool[idx->ev_used + i];
+        idx->ev_used += 4;
+    }
+    if (use_screen(idx, k, flags))
+        return screen_topk(idx, q, nq, probe, nprobe, k, flags, Rm, out_D, out_I, out_ncand, ws, ws_bytes, st, ev);
     ScanPlan pl = make_plan(idx, nq, nprobe, k);
     if (!ws) {
         if (idx->ws_bytes < pl.total) {
@@ -1027,17 +1001,7 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
     u64 *partial = (u64 *)(w + pl.off_partial);
     uint32_t *qbound = per_part ? nullptr : (uint32_t *)(w + pl.off_qbound);
 
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    if (idx->profiling) {
-        while (idx->ev_pool.size() < idx->ev_used + 4) {
-            hipEvent_t e;
-            LIRA_HIP_TRY(hipEventCreate(&e));
-            idx->ev_pool.push_back(e);
-        }
-        for (int i = 0; i < 4; ++i) ev[i] = idx->ev_pool[idx->ev_used + i];
-        idx->ev_used += 4;
-        LIRA_HIP_TRY(hipEventRecord(ev[0], st));
-    }
+    if (ev[0]) LIRA_HIP_TRY(hipEventRecord(ev[0], st));
     // cnt, cursor and head are contiguous at the start of the workspace
     LIRA_HIP_TRY(hipMemsetAsync(w, 0, pl.off_qoff, st));
     if (qbound) LIRA_HIP_TRY(hipMemsetAsync(qbound, 0xff, (size_t)nq * 4, st));
@@ -1069,8 +1033,8 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
     const size_t hf = nv <= kHistMax / 2 ? (size_t)nv * 8 : 0;
     hipLaunchKernelGGL(k_count, dim3(pg), dim3(256), hc, st, probe, npairs, nl, (int)nprobe, split, groups,
                        cnt, idx->err);
-    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, nv, pl.bpc, qoff,
-                       item_off, nch, head);
+    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, nv, pl.bpc, kQT, qoff,
+                       item_off, nch, head, (int32_t *)nullptr);
     hipLaunchKernelGGL(k_fill, dim3(pg), dim3(256), hf, st, probe, npairs, nl, (int)nprobe, split, groups,
                        qoff, cursor, qlist);
     LIRA_HIP_TRY(hipGetLastError());
@@ -1137,6 +1101,24 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
     LIRA_HIP_TRY(hipGetLastError());
     if (ev[3]) LIRA_HIP_TRY(hipEventRecord(ev[3], st));
     return LIRA_OK;
+}
+
+// Plan kernels for another scan kernel (lira_screen.hip): one group of
+// virtual partitions, `qr` queries per item, query-block offsets in qblk_off.
+// cnt, cursor and head must be zeroed by the caller.
+hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npairs, int nprobe, int bpc,
+                       int qr, int32_t *cnt, int32_t *cursor, int32_t *qoff, int32_t *item_off,
+                       int32_t *nch, int32_t *head, int32_t *qlist, int32_t *qblk_off, hipStream_t st) {
+    const int nl = (int)idx->n_lists;
+    const unsigned pg = (unsigned)((npairs + kPairsPerBlock - 1) / kPairsPerBlock);
+    const size_t hc = nl <= kHistMax ? (size_t)nl * 4 : 0;
+    const size_t hf = nl <= kHistMax / 2 ? (size_t)nl * 8 : 0;
+    hipLaunchKernelGGL(k_count, dim3(pg), dim3(256), hc, st, probe, npairs, nl, nprobe, 1, 1, cnt, idx->err);
+    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, nl, bpc, qr, qoff,
+                       item_off, nch, head, qblk_off);
+    hipLaunchKernelGGL(k_fill, dim3(pg), dim3(256), hf, st, probe, npairs, nl, nprobe, 1, 1, qoff, cursor,
+                       qlist);
+    return hipGetLastError();
 }
 
 }  // namespace lira

@@ -1,0 +1,909 @@
+// lira_screen.hip -- screened candidate scan with exact re-check (gfx950).
+// Default path of lira_scan_topk; replaces search.cpp:468-514 and the
+// per-(query, bucket) faiss IndexFlat*.search calls (LIRA_smallscale.py:158-172)
+// with results identical to the all-exact scan (lira_scan.hip k_scan).
+//
+// Why.  search.cpp's distance is a sequential fp32 sum of separately rounded
+// terms: fl(fl(q-x)^2) for L2 (3 VALU ops per candidate-dim, no FMA allowed)
+// and fl(q*x) for IP (2 ops).  Computing that for every candidate makes the
+// scan VALU-bound at 3 ops/dim.  Here every candidate is first *screened* with
+// an fp32 fused-multiply-add dot product (1 op/dim on v_pk_fma_f32), and only
+// the few candidates that can still reach the top-k are re-computed in the
+// reference's arithmetic.  Nothing is approximated: the screen is a rigorous
+// filter, so the output is bit-identical.
+//
+// Error model (u = 2^-24, per (query, partition); double on the host side of
+// each bound, fp32 values rounded in the safe direction):
+//   L2:  s~ = fma(-2, dot, fl(qn + xn)) with qn = fl(||q||^2), xn = fl(||x||^2)
+//        and dot an fp32 FMA chain, so |s~ - D| <= E = 1.05 (d+8) u (|q|+R)^2 + dl,
+//        D = ||q-x||^2 real, R >= max ||x|| of the partition, dl = d 2^-140
+//        (underflow).  search.cpp's sum s (all terms >= 0) satisfies
+//        D (1-g) - dl <= s <= D (1+g) + dl with g = (d+4) u.
+//   IP:  score = -ip; |s - (-dot)| <= E = 1.05 * 2 (d+2) u |q| R + dl.
+// A list's k-th screened score s~k therefore bounds the final k-th exact score
+// by P = (s~k + E)(1+g) + dl (IP: s~k + E), and a candidate can only matter if
+// its s~ <= lim(T) = (T + dl)/(1-g) + E (IP: T + E), T = the best such bound
+// known.  The per-block test is that inequality on the dot product with one
+// more rounding absorbed (see row_h).
+//
+// Schedule: as k_scan (partition-major items of QR queries x a chunk of the
+// bucket, persistent grid, atomic work head).  X tiles stream through a 2-deep
+// LDS ring by LDS-DMA; each wave owns RW = QR/4 query rows and all 256
+// candidates of a block (4 per lane); the rows' query values come from a
+// per-item transposed copy (k_qstage) through scalar loads, so the inner step
+// is one ds_read_b128 + RW*2 v_pk_fma_f32 with SGPR-broadcast operands.
+//
+// Selection per row: a sorted list of K2 = 32*RL >= k+8 screened keys
+// (s~ << 32 | storage row) in LDS with a 32-key survivor buffer (ballot
+// compaction, half-wave bitonic merge when full).  k_smerge then takes, per
+// query, every listed candidate with s~ <= lim(T_final), re-computes its exact
+// score from the tiles, and selects/dedups exactly as k_merge.  A list whose
+// K2-th key is still inside lim may have dropped a needed candidate: k_smerge
+// then re-scans that chunk exactly (never seen in the benches; tested).
+#include <algorithm>
+#include <cstdlib>
+#include <string>
+
+#include "lira_device.hpp"
+#include "lira_internal.hpp"
+
+namespace lira {
+
+hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npairs, int nprobe, int bpc,
+                       int qr, int32_t *cnt, int32_t *cursor, int32_t *qoff, int32_t *item_off,
+                       int32_t *nch, int32_t *head, int32_t *qlist, int32_t *qblk_off, hipStream_t st);
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(4))) float cfloat;  // uniform address -> s_load
+
+static constexpr int kSBT = 4;     // tiles per candidate block (256 candidates)
+static constexpr int kSDK = 16;    // dims per staged chunk
+static constexpr int kSThreads = 256;
+static constexpr double kU = 0x1p-24;
+
+struct ScreenArgs {
+    const float *X;        // [n_tiles][dpad][64]
+    const float *xadj;     // [n_tiles*64]
+    const float *rmax;     // [n_lists]
+    const int32_t *tile_off, *cnt, *item_off, *qblk_off;
+    int32_t *head;
+    const float *QT;       // [qblk][4][dpad][RW]
+    const float4 *QN;      // [qblk*QR]: qn, |q| (up), pair (int bits), 0
+    u64 *partial;          // [pair][nch_max][K2]
+    uint32_t *qbound;      // [nq] f2ord(bound on the final k-th exact score); NULL = off
+    int64_t d, dpad;
+    int n_lists, nprobe, k, bpc, nch_max;
+    unsigned long long *stats;  // NULL or lira_index_set_stats counters
+};
+
+// ---- error model (double) -------------------------------------------------
+template <int METRIC>
+__device__ __forceinline__ double err_E(double qnorm, double R, double d) {
+    const double dl = d * 0x1p-140;
+    if (METRIC == LIRA_METRIC_L2) {
+        const double s = qnorm + R;
+        return 1.05 * ((d + 8.0) * kU * s * s) + dl;
+    }
+    return 1.05 * (2.0 * (d + 2.0) * kU * qnorm * R) + dl;
+}
+// bound on the final k-th exact score from a list's k-th screened score
+template <int METRIC>
+__device__ __forceinline__ double bound_P(double sk, double E, double d) {
+    if (METRIC == LIRA_METRIC_L2) return (sk + E) * (1.0 + (d + 4.0) * kU) * (1.0 + 0x1p-50) + d * 0x1p-140;
+    return (sk + E) + __builtin_fabs(sk + E) * 0x1p-50;
+}
+// largest screened score a candidate may have and still score <= T exactly
+template <int METRIC>
+__device__ __forceinline__ double s_lim(double T, double E, double d) {
+    if (METRIC == LIRA_METRIC_L2) return ((T + d * 0x1p-140) / (1.0 - (d + 4.0) * kU)) * (1.0 + 0x1p-50) + E;
+    return T + E + __builtin_fabs(T + E) * 0x1p-50;
+}
+// per-block test threshold on the dot product: pass iff fl(dot - xadj) >= h.
+// L2: s~ <= lim  <=>  dot - xn/2 >= (qn - lim)/2; fl(dot - xadj) is off by at
+// most u (|q| + R)^2.  IP: xadj = 0, -s~ = dot >= -lim.
+template <int METRIC>
+__device__ __forceinline__ float row_h(double lim, double qn, double qnorm, double R) {
+    if (!(lim < 1e300)) return -__builtin_inff();
+    double h;
+    if (METRIC == LIRA_METRIC_L2) {
+        const double s = qnorm + R;
+        h = (qn - lim) * 0.5 - 1.05 * kU * s * s;
+    } else {
+        h = -lim;
+    }
+    h -= __builtin_fabs(h) * 0x1p-50;
+    return __double2float_rd(h);
+}
+
+// ---- Q staging: transposed per-item query copy + norms ---------------------
+// Block b = one query block (virtual partition v, block qb of QR pairs).
+template <int QR>
+__global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64_t dpad, int nprobe,
+                                                int n_lists, const int32_t *cnt, const int32_t *qoff,
+                                                const int32_t *qlist, const int32_t *qblk_off, float *QT,
+                                                float4 *QN) {
+    constexpr int RW = QR / 4;
+    __shared__ int pairs[QR];
+    __shared__ int s_v;
+    const int b = blockIdx.x;
+    if (b >= qblk_off[n_lists]) return;
+    if (threadIdx.x == 0) {
+        int lo = 0, hi = n_lists - 1;  // last v with qblk_off[v] <= b
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (qblk_off[mid] <= b) lo = mid; else hi = mid - 1;
+        }
+        s_v = lo;
+    }
+    __syncthreads();
+    const int v = s_v, qb = b - qblk_off[v];
+    const int nval = min(QR, cnt[v] - qb * QR);
+    if (threadIdx.x < QR) pairs[threadIdx.x] = (int)threadIdx.x < nval ? qlist[qoff[v] + qb * QR + threadIdx.x] : -1;
+    __syncthreads();
+    for (int64_t i = threadIdx.x; i < (int64_t)QR * dpad; i += 256) {
+        const int r = (int)(i / dpad);
+        const int64_t j = i - (int64_t)r * dpad;
+        const int pr = pairs[r];
+        const float val = pr >= 0 && j < d ? Q[(int64_t)(pr / nprobe) * d + j] : 0.0f;
+        QT[(((int64_t)b * 4 + r / RW) * dpad + j) * RW + (r % RW)] = val;
+    }
+    const int lane = threadIdx.x & 63;
+    for (int r = threadIdx.x >> 6; r < QR; r += 4) {
+        const int pr = pairs[r];
+        double s = 0.0;
+        if (pr >= 0) {
+            const float *qr = Q + (int64_t)(pr / nprobe) * d;
+            for (int64_t j = lane; j < d; j += 64) {
+                const double x = (double)qr[j];
+                s = __builtin_fma(x, x, s);
+            }
+        }
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+        if (lane == 0)
+            QN[(int64_t)b * QR + r] = make_float4((float)s, __double2float_ru(__builtin_sqrt(s) * (1.0 + 0x1p-40)),
+                                                  __int_as_float(pr), 0.0f);
+    }
+}
+
+// ---- the screening kernel --------------------------------------------------
+template <int QR, int RL>
+struct SSmem {
+    static constexpr int RW = QR / 4, K2 = 32 * RL;
+    static constexpr int kX = 2 * kSBT * kSDK * kTile * 4;  // 32 KiB ring
+    static constexpr int kLists = QR * K2 * 8;
+    static constexpr int kBufs = QR * 32 * 8;
+    static constexpr int kMeta = 64 + QR * 4 * 3;           // item; pair, bufc, (spare) per row
+    static constexpr int total = kX + kLists + kBufs + kMeta;
+};
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+__device__ __forceinline__ void sglds16(const void *gsrc, uint32_t lds_addr) {
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds_addr)
+        : "memory");
+}
+
+// 64 u32 values, one per lane: ascending bitonic sort.
+__device__ __forceinline__ uint32_t wave_sort64_u32(uint32_t v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            const uint32_t o = (uint32_t)__shfl_xor((int)v, stride, 64);
+            const bool lower = (lane & stride) == 0, asc = (lane & size) == 0;
+            v = (lower == asc) ? min(v, o) : max(v, o);
+        }
+    }
+    return v;
+}
+
+// Merge a row's survivor buffer (n keys) into its sorted K2-list.  Both halves
+// run the half-wave network on the same row; half 0 stores.
+template <int RL>
+__device__ __forceinline__ void s_flush(u64 *L, const u64 *buf, int n) {
+    const int hl = lane_id() & 31;
+    u64 lst[RL];
+#pragma unroll
+    for (int r = 0; r < RL; ++r) lst[r] = L[r * 32 + hl];
+    const u64 b = hl < n ? buf[hl] : kEmptyKey;
+    half_merge_batch1<RL>(lst, b);
+    if (lane_id() < 32) {
+#pragma unroll
+        for (int r = 0; r < RL; ++r) L[r * 32 + hl] = lst[r];
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Append this lane's passing keys (v-major order) to the row's buffer,
+// merging into the list whenever the buffer fills.  Returns the new fill.
+template <int RL>
+__device__ __forceinline__ int s_append(u64 *L, u64 *buf, int bc, u64 k0, u64 k1, u64 k2, u64 k3, int pmask,
+                                     unsigned long long *stats) {
+    const u64 key[4] = {k0, k1, k2, k3};
+    u64 b[4];
+    int pos[4], tot = 0;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        b[v] = __ballot((pmask >> v) & 1);
+        pos[v] = tot + mbcnt64(b[v]);
+        tot += popc64(b[v]);
+    }
+    if (stats && lane_id() == 0) atomicAdd(stats + 7, (unsigned long long)tot);
+    int consumed = 0;
+    for (;;) {
+        const int room = 32 - bc;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int rel = pos[v] - consumed;
+            if (((pmask >> v) & 1) && rel >= 0 && rel < room) buf[bc + rel] = key[v];
+        }
+        const int placed = min(room, tot - consumed);
+        bc += placed;
+        consumed += placed;
+        __builtin_amdgcn_wave_barrier();
+        if (bc == 32) {
+            s_flush<RL>(L, buf, 32);
+            bc = 0;
+        }
+        if (consumed >= tot) break;
+    }
+    return bc;
+}
+
+template <int METRIC, int RL, int QR, int OCC>
+__global__ __launch_bounds__(kSThreads, OCC) void k_screen(ScreenArgs a) {
+    typedef SSmem<QR, RL> S;
+    constexpr int RW = S::RW, K2 = S::K2;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float *Xs = (float *)smem;                               // [2][4 tiles][16 dims][64]
+    u64 *lists = (u64 *)(smem + S::kX);                      // [QR][K2]
+    u64 *bufs = (u64 *)(smem + S::kX + S::kLists);           // [QR][32]
+    int *meta = (int *)(smem + S::kX + S::kLists + S::kBufs);
+    int *m_pair = meta + 16, *m_bufc = meta + 16 + QR;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int k = a.k;
+    const double dd = (double)a.d;
+    const float4 *Xg = (const float4 *)a.X;
+    const uint32_t xs_lds = (uint32_t)(uintptr_t)(lds_void_t *)Xs;
+    const int tstride = (int)a.dpad * (kTile / 4);  // float4 per tile
+    const int nchunk = (int)(a.dpad / kSDK);
+    const int ti = lane >> 4, col = (lane & 15) * 4;   // this lane's 4 candidates of a block
+
+    for (;;) {
+        if (tid == 0) {
+            const int item = atomicAdd(&a.head[0], 1);
+            const int ok = item < a.head[1];
+            int v = 0, qb = 0, ch = 0;
+            if (ok) {
+                int lo = 0, hi = a.n_lists - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (a.item_off[mid] <= item) lo = mid; else hi = mid - 1;
+                }
+                v = lo;
+                const int local = item - a.item_off[v];
+                const int nqb = (a.cnt[v] + QR - 1) / QR;
+                ch = local / nqb;
+                qb = local - ch * nqb;
+            }
+            meta[0] = ok;
+            meta[1] = v;
+            meta[2] = qb;
+            meta[3] = ch;
+        }
+        __syncthreads();
+        if (!meta[0]) break;
+        const int p = __builtin_amdgcn_readfirstlane(meta[1]);
+        const int qb = __builtin_amdgcn_readfirstlane(meta[2]);
+        const int ch = __builtin_amdgcn_readfirstlane(meta[3]);
+        const int gqb = __builtin_amdgcn_readfirstlane(a.qblk_off[p]) + qb;
+        if (tid < QR) {
+            m_pair[tid] = __float_as_int(a.QN[(int64_t)gqb * QR + tid].z);
+            m_bufc[tid] = 0;
+        }
+        for (int i = tid; i < QR * K2; i += kSThreads) lists[i] = kEmptyKey;
+        __syncthreads();
+
+        const int tile0 = __builtin_amdgcn_readfirstlane(a.tile_off[p]);
+        const int ntl = __builtin_amdgcn_readfirstlane(a.tile_off[p + 1]) - tile0;
+        const int tb_begin = ch * a.bpc * kSBT;
+        const int tb_end = min(ntl, tb_begin + a.bpc * kSBT);
+        const double R = (double)a.rmax[p];
+
+        // this lane's row for threshold work: row = wave*RW + (lane % RW)
+        const int my_row = wave * RW + (lane % RW);
+        const float4 qrec = a.QN[(int64_t)gqb * QR + my_row];
+        const int my_pair = __float_as_int(qrec.z);
+        const int my_q = my_pair >= 0 ? my_pair / a.nprobe : -1;
+        const double my_qn = (double)qrec.x, my_qnorm = (double)qrec.y;
+        const double my_E = err_E<METRIC>(my_qnorm, R, dd);
+        u64 *my_list = lists + my_row * K2;
+
+        cfloat *qt = (cfloat *)(a.QT + ((int64_t)gqb * 4 + wave) * a.dpad * RW);
+
+        auto stage = [&](int tb, int jc, int slot) {
+            const int ntv = min(kSBT, tb_end - tb);
+            const float4 *src = Xg + (int64_t)(tile0 + tb) * tstride + jc * (kTile / 4) + tid;
+            const uint32_t dst = __builtin_amdgcn_readfirstlane(
+                xs_lds + (uint32_t)(slot * (kSBT * kSDK * kTile) + wave * 256) * 4u);
+#pragma unroll
+            for (int i = 0; i < kSBT; ++i)
+                sglds16(src + min(i, ntv - 1) * tstride, dst + (uint32_t)(i * (kSDK * kTile) * 4));
+        };
+        int slot = 0;
+        if (tb_begin < tb_end) stage(tb_begin, 0, 0);
+
+#pragma unroll 1
+        for (int tb = tb_begin; tb < tb_end; tb += kSBT) {
+            const int ntv = min(kSBT, tb_end - tb);
+            // screening constants of my 4 candidates (+inf: padding / past the block)
+            f4 a4 = (f4)(__builtin_inff());
+            if (ti < ntv) a4 = *(const f4 *)&a.xadj[(int64_t)(tile0 + tb + ti) * kTile + col];
+            const uint32_t pub = a.qbound && my_q >= 0
+                ? __hip_atomic_load(a.qbound + my_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
+
+            f2 acc[RW][2];
+#pragma unroll
+            for (int r = 0; r < RW; ++r) acc[r][0] = acc[r][1] = (f2)(0.0f);
+
+#pragma unroll 1
+            for (int c = 0; c < nchunk; ++c) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA landed
+                __syncthreads();  // every wave's DMA landed; every wave is done with the other slot
+                {
+                    int njc = (c + 1) * kSDK, ntb = tb;
+                    if (c + 1 == nchunk) {
+                        njc = 0;
+                        ntb = tb + kSBT;
+                    }
+                    if (ntb < tb_end) stage(ntb, njc, slot ^ 1);
+                }
+                const float *xp = Xs + slot * (kSBT * kSDK * kTile) + ti * (kSDK * kTile) + col;
+                cfloat *qc = qt + (int64_t)c * kSDK * RW;
+#pragma unroll
+                for (int j = 0; j < kSDK; ++j) {
+                    const f4 x = *(const f4 *)(xp + j * kTile);
+                    const f2 xa = x.xy, xb = x.zw;
+#pragma unroll
+                    for (int r = 0; r < RW; ++r) {
+                        const float qv = qc[j * RW + r];
+                        acc[r][0] = __builtin_elementwise_fma(xa, (f2)(qv), acc[r][0]);
+                        acc[r][1] = __builtin_elementwise_fma(xb, (f2)(qv), acc[r][1]);
+                    }
+                }
+                slot ^= 1;
+            }
+
+            // ---- thresholds: lane (row) computes h from its list and the published bound
+            float h_l;
+            {
+                const u64 kk = my_list[k - 1];
+                double T = kk == kEmptyKey ? __builtin_inf() : bound_P<METRIC>((double)key_score(kk), my_E, dd);
+                if (pub != ~0u) T = fmin(T, (double)ord2f(pub));
+                h_l = my_pair < 0 ? __builtin_inff()  // no query: nothing passes
+                                  : row_h<METRIC>(s_lim<METRIC>(T, my_E, dd), my_qn, my_qnorm, R);
+            }
+            if (a.stats && lane == 0 && wave == 0) atomicAdd(a.stats + 2, 1ull);
+
+            // ---- selection.  Phase 1 (unrolled): per row, which of my 4
+            // candidates pass h; rows where any lane has one set `hit`
+            // (wave-uniform).  Phase 2 (one copy of the code): those rows.
+            int vmask = 0;  // real candidates (padding has xadj = +inf)
+            vmask |= a4.x != __builtin_inff() ? 1 : 0;
+            vmask |= a4.y != __builtin_inff() ? 2 : 0;
+            vmask |= a4.z != __builtin_inff() ? 4 : 0;
+            vmask |= a4.w != __builtin_inff() ? 8 : 0;
+            uint32_t hit = 0;
+            u64 pmw = 0;
+#pragma unroll
+            for (int r = 0; r < RW; ++r) {
+                const float h = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(h_l), r));
+                const f2 w0 = acc[r][0] - a4.xy, w1 = acc[r][1] - a4.zw;
+                const int pm = ((w0.x >= h) | ((w0.y >= h) << 1) | ((w1.x >= h) << 2) | ((w1.y >= h) << 3)) & vmask;
+                pmw |= (u64)pm << (4 * r);
+                if (__any(pm)) hit |= 1u << r;
+            }
+            hit = __builtin_amdgcn_readfirstlane(hit);
+            while (hit) {
+                const int r = __builtin_ctz(hit);
+                hit &= hit - 1;
+                const int row = wave * RW + r;
+                // this row's dot products (uniform r: a select chain, no
+                // dynamic register indexing)
+                f2 d0 = acc[0][0], d1 = acc[0][1];
+#pragma unroll
+                for (int rr = 1; rr < RW; ++rr) {
+                    d0 = r == rr ? acc[rr][0] : d0;
+                    d1 = r == rr ? acc[rr][1] : d1;
+                }
+                float h = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(h_l), r));
+                int pm = (int)(pmw >> (4 * r)) & 15;
+                const float qnf = __int_as_float(__builtin_amdgcn_readlane(__float_as_int((float)my_qn), r));
+                const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+                const float dv[4] = {d0.x, d0.y, d1.x, d1.y};
+                float sc[4];  // screened scores (+inf for padding)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    if (METRIC == LIRA_METRIC_L2)
+                        sc[v] = (vmask >> v) & 1 ? __builtin_fmaf(-2.0f, dv[v], qnf + 2.0f * av[v]) : __builtin_inff();
+                    else
+                        sc[v] = (vmask >> v) & 1 ? -dv[v] : __builtin_inff();
+                }
+                if (h == -__builtin_inff()) {
+                    // no bound yet (an item's first block): take one from the
+                    // block itself.  t = ceil(k/64) smallest per lane, j =
+                    // ceil(k/t): the j-th smallest lane value has >= j*t >= k
+                    // real candidates at or below it.
+                    float srt[4] = {sc[0], sc[1], sc[2], sc[3]};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int v = 0; v + 1 < 4 - i; ++v) {
+                            const float lo = fminf(srt[v], srt[v + 1]), hi = fmaxf(srt[v], srt[v + 1]);
+                            srt[v] = lo;
+                            srt[v + 1] = hi;
+                        }
+                    const int t = (k + 63) / 64;
+                    const float mine = t <= 1 ? srt[0] : t == 2 ? srt[1] : t == 3 ? srt[2] : srt[3];
+                    const uint32_t sorted = wave_sort64_u32(f2ord(mine == mine ? mine : __builtin_inff()));
+                    const int j = (k + t - 1) / t;
+                    const float B = ord2f((uint32_t)__shfl((int)sorted, j - 1, 64));
+                    if (B < __builtin_inff()) {
+                        const double qnorm_r =
+                            (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int((float)my_qnorm), r));
+                        const double E_r = err_E<METRIC>(qnorm_r, R, dd);
+                        h = row_h<METRIC>(s_lim<METRIC>(bound_P<METRIC>((double)B, E_r, dd), E_r, dd), (double)qnf,
+                                          qnorm_r, R);
+                        const f2 w0 = d0 - a4.xy, w1 = d1 - a4.zw;
+                        pm = ((w0.x >= h) | ((w0.y >= h) << 1) | ((w1.x >= h) << 2) | ((w1.y >= h) << 3)) & vmask;
+                    }
+                }
+                const int lo_pos = (tile0 + tb + ti) * kTile + col;
+                u64 key[4];
+#pragma unroll
+                for (int v = 0; v < 4; ++v) key[v] = ((u64)f2ord(sc[v]) << 32) | (uint32_t)(lo_pos + v);
+                m_bufc[row] = s_append<RL>(lists + row * K2, bufs + row * 32, m_bufc[row], key[0], key[1], key[2],
+                                           key[3], pm, a.stats);
+            }
+        }
+
+        // ---- flush buffers, emit lists, publish bounds (wave-owned rows)
+#pragma unroll 1
+        for (int r = 0; r < RW; ++r) {
+            const int row = wave * RW + r;
+            const int bc = m_bufc[row];
+            if (bc > 0) s_flush<RL>(lists + row * K2, bufs + row * 32, bc);
+            const int pr = m_pair[row];
+            if (pr >= 0) {
+                u64 *dst = a.partial + ((int64_t)pr * a.nch_max + ch) * K2;
+                for (int e = lane; e < K2; e += 64) dst[e] = lists[row * K2 + e];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (lane < RW && a.qbound && my_q >= 0) {
+            const u64 kk = my_list[k - 1];
+            if (kk != kEmptyKey) {
+                const double P = bound_P<METRIC>((double)key_score(kk), my_E, dd);
+                atomicMin(a.qbound + my_q, f2ord(__double2float_ru(P)));
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---- merge: exact re-check of the survivors, final selection ---------------
+struct SMergeArgs {
+    const u64 *partial;
+    const int32_t *probe, *nch, *list_size, *tile_off, *ids;
+    const float *Q, *X, *rmax;
+    const uint32_t *qbound;
+    float *D;
+    int64_t *I;
+    int64_t *ncand;
+    int64_t nq, d, dpad;
+    int n_lists, nprobe, k, K2, nch_max, bpc, dedup, per_partition;
+    unsigned long long *stats;
+};
+
+// exact score of the candidate at storage row pos (search.cpp:253-269 order)
+template <int METRIC>
+__device__ __forceinline__ float exact_score(const float *q, const float *X, int64_t d, int64_t dpad, int pos) {
+    const float *xp = X + (int64_t)(pos >> 6) * dpad * kTile + (pos & 63);
+    float acc = 0.0f;
+#pragma unroll 16
+    for (int64_t j = 0; j < d; ++j) {
+        if (METRIC == LIRA_METRIC_L2) {
+            const float df = q[j] - xp[j * kTile];
+            acc = acc + df * df;
+        } else {
+            acc = acc + q[j] * xp[j * kTile];
+        }
+    }
+    return METRIC == LIRA_METRIC_L2 ? acc : -acc;
+}
+
+template <int R>
+__device__ __forceinline__ void merge_batch_if(u64 (&lst)[R], u64 batch) {
+    const u64 thr = wave_list_at<R>(lst, 64 * R - 1);
+    if (__ballot(batch < thr)) wave_merge_batch<R>(lst, batch);
+}
+
+template <int METRIC, int R>
+__global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
+    __shared__ uint32_t s_pend[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t q = (int64_t)blockIdx.x * 4 + w;
+    if (q >= a.nq) return;
+    const int k = a.k, K2 = a.K2;
+    const double dd = (double)a.d;
+    const float *qrow = a.Q + q * a.d;
+    double qs = 0.0;
+    for (int64_t j = lane; j < a.d; j += 64) {
+        const double x = (double)qrow[j];
+        qs = __builtin_fma(x, x, qs);
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) qs += __shfl_xor(qs, m, 64);
+    // rounded up by more than any summation-order difference to k_qstage's value
+    const double qnorm = __builtin_sqrt(qs) * (1.0 + 0x1p-30);
+    const int32_t *prow = a.probe + q * a.nprobe;
+    uint32_t *pend = s_pend[w];
+    int64_t ncand = 0;
+    unsigned long long n_rechecked = 0, n_rescans = 0;
+
+    u64 lst[R];
+    int pc = 0;  // pending survivors (storage rows) in pend[0..pc)
+    auto reset = [&]() {
+#pragma unroll
+        for (int r = 0; r < R; ++r) lst[r] = kEmptyKey;
+    };
+    auto flush_pending = [&]() {
+        if (!pc) return;
+        u64 key = kEmptyKey;
+        if (lane < pc) {
+            const int pos = (int)pend[lane];
+            key = make_key(exact_score<METRIC>(qrow, a.X, a.d, a.dpad, pos), a.ids[pos]);
+        }
+        n_rechecked += pc;
+        merge_batch_if<R>(lst, key);
+        pc = 0;
+        __builtin_amdgcn_wave_barrier();
+    };
+    auto add = [&](bool take, uint32_t pos) {
+        const u64 m = __ballot(take);
+        const int n = popc64(m);
+        if (!n) return;
+        if (pc + n > 64) flush_pending();
+        if (take) pend[pc + mbcnt64(m)] = pos;
+        pc += n;
+        __builtin_amdgcn_wave_barrier();
+    };
+    // the chunk's candidates, all exact (a list that may have dropped one)
+    auto rescan = [&](int p, int c, float T) {
+        ++n_rescans;
+        flush_pending();
+        const int tile0 = a.tile_off[p], ntl = a.tile_off[p + 1] - tile0;
+        const int t0 = c * a.bpc * kSBT, t1 = min(ntl, t0 + a.bpc * kSBT);
+        for (int t = t0; t < t1; ++t) {
+            const int pos = (tile0 + t) * kTile + lane;
+            const int gid = a.ids[pos];
+            u64 key = kEmptyKey;
+            if (gid >= 0) {
+                const float s = exact_score<METRIC>(qrow, a.X, a.d, a.dpad, pos);
+                if (s <= T) key = make_key(s, gid);
+            }
+            merge_batch_if<R>(lst, key);
+        }
+    };
+    // survivors of one list (pair slot s, chunk c) against the exact bound T
+    // survivors of one list (pair slot s, chunk c) against the exact bound T;
+    // a list whose K2-th key is still within lim may have dropped a needed
+    // candidate: the chunk is then re-scanned exactly instead
+    auto take_list = [&](const u64 *src, int p, int c, float T, double E) {
+        const double lim = s_lim<METRIC>((double)T, E, dd);
+        const u64 last = src[K2 - 1];
+        if (last != kEmptyKey && (double)key_score(last) <= lim) {
+            rescan(p, c, T);
+            return;
+        }
+        for (int e0 = 0; e0 < K2; e0 += 64) {
+            const u64 key = e0 + lane < K2 ? src[e0 + lane] : kEmptyKey;
+            const bool take = key != kEmptyKey && (double)key_score(key) <= lim;
+            add(take, (uint32_t)key);
+            if (!__any(take)) break;  // sorted: the rest is beyond lim
+        }
+    };
+    auto list_bound = [&](const u64 *src, double E) {
+        const u64 kk = src[k - 1];
+        return kk == kEmptyKey ? __builtin_inff() : __double2float_ru(bound_P<METRIC>((double)key_score(kk), E, dd));
+    };
+
+    if (a.per_partition) {
+        for (int s = 0; s < a.nprobe; ++s) {
+            const int p = prow[s];
+            reset();
+            if (p >= 0 && p < a.n_lists) {
+                ncand += a.list_size[p];
+                const double E = err_E<METRIC>(qnorm, (double)a.rmax[p], dd);
+                const u64 *base = a.partial + (q * a.nprobe + s) * (int64_t)a.nch_max * K2;
+                float T = __builtin_inff();
+                for (int c = 0; c < a.nch[p]; ++c) T = fminf(T, list_bound(base + (int64_t)c * K2, E));
+                for (int c = 0; c < a.nch[p]; ++c) take_list(base + (int64_t)c * K2, p, c, T, E);
+                flush_pending();
+            }
+            const int64_t o = (q * a.nprobe + s) * (int64_t)k;
+            emit_list<R>(lst, k, 0, METRIC, a.D + o, a.I + o);
+        }
+    } else {
+        reset();
+        float T = a.qbound ? ord2f(a.qbound[q]) : __builtin_inff();
+        if (a.qbound && a.qbound[q] == ~0u) T = __builtin_inff();
+        if (!a.qbound) {
+            for (int s = 0; s < a.nprobe; ++s) {
+                const int p = prow[s];
+                if (p < 0 || p >= a.n_lists) continue;
+                const double E = err_E<METRIC>(qnorm, (double)a.rmax[p], dd);
+                const u64 *base = a.partial + (q * a.nprobe + s) * (int64_t)a.nch_max * K2;
+                for (int c = 0; c < a.nch[p]; ++c) T = fminf(T, list_bound(base + (int64_t)c * K2, E));
+            }
+        }
+        for (int s = 0; s < a.nprobe; ++s) {
+            const int p = prow[s];
+            if (p < 0 || p >= a.n_lists) continue;
+            ncand += a.list_size[p];
+            const double E = err_E<METRIC>(qnorm, (double)a.rmax[p], dd);
+            const u64 *base = a.partial + (q * a.nprobe + s) * (int64_t)a.nch_max * K2;
+            for (int c = 0; c < a.nch[p]; ++c) take_list(base + (int64_t)c * K2, p, c, T, E);
+        }
+        flush_pending();
+        emit_list<R>(lst, k, a.dedup, METRIC, a.D + q * k, a.I + q * k);
+    }
+    if (lane == 0) {
+        if (a.ncand) a.ncand[q] = ncand;
+        if (a.stats) {
+            atomicAdd(a.stats + 5, n_rechecked);
+            if (n_rescans) atomicAdd(a.stats + 6, n_rescans);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ host side
+
+static int cu_count_s(int device) {
+    static int cached[64] = {0};
+    if (device < 0 || device >= 64) return 256;
+    if (!cached[device]) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || v <= 0)
+            v = 256;
+        cached[device] = v;
+    }
+    return cached[device];
+}
+
+// RL (list registers per half-wave, K2 = 32*RL >= k + 8), QR (queries per item)
+static int screen_rl(int64_t k) { return k <= 24 ? 1 : k <= 56 ? 2 : k <= 120 ? 4 : k <= 248 ? 8 : -1; }
+static int screen_qr(int rl) { return rl <= 1 ? 64 : 32; }
+static int screen_smem(int qr, int rl) {
+    return qr == 64 ? SSmem<64, 1>::total : rl == 2 ? SSmem<32, 2>::total : rl == 4 ? SSmem<32, 4>::total
+                                                                          : SSmem<32, 8>::total;
+}
+static int screen_occ(int qr, int rl) { return std::max(1, std::min(2, (160 * 1024) / screen_smem(qr, rl))); }
+
+struct SPlan {
+    int rl = 1, qr = 64, K2 = 32, bpc = 1, nch_max = 1, grid = 1, smem = 0;
+    int64_t max_qblk = 0;
+    size_t off_cnt, off_cursor, off_head, off_qoff, off_item, off_nch, off_qblk, off_qlist, off_qt, off_qn,
+        off_partial, off_qbound, total;
+};
+
+static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k) {
+    SPlan pl;
+    pl.rl = screen_rl(k);
+    pl.qr = screen_qr(pl.rl);
+    pl.K2 = 32 * pl.rl;
+    pl.smem = screen_smem(pl.qr, pl.rl);
+    const int64_t npairs = nq * nprobe;
+    pl.grid = cu_count_s(idx->device) * screen_occ(pl.qr, pl.rl);
+    static const int rounds = [] {
+        const char *e = getenv("LIRA_SCAN_ROUNDS");
+        return e && atoi(e) > 0 ? atoi(e) : 16;
+    }();
+    const int64_t target = (int64_t)rounds * pl.grid;
+    const int64_t est_items = (npairs + pl.qr - 1) / pl.qr + std::min<int64_t>(idx->n_lists, npairs);
+    const int64_t max_blocks = std::max<int64_t>(1, (idx->max_list_tiles + kSBT - 1) / kSBT);
+    if (est_items >= target) {
+        pl.bpc = (int)max_blocks;
+    } else {
+        const int64_t split = (target + est_items - 1) / std::max<int64_t>(1, est_items);
+        pl.bpc = (int)std::max<int64_t>(1, (max_blocks + split - 1) / split);
+    }
+    pl.nch_max = (int)((max_blocks + pl.bpc - 1) / pl.bpc);
+    pl.max_qblk = npairs / pl.qr + std::min<int64_t>(idx->n_lists, npairs) + 1;
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        size_t at = o;
+        o += (bytes + 255) & ~size_t(255);
+        return at;
+    };
+    const size_t nl = (size_t)idx->n_lists;
+    pl.off_cnt = take(nl * 4);
+    pl.off_cursor = take(nl * 4);
+    pl.off_head = take(16);
+    pl.off_qoff = take((nl + 1) * 4);
+    pl.off_item = take((nl + 1) * 4);
+    pl.off_nch = take(nl * 4);
+    pl.off_qblk = take((nl + 1) * 4);
+    pl.off_qlist = take((size_t)npairs * 4);
+    pl.off_qt = take((size_t)pl.max_qblk * pl.qr * idx->dpad * 4);
+    pl.off_qn = take((size_t)pl.max_qblk * pl.qr * 16);
+    pl.off_partial = take((size_t)npairs * pl.nch_max * pl.K2 * 8);
+    pl.off_qbound = take((size_t)nq * 4);
+    pl.total = o;
+    return pl;
+}
+
+bool screen_supported(const lira_index *idx, int64_t k) {
+    return screen_rl(k) > 0 && idx->xadj != nullptr && idx->n_lists <= 16384 / 2;
+}
+
+size_t screen_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k) {
+    return make_splan(idx, nq, nprobe, k).total;
+}
+
+template <int M, int RL, int QR>
+static hipError_t launch_screen(const ScreenArgs &a, const SPlan &pl, hipStream_t st) {
+    constexpr int OCC = (160 * 1024) / SSmem<QR, RL>::total >= 2 ? 2 : 1;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void *)k_screen<M, RL, QR, OCC>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    constexpr int smem = SSmem<QR, RL>::total;
+    hipLaunchKernelGGL((k_screen<M, RL, QR, OCC>), dim3(pl.grid), dim3(kSThreads), smem, st, a);
+    return hipGetLastError();
+}
+
+template <int M>
+static hipError_t launch_screen_rl(const ScreenArgs &a, const SPlan &pl, hipStream_t st) {
+    switch (pl.rl) {
+        case 1: return launch_screen<M, 1, 64>(a, pl, st);
+        case 2: return launch_screen<M, 2, 32>(a, pl, st);
+        case 4: return launch_screen<M, 4, 32>(a, pl, st);
+        default: return launch_screen<M, 8, 32>(a, pl, st);
+    }
+}
+
+template <int M>
+static void launch_smerge(int R, const SMergeArgs &m, hipStream_t st) {
+    const dim3 g((unsigned)((m.nq + 3) / 4)), b(256);
+    switch (R) {
+        case 1: hipLaunchKernelGGL((k_smerge<M, 1>), g, b, 0, st, m); break;
+        case 2: hipLaunchKernelGGL((k_smerge<M, 2>), g, b, 0, st, m); break;
+        case 4: hipLaunchKernelGGL((k_smerge<M, 4>), g, b, 0, st, m); break;
+        default: hipLaunchKernelGGL((k_smerge<M, 8>), g, b, 0, st, m); break;
+    }
+}
+
+// Precondition (scan_topk): screen_supported, nq > 0, nq*nprobe < 2^31, the
+// merge list size Rm valid.  ev = 4 profiling events or NULLs.
+int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe, int64_t nprobe, int64_t k,
+                unsigned flags, int Rm, float *out_D, int64_t *out_I, int64_t *out_ncand, void *ws,
+                size_t ws_bytes, hipStream_t st, hipEvent_t *ev) {
+    const bool dedup = (flags & LIRA_SCAN_DEDUP) != 0;
+    const bool per_part = (flags & LIRA_SCAN_PER_PARTITION) != 0;
+    const SPlan pl = make_splan(idx, nq, nprobe, k);
+    if (!ws) {
+        if (idx->ws_bytes < pl.total) {
+            if (idx->ws) hipFree(idx->ws);
+            idx->ws = nullptr;
+            idx->ws_bytes = 0;
+            LIRA_HIP_TRY(hipMalloc(&idx->ws, pl.total));
+            idx->ws_bytes = pl.total;
+        }
+        ws = idx->ws;
+    } else if (ws_bytes < pl.total) {
+        return fail(LIRA_EINVAL, "workspace too small: need " + std::to_string(pl.total) + " bytes");
+    }
+    char *w = (char *)ws;
+    int32_t *cnt = (int32_t *)(w + pl.off_cnt);
+    int32_t *cursor = (int32_t *)(w + pl.off_cursor);
+    int32_t *head = (int32_t *)(w + pl.off_head);
+    int32_t *qoff = (int32_t *)(w + pl.off_qoff);
+    int32_t *item_off = (int32_t *)(w + pl.off_item);
+    int32_t *nch = (int32_t *)(w + pl.off_nch);
+    int32_t *qblk = (int32_t *)(w + pl.off_qblk);
+    int32_t *qlist = (int32_t *)(w + pl.off_qlist);
+    float *QT = (float *)(w + pl.off_qt);
+    float4 *QN = (float4 *)(w + pl.off_qn);
+    u64 *partial = (u64 *)(w + pl.off_partial);
+    uint32_t *qbound = per_part ? nullptr : (uint32_t *)(w + pl.off_qbound);
+    const int64_t npairs = nq * nprobe;
+
+    if (ev[0]) LIRA_HIP_TRY(hipEventRecord(ev[0], st));
+    LIRA_HIP_TRY(hipMemsetAsync(w, 0, pl.off_qoff, st));  // cnt, cursor, head
+    if (qbound) LIRA_HIP_TRY(hipMemsetAsync(qbound, 0xff, (size_t)nq * 4, st));
+    LIRA_HIP_TRY(launch_plan(idx, probe, npairs, (int)nprobe, pl.bpc, pl.qr, cnt, cursor, qoff, item_off, nch,
+                             head, qlist, qblk, st));
+    if (pl.qr == 64)
+        hipLaunchKernelGGL(k_qstage<64>, dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
+                           (int)nprobe, (int)idx->n_lists, cnt, qoff, qlist, qblk, QT, QN);
+    else
+        hipLaunchKernelGGL(k_qstage<32>, dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
+                           (int)nprobe, (int)idx->n_lists, cnt, qoff, qlist, qblk, QT, QN);
+    LIRA_HIP_TRY(hipGetLastError());
+    if (ev[1]) LIRA_HIP_TRY(hipEventRecord(ev[1], st));
+
+    ScreenArgs a;
+    a.X = idx->X;
+    a.xadj = idx->xadj;
+    a.rmax = idx->rmax;
+    a.tile_off = idx->tile_off;
+    a.cnt = cnt;
+    a.item_off = item_off;
+    a.qblk_off = qblk;
+    a.head = head;
+    a.QT = QT;
+    a.QN = QN;
+    a.partial = partial;
+    a.qbound = qbound;
+    a.d = idx->d;
+    a.dpad = idx->dpad;
+    a.n_lists = (int)idx->n_lists;
+    a.nprobe = (int)nprobe;
+    a.k = (int)k;
+    a.bpc = pl.bpc;
+    a.nch_max = pl.nch_max;
+    a.stats = idx->stats_on ? (unsigned long long *)idx->stats : nullptr;
+    hipError_t e = idx->metric == LIRA_METRIC_L2 ? launch_screen_rl<LIRA_METRIC_L2>(a, pl, st)
+                                                 : launch_screen_rl<LIRA_METRIC_IP>(a, pl, st);
+    if (e != hipSuccess) return fail(LIRA_EHIP, std::string("k_screen launch: ") + hipGetErrorString(e));
+    if (ev[2]) LIRA_HIP_TRY(hipEventRecord(ev[2], st));
+
+    SMergeArgs m;
+    m.partial = partial;
+    m.probe = probe;
+    m.nch = nch;
+    m.list_size = idx->list_size;
+    m.tile_off = idx->tile_off;
+    m.ids = idx->ids;
+    m.Q = q;
+    m.X = idx->X;
+    m.rmax = idx->rmax;
+    m.qbound = qbound;
+    m.D = out_D;
+    m.I = out_I;
+    m.ncand = out_ncand;
+    m.nq = nq;
+    m.d = idx->d;
+    m.dpad = idx->dpad;
+    m.n_lists = (int)idx->n_lists;
+    m.nprobe = (int)nprobe;
+    m.k = (int)k;
+    m.K2 = pl.K2;
+    m.nch_max = pl.nch_max;
+    m.bpc = pl.bpc;
+    m.dedup = dedup ? 1 : 0;
+    m.per_partition = per_part ? 1 : 0;
+    m.stats = a.stats;
+    if (idx->metric == LIRA_METRIC_L2)
+        launch_smerge<LIRA_METRIC_L2>(Rm, m, st);
+    else
+        launch_smerge<LIRA_METRIC_IP>(Rm, m, st);
+    LIRA_HIP_TRY(hipGetLastError());
+    if (ev[3]) LIRA_HIP_TRY(hipEventRecord(ev[3], st));
+    return LIRA_OK;
+}
+
+}  // namespace lira

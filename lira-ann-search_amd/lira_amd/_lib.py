@@ -21,6 +21,7 @@ LIRA_SCAN_DEDUP = 1
 LIRA_SCAN_PER_PARTITION = 2
 LIRA_SCAN_FMA = 4
 LIRA_SCAN_NO_PRUNE = 8
+LIRA_SCAN_EXACT = 16
 LIRA_PROBE_NEAREST = 0
 LIRA_PROBE_THRESHOLD_GE = 1
 LIRA_PROBE_THRESHOLD_GT = 2

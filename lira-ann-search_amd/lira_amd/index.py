@@ -177,7 +177,7 @@ class PartitionedIndex:
     # --------------------------------------------------------------- search
     def search(self, q: torch.Tensor, probe: torch.Tensor, k: int, dedup: bool = True,
                per_partition: bool = False, out=None, stream=None, fma: bool = False,
-               prune: bool = True):
+               prune: bool = True, exact: bool = False):
         """Scan the probed lists of every query; exact top-k.
 
         q (nq, d) fp32, probe (nq, nprobe_max) int32 (-1 = unused slot).
@@ -187,7 +187,11 @@ class PartitionedIndex:
         Distances are search.cpp's sequential fp32 sums bit for bit; fma=True
         accumulates with fused multiply-adds instead (LIRA_SCAN_FMA: fewer
         operations, ~1e-6 relative difference, near-ties may order differently).
-        prune=False turns off the L2 early abandon (same results; for A/B).
+        By default every candidate is screened with an fp32 FMA dot product
+        under a rigorous error bound and only possible top-k members are
+        re-computed in search.cpp's arithmetic (same results); exact=True runs
+        the all-exact scan instead (LIRA_SCAN_EXACT), prune=False additionally
+        turns off its L2 early abandon (same results; for A/B).
         """
         q = _dev(q, torch.float32, self.device)
         probe = _dev(probe, torch.int32, self.device)
@@ -209,7 +213,8 @@ class PartitionedIndex:
         flags = (_lib.LIRA_SCAN_DEDUP if dedup else 0) | \
             (_lib.LIRA_SCAN_PER_PARTITION if per_partition else 0) | \
             (_lib.LIRA_SCAN_FMA if fma else 0) | \
-            (0 if prune else _lib.LIRA_SCAN_NO_PRUNE)
+            (0 if prune else _lib.LIRA_SCAN_NO_PRUNE) | \
+            (_lib.LIRA_SCAN_EXACT if exact else 0)
         with torch.cuda.device(self.device):
             _lib.call("lira_scan_topk", self._h, _lib.ptr(q), nq, _lib.ptr(probe), npm, int(k),
                       flags, _lib.ptr(D), _lib.ptr(I), _lib.ptr(ncand), None, 0,
@@ -246,7 +251,7 @@ class PartitionedIndex:
         with torch.cuda.device(self.device):
             _lib.call("lira_index_stats_read", self._h, v)
         return {"chunks_computed": v[0], "chunks_nominal": v[1], "blocks": v[2], "blocks_dropped": v[3],
-                "blocks_skipped": v[4]}
+                "blocks_skipped": v[4], "rechecked": v[5], "rescans": v[6], "survivors": v[7]}
 
     def memory_bytes(self) -> int:
         v = ctypes.c_int64()

@@ -66,16 +66,19 @@ def random_case(seed, n, d, b, nq, nprobe, metric, red=0.0, uniform=False):
 
 
 def check_vs_oracle(x, q, d2b, probe, b, k, metric, dedup=True):
+    # both scan paths: the default FMA screen + exact re-check, and the
+    # all-exact kernel (exact=True)
     idx = make_index(x, d2b, b, metric)
     off, ids = oracle.build_csr(d2b, b)
     vecs = oracle.gather_lists(x, off, ids)
     met = oracle.IP if metric == "inner_product" else oracle.L2
     rep = idx.max_replicas if dedup else 0
     Do, Io, nco = oracle.scan_topk(q, off, ids, vecs, probe, k, met, rep)
-    D, I, nc = run(idx, q, probe, k, dedup=dedup)
-    assert np.array_equal(I, Io)
-    assert np.array_equal(bits(D), bits(Do))
-    assert np.array_equal(nc, nco)
+    for exact in (False, True):
+        D, I, nc = run(idx, q, probe, k, dedup=dedup, exact=exact)
+        assert np.array_equal(I, Io), f"ids differ (exact={exact})"
+        assert np.array_equal(bits(D), bits(Do)), f"distances differ (exact={exact})"
+        assert np.array_equal(nc, nco)
     return idx
 
 
@@ -258,3 +261,57 @@ def test_early_abandon_exact(d, k, nq, ints):
     off, ids = oracle.build_csr(d2b, b)
     Dq, Iq = oracle.scan_per_partition(q, off, ids, oracle.gather_lists(x, off, ids), probe, k, oracle.L2)
     assert np.array_equal(Ip, Iq) and np.array_equal(bits(Dp), bits(Dq))
+
+
+@pytest.mark.parametrize("metric", ["L2", "inner_product"])
+@pytest.mark.parametrize("k", [24, 25, 56, 57, 120, 121, 248, 249])
+def test_screen_list_size_boundaries(metric, k):
+    # screened path: K2 = 32*RL >= k+8 list keys per row (RL 1/2/4/8, 64 or 32
+    # queries per item); k = 249 falls back to the all-exact kernel
+    x, q, d2b, probe = random_case(700 + k, 9000, 40, 10, 150, 4, metric, red=0.1)
+    check_vs_oracle(x, q, d2b, probe, 10, k, metric)
+
+
+@pytest.mark.parametrize("metric", ["L2", "inner_product"])
+def test_screen_large_norms_and_ties(metric):
+    # SIFT-like integer vectors (norms ~ 500, many exactly tied distances): the
+    # screening error bound scales with (|q| + R)^2 and must still admit every
+    # tied candidate at the k-th score
+    rng = np.random.default_rng(31)
+    n, d, b = 20000, 128, 16
+    c = rng.integers(0, 120, (b, d)).astype(np.float32)
+    lab = rng.integers(0, b, n)
+    x = np.clip(c[lab] + rng.integers(-6, 7, (n, d)), 0, 255).astype(np.float32)
+    q = np.clip(c[rng.integers(0, b, 200)] + rng.integers(-6, 7, (200, d)), 0, 255).astype(np.float32)
+    d2b = lab.astype(np.int32)[:, None]
+    probe = oracle.probe_nearest(oracle.centroid_dist(q, c), 3)
+    for k in (1, 10, 100):
+        check_vs_oracle(x, q, d2b, probe, b, k, metric)
+        check_vs_oracle(x, q, d2b, probe, b, k, metric, dedup=False)
+
+
+@pytest.mark.parametrize("metric", ["L2", "inner_product"])
+def test_screen_duplicate_rows_force_exact_rescan(metric):
+    # 400 exact copies of a few vectors: more candidates tie within the error
+    # band of the k-th than a row's screened list holds, so the merge must
+    # re-scan those chunks exactly (lira_index_stats_read()[6] counts it)
+    rng = np.random.default_rng(41)
+    d, b = 24, 4
+    base = rng.standard_normal((8, d), dtype=np.float32)
+    # copies stored contiguously, so one 256-candidate chunk holds ~100 of them
+    x = np.concatenate([np.repeat(base, 400, axis=0), rng.standard_normal((6000, d), dtype=np.float32)])
+    d2b = rng.integers(0, b, (x.shape[0], 1)).astype(np.int32)
+    q = np.concatenate([base, rng.standard_normal((40, d), dtype=np.float32)]).astype(np.float32)
+    probe = np.tile(np.arange(b, dtype=np.int32), (q.shape[0], 1))
+    check_vs_oracle(x, q, d2b, probe, b, 10, metric)
+    idx2 = check_vs_oracle(x, q, d2b, probe, b, 10, metric, dedup=False)
+    idx2.set_stats(True)
+    run(idx2, q, probe, 10)
+    st = idx2.stats_read()
+    idx2.set_stats(False)
+    assert st["rescans"] > 0
+    off, ids = oracle.build_csr(d2b, b)
+    met = oracle.IP if metric == "inner_product" else oracle.L2
+    Dq, Iq = oracle.scan_per_partition(q, off, ids, oracle.gather_lists(x, off, ids), probe, 10, met)
+    D, I, _ = run(idx2, q, probe, 10, per_partition=True, dedup=False)
+    assert np.array_equal(I, Iq) and np.array_equal(bits(D), bits(Dq))
