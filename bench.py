@@ -153,15 +153,19 @@ def main():
         return e0.elapsed_time(e1) / reps
 
     gemm_ms = event_ms(lambda: centroid_gemm(q, centres))
-    # the same scan with the exact pruning off (every candidate to the last dim):
-    # the brute-force cost the early abandon + triangle skip are measured against
+    # the same batch through the all-exact kernel (every candidate in
+    # search.cpp's arithmetic; LIRA_SCAN_EXACT) into separate buffers: its time
+    # is what the FMA screen is measured against, and its output must equal
+    # the screened path's bit for bit on the whole batch
+    De, Ie, nce = torch.empty_like(D), torch.empty_like(I), torch.empty_like(ncand)
     index.set_profiling(True)
     for _ in range(3):
-        index.search(q, probe, k, dedup=True, out=(D, I, ncand), fma=args.fma, prune=False)
+        index.search(q, probe, k, dedup=True, out=(De, Ie, nce), exact=True)
     torch.cuda.synchronize()
-    prof_np = index.profile_read()
+    prof_ex = index.profile_read()
     index.set_profiling(False)
-    scan_np_ms = prof_np["scan_ms"] / max(1, prof_np["calls"])
+    scan_ex_ms = prof_ex["scan_ms"] / max(1, prof_ex["calls"])
+    full_batch_equal = bool(torch.equal(I, Ie) and torch.equal(D.view(torch.int32), De.view(torch.int32)))
     rank_ms = event_ms(lambda: rank_nearest(q, centres, nprobe, out=probe, workspace=ws))
     gemm_tflops = 2.0 * nq * B * d / (gemm_ms * 1e-3) / 1e12
 
@@ -173,12 +177,11 @@ def main():
     merge_ms = prof["merge_ms"] / max(1, prof["calls"])
     plan_ms = prof["plan_ms"] / max(1, prof["calls"])
     achieved_gbs = bytes_launch / (scan_ms * 1e-3) / 1e9
-    valu_tops = flops_launch / (scan_ms * 1e-3) / 1e12
-    # lane-ops the VALU actually executed on distance math (incl. padding rows and
-    # candidates): per computed wave-chunk 16 dims x 2048 (query, candidate) pairs
-    exec_ops = work["chunks_computed"] * 16 * 2048 * (3 if metric == "L2" else 2)
-    exec_tops = exec_ops / (scan_ms * 1e-3) / 1e12
-    np_tops = cand * d * (3 if metric == "L2" else 2) / (scan_np_ms * 1e-3) / 1e12
+    # VALU: the screen issues one fp32 FMA per candidate-dim (v_pk_fma_f32: 2
+    # per lane-instruction, so the 78.6 T lane-op/s peak counts an FMA as one);
+    # the all-exact kernel 3 (L2: sub, mul, add) or 2 (IP: mul, add)
+    screen_tops = cand * d / (scan_ms * 1e-3) / 1e12
+    ex_tops = flops_launch / (scan_ex_ms * 1e-3) / 1e12
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_scan_{args.config}.json")
     if os.path.exists(pmc_path):
@@ -269,29 +272,24 @@ def main():
                              "achieved": traffic / (scan_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": traffic / (scan_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                              "source": "profiles/pmc_scan_%s.json (rocprofv3 PMC)" % args.config},
-                         "valu": {"achieved": exec_tops, "peak": VALU_F32_PEAK_TOPS,
-                                  "unit": "T lane-op/s (fp32 sub/mul/add executed, no FMA)",
-                                  "frac": exec_tops / VALU_F32_PEAK_TOPS,
-                                  "algorithmic": valu_tops,
-                                  "note": "achieved = distance lane-ops the kernel executed "
-                                          "(work counters) / k_scan time; algorithmic = "
-                                          "candidates*d*3 / time, which exceeds peak once the "
-                                          "early abandon skips work"},
-                         "no_prune": {"scan_ms": scan_np_ms, "valu_achieved": np_tops,
-                                      "valu_frac": np_tops / VALU_F32_PEAK_TOPS,
-                                      "speedup_from_pruning": scan_np_ms / scan_ms},
-                         "work": {**work, "computed_frac": work["chunks_computed"] /
-                                  max(1, work["chunks_nominal"]),
-                                  "dropped_block_frac": work["blocks_dropped"] /
-                                  max(1, work["blocks"] + work["blocks_skipped"]),
-                                  "skipped_block_frac": work["blocks_skipped"] /
-                                  max(1, work["blocks"] + work["blocks_skipped"])},
+                         "valu": {"kernel": "k_screen", "achieved": screen_tops, "peak": VALU_F32_PEAK_TOPS,
+                                  "unit": "T lane-op/s (fp32 FMA per candidate-dim)",
+                                  "frac": screen_tops / VALU_F32_PEAK_TOPS},
+                         "exact_kernel": {"kernel": "k_scan (LIRA_SCAN_EXACT)", "scan_ms": scan_ex_ms,
+                                          "valu_achieved": ex_tops, "valu_frac": ex_tops / VALU_F32_PEAK_TOPS,
+                                          "valu_unit": "T lane-op/s (%d fp32 ops per candidate-dim)"
+                                                       % (3 if metric == "L2" else 2),
+                                          "speedup_of_screen": scan_ex_ms / scan_ms,
+                                          "same_output_full_batch": full_batch_equal},
+                         "work": {"blocks": work["blocks"], "survivors": work["survivors"],
+                                  "rechecked": work["rechecked"], "rescans": work["rescans"],
+                                  "rechecked_per_query": work["rechecked"] / nq,
+                                  "rechecked_frac_of_candidates": work["rechecked"] / max(1, cand)},
                          "note": "SURVEY 8(d) algorithmic bytes = sum over queries of probed-bucket "
                                  "bytes; the partition-major scan reads a candidate tile once per "
-                                 "32-query block and the exact L2 early abandon drops blocks whose "
-                                 "partial sums already exceed every row's k-th score, so that "
-                                 "effective figure exceeds the HBM peak (frac > 1) while actual "
-                                 "HBM traffic stays far below it; see DESIGN.md"},
+                                 "64-query block, so that effective figure exceeds the HBM peak "
+                                 "(frac > 1) while actual HBM traffic stays far below it; the "
+                                 "binding resource is the fp32 FMA rate (valu); see DESIGN.md"},
             "kernels_ms_per_step": {"plan": plan_ms, "scan": scan_ms, "merge": merge_ms,
                                     "rank_nearest": rank_ms},
             "rank_gemm": {"kernel": "k_centroid_gemm (v_mfma_f32_32x32x2_f32)", "ms": gemm_ms,

@@ -126,6 +126,25 @@ __global__ __launch_bounds__(256) void k_row_norms(const float *X, const int32_t
     if (lane == 0 && r > 0.0f) atomicMax((unsigned int *)&rmax[tile_list[t]], __float_as_uint(r));
 }
 
+// Xr[pos][j] = X[tile][j][row]: one workgroup per tile, LDS transpose of
+// 64-dim slabs (reads and writes coalesced).
+__global__ __launch_bounds__(256) void k_rowmajor(const float *X, int64_t d, int64_t dpad, float *Xr) {
+    __shared__ float sl[64][65];
+    const int64_t t = blockIdx.x;
+    for (int64_t j0 = 0; j0 < d; j0 += 64) {
+        for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+            const int jj = i >> 6, r = i & 63;
+            if (j0 + jj < d) sl[jj][r] = X[(t * dpad + j0 + jj) * kTile + r];
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+            const int r = i >> 6, jj = i & 63;
+            if (j0 + jj < d) Xr[(t * kTile + r) * d + j0 + jj] = sl[jj][r];
+        }
+        __syncthreads();
+    }
+}
+
 __global__ void k_check_ids(const int32_t *ids, int64_t n, int64_t n_rows, int32_t *bad) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x)
@@ -137,6 +156,8 @@ static void free_storage(lira_index *idx) {
     if (idx->ids) hipFree(idx->ids);
     if (idx->tile_off) hipFree(idx->tile_off);
     if (idx->list_size) hipFree(idx->list_size);
+    if (idx->Xr) hipFree(idx->Xr);
+    idx->Xr = nullptr;
     if (idx->xadj) hipFree(idx->xadj);
     if (idx->rmax) hipFree(idx->rmax);
     idx->xadj = nullptr;
@@ -312,7 +333,8 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
         }
         if (tiles > 0) {
             if (hipMalloc(&idx->xadj, (size_t)tiles * kTile * 4) != hipSuccess ||
-                hipMalloc(&idx->rmax, (size_t)n_lists * 4) != hipSuccess) {
+                hipMalloc(&idx->rmax, (size_t)n_lists * 4) != hipSuccess ||
+                hipMalloc(&idx->Xr, (size_t)tiles * kTile * idx->d * 4) != hipSuccess) {
                 rc = fail(LIRA_ENOMEM, "hipMalloc of the row-norm arrays failed");
                 break;
             }
@@ -321,6 +343,8 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
                 hipLaunchKernelGGL(k_row_norms, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, idx->X,
                                    idx->ids, idx->d, idx->dpad, d_tlist, tiles, idx->metric, idx->xadj,
                                    idx->rmax);
+                hipLaunchKernelGGL(k_rowmajor, dim3((unsigned)tiles), dim3(256), 0, st, idx->X, idx->d, idx->dpad,
+                                   idx->Xr);
                 e = hipGetLastError();
             }
             if (e == hipSuccess) e = hipStreamSynchronize(st);
@@ -387,7 +411,8 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes) {
     if (!idx || !bytes) return fail(LIRA_EINVAL, "NULL argument");
     *bytes = idx->n_tiles * idx->dpad * kTile * 4 + idx->n_tiles * kTile * 4 + idx->n_lists * 8 +
              (idx->pivot ? idx->n_lists * idx->d * 4 + idx->n_tiles * 8 : 0) +
-             (idx->xadj ? idx->n_tiles * kTile * 4 + idx->n_lists * 4 : 0);
+             (idx->xadj ? idx->n_tiles * kTile * 4 + idx->n_lists * 4 : 0) +
+             (idx->Xr ? idx->n_tiles * kTile * idx->d * 4 : 0);
     return LIRA_OK;
 }
 

@@ -51,6 +51,10 @@ struct lira_index_impl {
     // padding rows; per list rmax >= max ||x|| over its rows (rounded up).
     float *xadj = nullptr;
     float *rmax = nullptr;
+    // Row-major copy of the tiles, [n_tiles*64][d] fp32 by storage row: the
+    // screened path's exact re-check reads one candidate's d values
+    // contiguously (a tile column would cost one cache line per value).
+    float *Xr = nullptr;
     int32_t *err = nullptr;        // device error word
     void *ws = nullptr;            // cached scan workspace
     size_t ws_bytes = 0;

@@ -68,7 +68,7 @@ struct ScreenArgs {
     const float *rmax;     // [n_lists]
     const int32_t *tile_off, *cnt, *item_off, *qblk_off;
     int32_t *head;
-    const float *QT;       // [qblk][4][dpad][RW]
+    const float *QT;       // [qblk][dpad][QR]
     const float4 *QN;      // [qblk*QR]: qn, |q| (up), pair (int bits), 0
     u64 *partial;          // [pair][nch_max][K2]
     uint32_t *qbound;      // [nq] f2ord(bound on the final k-th exact score); NULL = off
@@ -123,7 +123,6 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
                                                 int n_lists, const int32_t *cnt, const int32_t *qoff,
                                                 const int32_t *qlist, const int32_t *qblk_off, float *QT,
                                                 float4 *QN) {
-    constexpr int RW = QR / 4;
     __shared__ int pairs[QR];
     __shared__ int s_v;
     const int b = blockIdx.x;
@@ -146,7 +145,7 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
         const int64_t j = i - (int64_t)r * dpad;
         const int pr = pairs[r];
         const float val = pr >= 0 && j < d ? Q[(int64_t)(pr / nprobe) * d + j] : 0.0f;
-        QT[(((int64_t)b * 4 + r / RW) * dpad + j) * RW + (r % RW)] = val;
+        QT[((int64_t)b * dpad + j) * QR + r] = val;
     }
     const int lane = threadIdx.x & 63;
     for (int r = threadIdx.x >> 6; r < QR; r += 4) {
@@ -171,7 +170,9 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
 template <int QR, int RL>
 struct SSmem {
     static constexpr int RW = QR / 4, K2 = 32 * RL;
-    static constexpr int kX = 2 * kSBT * kSDK * kTile * 4;  // 32 KiB ring
+    static constexpr int kXS = kSBT * kSDK * kTile * 4;      // X chunk: 16 KiB
+    static constexpr int kQS = kSDK * QR * 4;                // Q chunk: 4 / 2 KiB
+    static constexpr int kX = 2 * (kXS + kQS);               // 2-deep ring of both
     static constexpr int kLists = QR * K2 * 8;
     static constexpr int kBufs = QR * 32 * 8;
     static constexpr int kMeta = 64 + QR * 4 * 3;           // item; pair, bufc, (spare) per row
@@ -262,7 +263,7 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen(ScreenArgs a) {
     typedef SSmem<QR, RL> S;
     constexpr int RW = S::RW, K2 = S::K2;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    float *Xs = (float *)smem;                               // [2][4 tiles][16 dims][64]
+    float *Xs = (float *)smem;  // [2] x {X: [4 tiles][16 dims][64], Q: [16 dims][QR]}
     u64 *lists = (u64 *)(smem + S::kX);                      // [QR][K2]
     u64 *bufs = (u64 *)(smem + S::kX + S::kLists);           // [QR][32]
     int *meta = (int *)(smem + S::kX + S::kLists + S::kBufs);
@@ -328,16 +329,23 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen(ScreenArgs a) {
         const double my_E = err_E<METRIC>(my_qnorm, R, dd);
         u64 *my_list = lists + my_row * K2;
 
-        cfloat *qt = (cfloat *)(a.QT + ((int64_t)gqb * 4 + wave) * a.dpad * RW);
+        const float4 *qtg = (const float4 *)(a.QT + (int64_t)gqb * a.dpad * QR);
 
+        // Stage chunk (tb, jc) into ring slot `slot` by LDS-DMA: wave w moves
+        // 1 KiB of each of the block's 4 tile chunks (tiles past the block's
+        // end re-read its last valid one; masked by xadj = +inf) and, for
+        // w < QR/16, 1 KiB of the Q chunk
         auto stage = [&](int tb, int jc, int slot) {
             const int ntv = min(kSBT, tb_end - tb);
             const float4 *src = Xg + (int64_t)(tile0 + tb) * tstride + jc * (kTile / 4) + tid;
-            const uint32_t dst = __builtin_amdgcn_readfirstlane(
-                xs_lds + (uint32_t)(slot * (kSBT * kSDK * kTile) + wave * 256) * 4u);
+            const uint32_t base = xs_lds + (uint32_t)(slot * (S::kXS + S::kQS));
+            const uint32_t dst = __builtin_amdgcn_readfirstlane(base + (uint32_t)(wave * 256) * 4u);
 #pragma unroll
             for (int i = 0; i < kSBT; ++i)
                 sglds16(src + min(i, ntv - 1) * tstride, dst + (uint32_t)(i * (kSDK * kTile) * 4));
+            if (wave < QR / 16)
+                sglds16(qtg + (int64_t)jc * (QR / 4) + wave * 64 + lane,
+                        __builtin_amdgcn_readfirstlane(base + (uint32_t)S::kXS + (uint32_t)wave * 1024u));
         };
         int slot = 0;
         if (tb_begin < tb_end) stage(tb_begin, 0, 0);
@@ -367,17 +375,26 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen(ScreenArgs a) {
                     }
                     if (ntb < tb_end) stage(ntb, njc, slot ^ 1);
                 }
-                const float *xp = Xs + slot * (kSBT * kSDK * kTile) + ti * (kSDK * kTile) + col;
-                cfloat *qc = qt + (int64_t)c * kSDK * RW;
+                const float *sb = (const float *)((const char *)Xs + slot * (S::kXS + S::kQS));
+                const float *xp = sb + ti * (kSDK * kTile) + col;
+                const float *qp = sb + S::kXS / 4 + wave * RW;  // this wave's rows; broadcast reads
 #pragma unroll
                 for (int j = 0; j < kSDK; ++j) {
                     const f4 x = *(const f4 *)(xp + j * kTile);
                     const f2 xa = x.xy, xb = x.zw;
+                    float qv[RW];
+#pragma unroll
+                    for (int r4 = 0; r4 < RW / 4; ++r4) {
+                        const f4 q4 = *(const f4 *)(qp + j * QR + r4 * 4);
+                        qv[r4 * 4 + 0] = q4.x;
+                        qv[r4 * 4 + 1] = q4.y;
+                        qv[r4 * 4 + 2] = q4.z;
+                        qv[r4 * 4 + 3] = q4.w;
+                    }
 #pragma unroll
                     for (int r = 0; r < RW; ++r) {
-                        const float qv = qc[j * RW + r];
-                        acc[r][0] = __builtin_elementwise_fma(xa, (f2)(qv), acc[r][0]);
-                        acc[r][1] = __builtin_elementwise_fma(xb, (f2)(qv), acc[r][1]);
+                        acc[r][0] = __builtin_elementwise_fma(xa, (f2)(qv[r]), acc[r][0]);
+                        acc[r][1] = __builtin_elementwise_fma(xb, (f2)(qv[r]), acc[r][1]);
                     }
                 }
                 slot ^= 1;
@@ -504,7 +521,7 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen(ScreenArgs a) {
 struct SMergeArgs {
     const u64 *partial;
     const int32_t *probe, *nch, *list_size, *tile_off, *ids;
-    const float *Q, *X, *rmax;
+    const float *Q, *Xr, *rmax;
     const uint32_t *qbound;
     float *D;
     int64_t *I;
@@ -515,17 +532,18 @@ struct SMergeArgs {
 };
 
 // exact score of the candidate at storage row pos (search.cpp:253-269 order)
+// (Xr: the row-major copy, so one lane reads its candidate contiguously)
 template <int METRIC>
-__device__ __forceinline__ float exact_score(const float *q, const float *X, int64_t d, int64_t dpad, int pos) {
-    const float *xp = X + (int64_t)(pos >> 6) * dpad * kTile + (pos & 63);
+__device__ __forceinline__ float exact_score(const float *q, const float *Xr, int64_t d, int pos) {
+    const float *xp = Xr + (int64_t)pos * d;
     float acc = 0.0f;
 #pragma unroll 16
     for (int64_t j = 0; j < d; ++j) {
         if (METRIC == LIRA_METRIC_L2) {
-            const float df = q[j] - xp[j * kTile];
+            const float df = q[j] - xp[j];
             acc = acc + df * df;
         } else {
-            acc = acc + q[j] * xp[j * kTile];
+            acc = acc + q[j] * xp[j];
         }
     }
     return METRIC == LIRA_METRIC_L2 ? acc : -acc;
@@ -571,7 +589,7 @@ __global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
         u64 key = kEmptyKey;
         if (lane < pc) {
             const int pos = (int)pend[lane];
-            key = make_key(exact_score<METRIC>(qrow, a.X, a.d, a.dpad, pos), a.ids[pos]);
+            key = make_key(exact_score<METRIC>(qrow, a.Xr, a.d, pos), a.ids[pos]);
         }
         n_rechecked += pc;
         merge_batch_if<R>(lst, key);
@@ -598,7 +616,7 @@ __global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
             const int gid = a.ids[pos];
             u64 key = kEmptyKey;
             if (gid >= 0) {
-                const float s = exact_score<METRIC>(qrow, a.X, a.d, a.dpad, pos);
+                const float s = exact_score<METRIC>(qrow, a.Xr, a.d, pos);
                 if (s <= T) key = make_key(s, gid);
             }
             merge_batch_if<R>(lst, key);
@@ -753,7 +771,7 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
 }
 
 bool screen_supported(const lira_index *idx, int64_t k) {
-    return screen_rl(k) > 0 && idx->xadj != nullptr && idx->n_lists <= 16384 / 2;
+    return screen_rl(k) > 0 && idx->xadj != nullptr && idx->Xr != nullptr && idx->n_lists <= 16384 / 2;
 }
 
 size_t screen_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k) {
@@ -879,7 +897,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     m.tile_off = idx->tile_off;
     m.ids = idx->ids;
     m.Q = q;
-    m.X = idx->X;
+    m.Xr = idx->Xr;
     m.rmax = idx->rmax;
     m.qbound = qbound;
     m.D = out_D;
