@@ -1103,20 +1103,21 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
     return LIRA_OK;
 }
 
-// Plan kernels for another scan kernel (lira_screen.hip): one group of
-// virtual partitions, `qr` queries per item, query-block offsets in qblk_off.
+// Plan kernels for another scan kernel (lira_screen.hip): `groups` groups of
+// virtual partitions (2: every query's first probe slot ahead of the rest),
+// `qr` queries per item, query-block offsets in qblk_off.
 // cnt, cursor and head must be zeroed by the caller.
 hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npairs, int nprobe, int bpc,
-                       int qr, int32_t *cnt, int32_t *cursor, int32_t *qoff, int32_t *item_off,
+                       int qr, int groups, int32_t *cnt, int32_t *cursor, int32_t *qoff, int32_t *item_off,
                        int32_t *nch, int32_t *head, int32_t *qlist, int32_t *qblk_off, hipStream_t st) {
-    const int nl = (int)idx->n_lists;
+    const int nl = (int)idx->n_lists, nv = groups * nl;
     const unsigned pg = (unsigned)((npairs + kPairsPerBlock - 1) / kPairsPerBlock);
-    const size_t hc = nl <= kHistMax ? (size_t)nl * 4 : 0;
-    const size_t hf = nl <= kHistMax / 2 ? (size_t)nl * 8 : 0;
-    hipLaunchKernelGGL(k_count, dim3(pg), dim3(256), hc, st, probe, npairs, nl, nprobe, 1, 1, cnt, idx->err);
-    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, nl, bpc, qr, qoff,
+    const size_t hc = nv <= kHistMax ? (size_t)nv * 4 : 0;
+    const size_t hf = nv <= kHistMax / 2 ? (size_t)nv * 8 : 0;
+    hipLaunchKernelGGL(k_count, dim3(pg), dim3(256), hc, st, probe, npairs, nl, nprobe, 1, groups, cnt, idx->err);
+    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, nv, bpc, qr, qoff,
                        item_off, nch, head, qblk_off);
-    hipLaunchKernelGGL(k_fill, dim3(pg), dim3(256), hf, st, probe, npairs, nl, nprobe, 1, 1, qoff, cursor,
+    hipLaunchKernelGGL(k_fill, dim3(pg), dim3(256), hf, st, probe, npairs, nl, nprobe, 1, groups, qoff, cursor,
                        qlist);
     return hipGetLastError();
 }

@@ -50,7 +50,7 @@
 namespace lira {
 
 hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npairs, int nprobe, int bpc,
-                       int qr, int32_t *cnt, int32_t *cursor, int32_t *qoff, int32_t *item_off,
+                       int qr, int groups, int32_t *cnt, int32_t *cursor, int32_t *qoff, int32_t *item_off,
                        int32_t *nch, int32_t *head, int32_t *qlist, int32_t *qblk_off, hipStream_t st);
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -73,7 +73,7 @@ struct ScreenArgs {
     u64 *partial;          // [pair][nch_max][K2]
     uint32_t *qbound;      // [nq] f2ord(bound on the final k-th exact score); NULL = off
     int64_t d, dpad;
-    int n_lists, nprobe, k, bpc, nch_max;
+    int n_lists, n_virt, nprobe, k, bpc, nch_max;  // n_virt = groups * n_lists (virtual partitions)
     unsigned long long *stats;  // NULL or lira_index_set_stats counters
 };
 
@@ -120,15 +120,15 @@ __device__ __forceinline__ float row_h(double lim, double qn, double qnorm, doub
 // Block b = one query block (virtual partition v, block qb of QR pairs).
 template <int QR>
 __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64_t dpad, int nprobe,
-                                                int n_lists, const int32_t *cnt, const int32_t *qoff,
+                                                int n_virt, const int32_t *cnt, const int32_t *qoff,
                                                 const int32_t *qlist, const int32_t *qblk_off, float *QT,
                                                 float4 *QN) {
     __shared__ int pairs[QR];
     __shared__ int s_v;
     const int b = blockIdx.x;
-    if (b >= qblk_off[n_lists]) return;
+    if (b >= qblk_off[n_virt]) return;
     if (threadIdx.x == 0) {
-        int lo = 0, hi = n_lists - 1;  // last v with qblk_off[v] <= b
+        int lo = 0, hi = n_virt - 1;  // last v with qblk_off[v] <= b
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
             if (qblk_off[mid] <= b) lo = mid; else hi = mid - 1;
@@ -188,6 +188,16 @@ __device__ __forceinline__ void sglds16(const void *gsrc, uint32_t lds_addr) {
         : "=&s"(keep)
         : "v"(gsrc), "s"(lds_addr)
         : "memory");
+}
+
+// acc += x * splat(q.lo) / splat(q.hi) on packed fp32.  Inline asm: hipcc
+// otherwise copies every odd-register splat source with a v_mov first (one
+// extra VALU op per 8 FMAs), while op_sel reads either half in place.
+__device__ __forceinline__ void pkfma_lo(f2 &acc, f2 x, f2 q) {
+    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(acc) : "v"(x), "v"(q));
+}
+__device__ __forceinline__ void pkfma_hi(f2 &acc, f2 x, f2 q) {
+    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(x), "v"(q));
 }
 
 // 64 u32 values, one per lane: ascending bitonic sort.
@@ -258,6 +268,87 @@ __device__ __forceinline__ int s_append(u64 *L, u64 *buf, int bc, u64 k0, u64 k1
     return bc;
 }
 
+// s_append for NV keys per lane (v-major order), bit v of pmask = key v passes.
+template <int RL, int NV>
+__device__ __forceinline__ int s_append_n(u64 *L, u64 *buf, int bc, const u64 (&key)[NV], int pmask,
+                                          unsigned long long *stats) {
+    u64 b[NV];
+    int pos[NV], tot = 0;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        b[v] = __ballot((pmask >> v) & 1);
+        pos[v] = tot + mbcnt64(b[v]);
+        tot += popc64(b[v]);
+    }
+    if (stats && lane_id() == 0) atomicAdd(stats + 7, (unsigned long long)tot);
+    int consumed = 0;
+    for (;;) {
+        const int room = 32 - bc;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            const int rel = pos[v] - consumed;
+            if (((pmask >> v) & 1) && rel >= 0 && rel < room) buf[bc + rel] = key[v];
+        }
+        const int placed = min(room, tot - consumed);
+        bc += placed;
+        consumed += placed;
+        __builtin_amdgcn_wave_barrier();
+        if (bc == 32) {
+            s_flush<RL>(L, buf, 32);
+            bc = 0;
+        }
+        if (consumed >= tot) break;
+    }
+    return bc;
+}
+
+// Four rows at once (MFMA layout): lane group g = lane>>4 appends its own
+// row (rowbase + 4g) from its 16 lanes' keys; a row whose buffer fills is
+// merged into its list (one row at a time, rare).
+template <int RL>
+__device__ __forceinline__ void s_append4(u64 *lists, u64 *bufs, int *m_bufc, int rowbase, const u64 (&key)[16],
+                                          int pm, unsigned long long *stats) {
+    constexpr int K2 = 32 * RL;
+    const int g = lane_id() >> 4;
+    const u64 gmask = 0xffffull << (16 * g);
+    const int row = rowbase + 4 * g;
+    u64 b[16];
+    int pos[16], tot = 0;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        b[v] = __ballot((pm >> v) & 1) & gmask;
+        pos[v] = tot + mbcnt64(b[v]);
+        tot += popc64(b[v]);
+    }
+    if (stats && (lane_id() & 15) == 0 && tot) atomicAdd(stats + 7, (unsigned long long)tot);
+    int bc = m_bufc[row];
+    int consumed = 0;
+    for (;;) {
+        const int room = 32 - bc;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const int rel = pos[v] - consumed;
+            if (((pm >> v) & 1) && rel >= 0 && rel < room) bufs[row * 32 + bc + rel] = key[v];
+        }
+        const int placed = min(room, tot - consumed);
+        bc += placed;
+        consumed += placed;
+        __builtin_amdgcn_wave_barrier();
+        // lanes 0, 16, 32, 48 vote for their group's row (bit 16g of a u64)
+        u64 full = __ballot(bc == 32 && (lane_id() & 15) == 0);
+        while (full) {
+            const int gg = __builtin_ctzll(full) >> 4;
+            full &= full - 1;
+            const int r = rowbase + 4 * gg;
+            s_flush<RL>(lists + r * K2, bufs + r * 32, 32);
+        }
+        if (bc == 32) bc = 0;
+        if (!__any(consumed < tot)) break;
+    }
+    if ((lane_id() & 15) == 0) m_bufc[row] = bc;
+    __builtin_amdgcn_wave_barrier();
+}
+
 template <int METRIC, int RL, int QR, int OCC>
 __global__ __launch_bounds__(kSThreads, OCC) void k_screen(ScreenArgs a) {
     typedef SSmem<QR, RL> S;
@@ -285,7 +376,7 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen(ScreenArgs a) {
             const int ok = item < a.head[1];
             int v = 0, qb = 0, ch = 0;
             if (ok) {
-                int lo = 0, hi = a.n_lists - 1;
+                int lo = 0, hi = a.n_virt - 1;
                 while (lo < hi) {
                     const int mid = (lo + hi + 1) >> 1;
                     if (a.item_off[mid] <= item) lo = mid; else hi = mid - 1;
@@ -303,10 +394,11 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen(ScreenArgs a) {
         }
         __syncthreads();
         if (!meta[0]) break;
-        const int p = __builtin_amdgcn_readfirstlane(meta[1]);
+        const int vp = __builtin_amdgcn_readfirstlane(meta[1]);  // virtual partition
+        const int p = vp >= a.n_lists ? vp - a.n_lists : vp;
         const int qb = __builtin_amdgcn_readfirstlane(meta[2]);
         const int ch = __builtin_amdgcn_readfirstlane(meta[3]);
-        const int gqb = __builtin_amdgcn_readfirstlane(a.qblk_off[p]) + qb;
+        const int gqb = __builtin_amdgcn_readfirstlane(a.qblk_off[vp]) + qb;
         if (tid < QR) {
             m_pair[tid] = __float_as_int(a.QN[(int64_t)gqb * QR + tid].z);
             m_bufc[tid] = 0;
@@ -382,19 +474,18 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen(ScreenArgs a) {
                 for (int j = 0; j < kSDK; ++j) {
                     const f4 x = *(const f4 *)(xp + j * kTile);
                     const f2 xa = x.xy, xb = x.zw;
-                    float qv[RW];
 #pragma unroll
                     for (int r4 = 0; r4 < RW / 4; ++r4) {
                         const f4 q4 = *(const f4 *)(qp + j * QR + r4 * 4);
-                        qv[r4 * 4 + 0] = q4.x;
-                        qv[r4 * 4 + 1] = q4.y;
-                        qv[r4 * 4 + 2] = q4.z;
-                        qv[r4 * 4 + 3] = q4.w;
-                    }
-#pragma unroll
-                    for (int r = 0; r < RW; ++r) {
-                        acc[r][0] = __builtin_elementwise_fma(xa, (f2)(qv[r]), acc[r][0]);
-                        acc[r][1] = __builtin_elementwise_fma(xb, (f2)(qv[r]), acc[r][1]);
+                        const f2 q01 = q4.xy, q23 = q4.zw;
+                        pkfma_lo(acc[r4 * 4 + 0][0], xa, q01);
+                        pkfma_lo(acc[r4 * 4 + 0][1], xb, q01);
+                        pkfma_hi(acc[r4 * 4 + 1][0], xa, q01);
+                        pkfma_hi(acc[r4 * 4 + 1][1], xb, q01);
+                        pkfma_lo(acc[r4 * 4 + 2][0], xa, q23);
+                        pkfma_lo(acc[r4 * 4 + 2][1], xb, q23);
+                        pkfma_hi(acc[r4 * 4 + 3][0], xa, q23);
+                        pkfma_hi(acc[r4 * 4 + 3][1], xb, q23);
                     }
                 }
                 slot ^= 1;
@@ -547,6 +638,303 @@ __device__ __forceinline__ float exact_score(const float *q, const float *Xr, in
         }
     }
     return METRIC == LIRA_METRIC_L2 ? acc : -acc;
+}
+
+// ---- the MFMA screening kernel (default) ------------------------------------
+// Same items, ring, thresholds and lists as k_screen (QR = 64), but the dot
+// products run on v_mfma_f32_16x16x4_f32, which on gfx950 is bitwise an
+// fmaf chain in k order (cdna_hip_programming.md, FP32-input MFMA) -- the
+// screen's error model holds unchanged -- and reaches the f32 peak that the
+// VALU version (k_screen) cannot feed from LDS.  Wave w owns rows 16w..16w+15
+// and all 256 candidates of a block as 16 tiles of 16 x 16: tile (t, i) has
+// candidate 4j+i of block tile t in column j, so one ds_read_b128 per lane
+// loads the B fragments of 4 tiles.  Lane l (g = l>>4, j = l&15) holds, per
+// tile, rows 4g..4g+3 of column j: 16 candidates x 4 rows.
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+template <int METRIC, int RL, int OCC>
+__global__ __launch_bounds__(kSThreads, OCC) void k_screen_m(ScreenArgs a) {
+    constexpr int QR = 64;
+    typedef SSmem<QR, RL> S;
+    constexpr int K2 = S::K2;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float *Xs = (float *)smem;  // [2] x {X: [4 tiles][16 dims][64], Q: [16 dims][64]}
+    u64 *lists = (u64 *)(smem + S::kX);
+    u64 *bufs = (u64 *)(smem + S::kX + S::kLists);
+    int *meta = (int *)(smem + S::kX + S::kLists + S::kBufs);
+    int *m_pair = meta + 16, *m_bufc = meta + 16 + QR;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, cj = lane & 15;
+    const int k = a.k;
+    const double dd = (double)a.d;
+    const float4 *Xg = (const float4 *)a.X;
+    const uint32_t xs_lds = (uint32_t)(uintptr_t)(lds_void_t *)Xs;
+    const int tstride = (int)a.dpad * (kTile / 4);
+    const int nchunk = (int)(a.dpad / kSDK);
+
+    for (;;) {
+        if (tid == 0) {
+            const int item = atomicAdd(&a.head[0], 1);
+            const int ok = item < a.head[1];
+            int v = 0, qb = 0, ch = 0;
+            if (ok) {
+                int lo = 0, hi = a.n_virt - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (a.item_off[mid] <= item) lo = mid; else hi = mid - 1;
+                }
+                v = lo;
+                const int local = item - a.item_off[v];
+                const int nqb = (a.cnt[v] + QR - 1) / QR;
+                ch = local / nqb;
+                qb = local - ch * nqb;
+            }
+            meta[0] = ok;
+            meta[1] = v;
+            meta[2] = qb;
+            meta[3] = ch;
+        }
+        __syncthreads();
+        if (!meta[0]) break;
+        const int vp = __builtin_amdgcn_readfirstlane(meta[1]);  // virtual partition
+        const int p = vp >= a.n_lists ? vp - a.n_lists : vp;
+        const int qb = __builtin_amdgcn_readfirstlane(meta[2]);
+        const int ch = __builtin_amdgcn_readfirstlane(meta[3]);
+        const int gqb = __builtin_amdgcn_readfirstlane(a.qblk_off[vp]) + qb;
+        if (tid < QR) {
+            m_pair[tid] = __float_as_int(a.QN[(int64_t)gqb * QR + tid].z);
+            m_bufc[tid] = 0;
+        }
+        for (int i = tid; i < QR * K2; i += kSThreads) lists[i] = kEmptyKey;
+        __syncthreads();
+
+        const int tile0 = __builtin_amdgcn_readfirstlane(a.tile_off[p]);
+        const int ntl = __builtin_amdgcn_readfirstlane(a.tile_off[p + 1]) - tile0;
+        const int tb_begin = ch * a.bpc * kSBT;
+        const int tb_end = min(ntl, tb_begin + a.bpc * kSBT);
+        const double R = (double)a.rmax[p];
+
+        // lanes 0..15 of wave w hold row 16w + lane's threshold state
+        const int my_row = wave * 16 + cj;
+        const float4 qrec = a.QN[(int64_t)gqb * QR + my_row];
+        const int my_pair = __float_as_int(qrec.z);
+        const int my_q = my_pair >= 0 ? my_pair / a.nprobe : -1;
+        const double my_qn = (double)qrec.x, my_qnorm = (double)qrec.y;
+        const double my_E = err_E<METRIC>(my_qnorm, R, dd);
+        u64 *my_list = lists + my_row * K2;
+        // this lane's 4 output rows 4g + reg: qn for the screened scores
+        float qn_r[4];
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) qn_r[reg] = __shfl((float)my_qn, 4 * g + reg, 64);
+
+        const float4 *qtg = (const float4 *)(a.QT + (int64_t)gqb * a.dpad * QR);
+        auto stage = [&](int tb, int jc, int slot) {
+            const int ntv = min(kSBT, tb_end - tb);
+            const float4 *src = Xg + (int64_t)(tile0 + tb) * tstride + jc * (kTile / 4) + tid;
+            const uint32_t base = xs_lds + (uint32_t)(slot * (S::kXS + S::kQS));
+            const uint32_t dst = __builtin_amdgcn_readfirstlane(base + (uint32_t)(wave * 256) * 4u);
+#pragma unroll
+            for (int i = 0; i < kSBT; ++i)
+                sglds16(src + min(i, ntv - 1) * tstride, dst + (uint32_t)(i * (kSDK * kTile) * 4));
+            sglds16(qtg + (int64_t)jc * (QR / 4) + wave * 64 + lane,
+                    __builtin_amdgcn_readfirstlane(base + (uint32_t)S::kXS + (uint32_t)wave * 1024u));
+        };
+        int slot = 0;
+        if (tb_begin < tb_end) stage(tb_begin, 0, 0);
+
+#pragma unroll 1
+        for (int tb = tb_begin; tb < tb_end; tb += kSBT) {
+            const int ntv = min(kSBT, tb_end - tb);
+            f4 xa[4];  // xadj of my 16 candidates: tile t, i = 0..3 (+inf: padding / past the block)
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                xa[t] = t < ntv ? *(const f4 *)&a.xadj[(int64_t)(tile0 + tb + t) * kTile + 4 * cj] : (f4)(__builtin_inff());
+            const uint32_t pub = a.qbound && my_q >= 0
+                ? __hip_atomic_load(a.qbound + my_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
+
+            f4v acc[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[i] = (f4v)(0.0f);
+
+#pragma unroll 1
+            for (int c = 0; c < nchunk; ++c) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                {
+                    int njc = (c + 1) * kSDK, ntb = tb;
+                    if (c + 1 == nchunk) {
+                        njc = 0;
+                        ntb = tb + kSBT;
+                    }
+                    if (ntb < tb_end) stage(ntb, njc, slot ^ 1);
+                }
+                const float *sb = (const float *)((const char *)Xs + slot * (S::kXS + S::kQS));
+                const float *xb = sb + g * kTile + 4 * cj;                   // + t*1024 + 4s*64
+                const float *qa = sb + S::kXS / 4 + g * QR + wave * 16 + cj;  // + 4s*64
+#pragma unroll
+                for (int s4 = 0; s4 < kSDK / 4; ++s4) {
+                    const float av = qa[s4 * 4 * QR];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const f4 bv = *(const f4 *)(xb + t * (kSDK * kTile) + s4 * 4 * kTile);
+                        acc[t * 4 + 0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv.x, acc[t * 4 + 0], 0, 0, 0);
+                        acc[t * 4 + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv.y, acc[t * 4 + 1], 0, 0, 0);
+                        acc[t * 4 + 2] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv.z, acc[t * 4 + 2], 0, 0, 0);
+                        acc[t * 4 + 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv.w, acc[t * 4 + 3], 0, 0, 0);
+                    }
+                }
+                slot ^= 1;
+            }
+
+            // ---- thresholds (lanes 0..15: row 16w + lane), then per lane for its rows 4g + reg
+            float h_l;
+            {
+                const u64 kk = my_list[k - 1];
+                double T = kk == kEmptyKey ? __builtin_inf() : bound_P<METRIC>((double)key_score(kk), my_E, dd);
+                if (pub != ~0u) T = fmin(T, (double)ord2f(pub));
+                h_l = my_pair < 0 ? __builtin_inff()
+                                  : row_h<METRIC>(s_lim<METRIC>(T, my_E, dd), my_qn, my_qnorm, R);
+            }
+            if (a.stats && lane == 0 && wave == 0) atomicAdd(a.stats + 2, 1ull);
+            float h_r[4];
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) h_r[reg] = __shfl(h_l, 4 * g + reg, 64);
+
+            // ---- selection: per output register reg, lane group g holds row
+            // 4g + reg's 16 candidates; the four rows of a reg go together
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                float h = h_r[reg];
+                int pm = 0;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const f2 w0 = (f2){acc[t * 4 + 0][reg], acc[t * 4 + 1][reg]} - xa[t].xy;
+                    const f2 w1 = (f2){acc[t * 4 + 2][reg], acc[t * 4 + 3][reg]} - xa[t].zw;
+                    pm |= ((w0.x >= h) | ((w0.y >= h) << 1) | ((w1.x >= h) << 2) | ((w1.y >= h) << 3)) << (4 * t);
+                }
+                if (!__any(pm)) continue;  // wave-uniform: none of the four rows has a candidate
+                float sc[16];  // screened scores (+inf: padding)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const float av = xa[i >> 2][i & 3];
+                    const float dv = acc[i][reg];
+                    const bool real = av != __builtin_inff();
+                    if (METRIC == LIRA_METRIC_L2)
+                        sc[i] = real ? __builtin_fmaf(-2.0f, dv, qn_r[reg] + 2.0f * av) : __builtin_inff();
+                    else
+                        sc[i] = real ? -dv : __builtin_inff();
+                    if (!real) pm &= ~(1 << i);
+                }
+                if (__any(h == -__builtin_inff()) && k <= 64) {
+                    // a row without a bound yet: t = ceil(k/16) smallest of each
+                    // of its 16 lanes, j = ceil(k/t) <= 16 over those lanes
+                    float m4[4] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        float v = sc[i] == sc[i] ? sc[i] : __builtin_inff();
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const float lo = fminf(m4[u], v), hi = fmaxf(m4[u], v);
+                            m4[u] = lo;
+                            v = hi;
+                        }
+                    }
+                    const int t = (k + 15) / 16;
+                    uint32_t key16 = f2ord(t <= 1 ? m4[0] : t == 2 ? m4[1] : t == 3 ? m4[2] : m4[3]);
+#pragma unroll
+                    for (int size = 2; size <= 16; size <<= 1)  // ascending sort within each 16-lane group
+#pragma unroll
+                        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                            const uint32_t o = (uint32_t)__shfl_xor((int)key16, stride, 64);
+                            const bool lower = (cj & stride) == 0, asc = (cj & size) == 0;
+                            key16 = (lower == asc) ? min(key16, o) : max(key16, o);
+                        }
+                    const int j = (k + t - 1) / t;
+                    const float B = ord2f((uint32_t)__shfl((int)key16, 16 * g + j - 1, 64));
+                    if (h == -__builtin_inff() && B < __builtin_inff()) {
+                        const double qnorm_r = (double)__shfl((float)my_qnorm, 4 * g + reg, 64);
+                        const double E_r = err_E<METRIC>(qnorm_r, R, dd);
+                        h = row_h<METRIC>(s_lim<METRIC>(bound_P<METRIC>((double)B, E_r, dd), E_r, dd),
+                                          (double)qn_r[reg], qnorm_r, R);
+                        int pm2 = 0;
+#pragma unroll
+                        for (int i = 0; i < 16; ++i) pm2 |= (acc[i][reg] - xa[i >> 2][i & 3] >= h) << i;
+                        pm &= pm2;
+                    }
+                }
+                u64 key[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    key[i] = ((u64)f2ord(sc[i]) << 32) | (uint32_t)((tile0 + tb + (i >> 2)) * kTile + 4 * cj + (i & 3));
+                s_append4<RL>(lists, bufs, m_bufc, wave * 16 + reg, key, pm, a.stats);
+            }
+        }
+
+        // ---- flush buffers, emit lists, publish bounds (wave-owned rows)
+#pragma unroll 1
+        for (int r = 0; r < 16; ++r) {
+            const int row = wave * 16 + r;
+            const int bc = m_bufc[row];
+            if (bc > 0) s_flush<RL>(lists + row * K2, bufs + row * 32, bc);
+            const int pr = m_pair[row];
+            if (pr >= 0) {
+                u64 *dst = a.partial + ((int64_t)pr * a.nch_max + ch) * K2;
+                for (int e = lane; e < K2; e += 64) dst[e] = lists[row * K2 + e];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (lane < 16 && a.qbound && my_q >= 0) {
+            const u64 kk = my_list[k - 1];
+            if (kk != kEmptyKey) {
+                const double P = bound_P<METRIC>((double)key_score(kk), my_E, dd);
+                atomicMin(a.qbound + my_q, f2ord(__double2float_ru(P)));
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---- seed: a finite starting bound for every query ----------------------
+// One wave per query: exact scores of the first kSeedTiles tiles of its first
+// probed partition; with t = ceil(k/64) smallest per lane and j = ceil(k/t),
+// the j-th smallest lane value has >= k real (distinct) candidates at or below
+// it, so it bounds the query's final k-th exact score.  Written to qbound
+// before k_screen, so no item starts unbounded (which would push a whole
+// first block per row through the selection).
+static constexpr int kSeedTiles = 8;
+template <int METRIC>
+__global__ __launch_bounds__(256) void k_seed(const float *Q, const int32_t *probe, int nprobe, int n_lists,
+                                              const int32_t *tile_off, const int32_t *ids, const float *Xr,
+                                              int64_t d, int64_t nq, int k, uint32_t *qbound) {
+    const int lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    const int p = probe[q * nprobe];
+    if (p < 0 || p >= n_lists) return;
+    const int tile0 = tile_off[p], nt = min(kSeedTiles, tile_off[p + 1] - tile0);
+    const float *qrow = Q + q * d;
+    float m[4] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};  // 4 smallest
+    for (int t = 0; t < nt; ++t) {
+        const int pos = (tile0 + t) * kTile + lane;
+        if (ids[pos] < 0) continue;
+        float s = exact_score<METRIC>(qrow, Xr, d, pos);
+        if (!(s == s)) continue;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float lo = fminf(m[i], s), hi = fmaxf(m[i], s);
+            m[i] = lo;
+            s = hi;
+        }
+    }
+    const int t = (k + 63) / 64;
+    if (t > 4) return;
+    const float mine = t == 1 ? m[0] : t == 2 ? m[1] : t == 3 ? m[2] : m[3];
+    const uint32_t sorted = wave_sort64_u32(f2ord(mine));
+    const int j = (k + t - 1) / t;
+    const float B = ord2f((uint32_t)__shfl((int)sorted, j - 1, 64));
+    if (lane == 0 && B < __builtin_inff()) qbound[q] = f2ord(B);
 }
 
 template <int R>
@@ -718,7 +1106,7 @@ static int screen_smem(int qr, int rl) {
 static int screen_occ(int qr, int rl) { return std::max(1, std::min(2, (160 * 1024) / screen_smem(qr, rl))); }
 
 struct SPlan {
-    int rl = 1, qr = 64, K2 = 32, bpc = 1, nch_max = 1, grid = 1, smem = 0;
+    int rl = 1, qr = 64, K2 = 32, bpc = 1, nch_max = 1, grid = 1, smem = 0, mfma = 1;
     int64_t max_qblk = 0;
     size_t off_cnt, off_cursor, off_head, off_qoff, off_item, off_nch, off_qblk, off_qlist, off_qt, off_qn,
         off_partial, off_qbound, total;
@@ -726,12 +1114,20 @@ struct SPlan {
 
 static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k) {
     SPlan pl;
+    static const int mfma_env = [] {
+        const char *e = getenv("LIRA_SCAN_MFMA");  // 0 = VALU screen, 2 = MFMA for every k it supports
+        return e ? atoi(e) : 1;
+    }();
     pl.rl = screen_rl(k);
-    pl.qr = screen_qr(pl.rl);
+    // MFMA screen where its LDS (64-query lists) still fits 2 workgroups per
+    // CU; larger k (RL 4: DEEP10M's k = 100) measured faster on the VALU one
+    pl.mfma = mfma_env == 2 ? pl.rl <= 4 : mfma_env && pl.rl <= 2;
+    pl.qr = pl.mfma ? 64 : screen_qr(pl.rl);
     pl.K2 = 32 * pl.rl;
-    pl.smem = screen_smem(pl.qr, pl.rl);
+    pl.smem = pl.mfma ? (pl.rl == 1 ? SSmem<64, 1>::total : pl.rl == 2 ? SSmem<64, 2>::total : SSmem<64, 4>::total)
+                      : screen_smem(pl.qr, pl.rl);
     const int64_t npairs = nq * nprobe;
-    pl.grid = cu_count_s(idx->device) * screen_occ(pl.qr, pl.rl);
+    pl.grid = cu_count_s(idx->device) * std::max(1, std::min(2, (160 * 1024) / pl.smem));
     static const int rounds = [] {
         const char *e = getenv("LIRA_SCAN_ROUNDS");
         return e && atoi(e) > 0 ? atoi(e) : 16;
@@ -746,14 +1142,14 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
         pl.bpc = (int)std::max<int64_t>(1, (max_blocks + split - 1) / split);
     }
     pl.nch_max = (int)((max_blocks + pl.bpc - 1) / pl.bpc);
-    pl.max_qblk = npairs / pl.qr + std::min<int64_t>(idx->n_lists, npairs) + 1;
+    pl.max_qblk = npairs / pl.qr + std::min<int64_t>(2 * idx->n_lists, npairs) + 1;
     size_t o = 0;
     auto take = [&](size_t bytes) {
         size_t at = o;
         o += (bytes + 255) & ~size_t(255);
         return at;
     };
-    const size_t nl = (size_t)idx->n_lists;
+    const size_t nl = 2 * (size_t)idx->n_lists;  // up to two groups of virtual partitions
     pl.off_cnt = take(nl * 4);
     pl.off_cursor = take(nl * 4);
     pl.off_head = take(16);
@@ -793,8 +1189,30 @@ static hipError_t launch_screen(const ScreenArgs &a, const SPlan &pl, hipStream_
     return hipGetLastError();
 }
 
+template <int M, int RL>
+static hipError_t launch_screen_m(const ScreenArgs &a, const SPlan &pl, hipStream_t st) {
+    constexpr int OCC = (160 * 1024) / SSmem<64, RL>::total >= 2 ? 2 : 1;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void *)k_screen_m<M, RL, OCC>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    constexpr int smem = SSmem<64, RL>::total;
+    hipLaunchKernelGGL((k_screen_m<M, RL, OCC>), dim3(pl.grid), dim3(kSThreads), smem, st, a);
+    return hipGetLastError();
+}
+
 template <int M>
 static hipError_t launch_screen_rl(const ScreenArgs &a, const SPlan &pl, hipStream_t st) {
+    if (pl.mfma) {
+        switch (pl.rl) {
+            case 1: return launch_screen_m<M, 1>(a, pl, st);
+            case 2: return launch_screen_m<M, 2>(a, pl, st);
+            default: return launch_screen_m<M, 4>(a, pl, st);
+        }
+    }
     switch (pl.rl) {
         case 1: return launch_screen<M, 1, 64>(a, pl, st);
         case 2: return launch_screen<M, 2, 32>(a, pl, st);
@@ -852,15 +1270,41 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     if (ev[0]) LIRA_HIP_TRY(hipEventRecord(ev[0], st));
     LIRA_HIP_TRY(hipMemsetAsync(w, 0, pl.off_qoff, st));  // cnt, cursor, head
     if (qbound) LIRA_HIP_TRY(hipMemsetAsync(qbound, 0xff, (size_t)nq * 4, st));
-    LIRA_HIP_TRY(launch_plan(idx, probe, npairs, (int)nprobe, pl.bpc, pl.qr, cnt, cursor, qoff, item_off, nch,
-                             head, qlist, qblk, st));
+    // Two groups (every query's first probe slot -- its nearest partition, where
+    // most of its top-k lives -- queued ahead of the rest) when the bound is
+    // shared across a query's items and the first slots still fill blocks of
+    // QR queries per partition: later items then start from tight bounds.
+    static const int groups_env = [] {
+        const char *e = getenv("LIRA_SCAN_TWO_PHASE");
+        return e ? atoi(e) : 1;
+    }();
+    const int groups = qbound && groups_env && nprobe >= 2 &&
+                               (groups_env == 2 || nq >= (int64_t)pl.qr * idx->n_lists) ? 2 : 1;
+    const int nvirt = groups * (int)idx->n_lists;
+    LIRA_HIP_TRY(launch_plan(idx, probe, npairs, (int)nprobe, pl.bpc, pl.qr, groups, cnt, cursor, qoff, item_off,
+                             nch, head, qlist, qblk, st));
     if (pl.qr == 64)
         hipLaunchKernelGGL(k_qstage<64>, dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
-                           (int)nprobe, (int)idx->n_lists, cnt, qoff, qlist, qblk, QT, QN);
+                           (int)nprobe, nvirt, cnt, qoff, qlist, qblk, QT, QN);
     else
         hipLaunchKernelGGL(k_qstage<32>, dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
-                           (int)nprobe, (int)idx->n_lists, cnt, qoff, qlist, qblk, QT, QN);
+                           (int)nprobe, nvirt, cnt, qoff, qlist, qblk, QT, QN);
     LIRA_HIP_TRY(hipGetLastError());
+    static const int seed_env = [] {
+        const char *e = getenv("LIRA_SCAN_SEED");
+        return e && e[0] == '0' ? 0 : 1;
+    }();
+    if (qbound && seed_env) {
+        if (idx->metric == LIRA_METRIC_L2)
+            hipLaunchKernelGGL(k_seed<LIRA_METRIC_L2>, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, q, probe,
+                               (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->Xr, idx->d, nq,
+                               (int)k, qbound);
+        else
+            hipLaunchKernelGGL(k_seed<LIRA_METRIC_IP>, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, q, probe,
+                               (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->Xr, idx->d, nq,
+                               (int)k, qbound);
+        LIRA_HIP_TRY(hipGetLastError());
+    }
     if (ev[1]) LIRA_HIP_TRY(hipEventRecord(ev[1], st));
 
     ScreenArgs a;
@@ -879,6 +1323,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     a.d = idx->d;
     a.dpad = idx->dpad;
     a.n_lists = (int)idx->n_lists;
+    a.n_virt = nvirt;
     a.nprobe = (int)nprobe;
     a.k = (int)k;
     a.bpc = pl.bpc;
