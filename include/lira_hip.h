@@ -211,8 +211,9 @@ int lira_index_profile_read(lira_index *idx, double *plan_ms, double *scan_ms, d
  *   [5] candidates re-computed exactly by the screened path's merge,
  *   [6] chunks it re-scanned exactly (a screened list that may have dropped
  *       a needed candidate), [7] screened survivors appended to row lists.
- * The screened path (default) counts [2], [5], [6], [7]; the all-exact scan
- * (LIRA_SCAN_EXACT) [0]..[4].
+ * The screened path (default) counts [0] as the (query row, candidate) pairs
+ * it screened (padding rows included; x dpad = FMAs executed), and [2], [4],
+ * [5], [6], [7]; the all-exact scan (LIRA_SCAN_EXACT) [0]..[4] as above.
  * lira_index_stats_read synchronises the device, copies the 8 sums to `out8`
  * (host) and resets them.  Costs a few atomics per block: keep it off when
  * timing.

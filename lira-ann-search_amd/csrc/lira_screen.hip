@@ -75,6 +75,11 @@ struct ScreenArgs {
     int64_t d, dpad;
     int n_lists, n_virt, nprobe, k, bpc, nch_max;  // n_virt = groups * n_lists (virtual partitions)
     unsigned long long *stats;  // NULL or lira_index_set_stats counters
+    // L2 triangle-inequality block skip (k_screen_m): queries, per-list pivot,
+    // per-tile radius bounds (lira_abi.hip k_list_pivot / k_tile_stats); NULL = off
+    const float *Q;
+    const float *pivot;
+    const float2 *tstat;
 };
 
 // ---- error model (double) -------------------------------------------------
@@ -175,7 +180,9 @@ struct SSmem {
     static constexpr int kX = 2 * (kXS + kQS);               // 2-deep ring of both
     static constexpr int kLists = QR * K2 * 8;
     static constexpr int kBufs = QR * 32 * 8;
-    static constexpr int kMeta = 64 + QR * 4 * 3;           // item; pair, bufc, (spare) per row
+    // item; pair, bufc, (spare) per row; block-skip (A, B) x 2 parities and
+    // ||q - pivot|| (lo, hi) doubles per row
+    static constexpr int kMeta = 64 + QR * 4 * 3 + 2 * QR * 8 + QR * 16;
     static constexpr int total = kX + kLists + kBufs + kMeta;
 };
 
@@ -500,7 +507,10 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen(ScreenArgs a) {
                 h_l = my_pair < 0 ? __builtin_inff()  // no query: nothing passes
                                   : row_h<METRIC>(s_lim<METRIC>(T, my_E, dd), my_qn, my_qnorm, R);
             }
-            if (a.stats && lane == 0 && wave == 0) atomicAdd(a.stats + 2, 1ull);
+            if (a.stats && lane == 0) {
+                if (wave == 0) atomicAdd(a.stats + 2, 1ull);
+                atomicAdd(a.stats + 0, (unsigned long long)RW * kSBT * kTile);  // (row, candidate) pairs screened
+            }
 
             // ---- selection.  Phase 1 (unrolled): per row, which of my 4
             // candidates pass h; rows where any lane has one set `hit`
@@ -663,6 +673,9 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen_m(ScreenArgs a) {
     u64 *bufs = (u64 *)(smem + S::kX + S::kLists);
     int *meta = (int *)(smem + S::kX + S::kLists + S::kBufs);
     int *m_pair = meta + 16, *m_bufc = meta + 16 + QR;
+    float2 *tri_s = (float2 *)(meta + 16 + 3 * QR);         // [2][QR]
+    double *dq_s = (double *)(meta + 16 + 3 * QR + 4 * QR); // [QR][2]
+    const bool TRI = METRIC == LIRA_METRIC_L2 && a.tstat != nullptr;
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -741,18 +754,114 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen_m(ScreenArgs a) {
             sglds16(qtg + (int64_t)jc * (QR / 4) + wave * 64 + lane,
                     __builtin_amdgcn_readfirstlane(base + (uint32_t)S::kXS + (uint32_t)wave * 1024u));
         };
+
+        // Triangle-inequality block skip (L2), as k_scan: ||q - x|| >= |
+        // ||q - c_p|| - ||x - c_p|| | with per-tile bounds lo <= ||x - c_p||
+        // <= hi, so a block whose radius range lies farther than rad_r from
+        // ||q_r - c_p|| cannot hold a pair with exact score <= T_r, rad_r =
+        // sqrt((T_r + d 2^-140) / (1 - (d+4) 2^-24)).  ||q_r - c_p|| in double:
+        // row = 16w + (lane & 15), 4 lanes per row.
+        if (TRI) {
+            const int rrow = wave * 16 + cj;
+            const int rp = m_pair[rrow];
+            double sq = 0.0;
+            if (rp >= 0) {
+                const float *qr = a.Q + (int64_t)(rp / a.nprobe) * a.d;
+                const float *pv = a.pivot + (int64_t)p * a.d;
+                for (int j = g; j < (int)a.d; j += 4) {
+                    const double df = (double)qr[j] - (double)pv[j];
+                    sq = __builtin_fma(df, df, sq);
+                }
+            }
+            sq += __shfl_xor(sq, 16, 64);
+            sq += __shfl_xor(sq, 32, 64);
+            if (g == 0) {
+                const double dq = __builtin_sqrt(sq), m = (double)(a.d + 8) * 0x1p-50;
+                dq_s[rrow * 2] = dq * (1.0 - m);
+                dq_s[rrow * 2 + 1] = dq * (1.0 + m);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        // Thresholds at a block's start (lanes 0..15: row 16w + lane): the
+        // dot-product test h, and (TRI) the row's skip interval into tri_s[par]
+        // (two parities: a wave refreshing the next block's never races one
+        // still testing with this block's).
+        auto refresh = [&](int par) {
+            const uint32_t pub = a.qbound && my_q >= 0
+                ? __hip_atomic_load(a.qbound + my_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
+            const u64 kk = my_list[k - 1];
+            double T = kk == kEmptyKey ? __builtin_inf() : bound_P<METRIC>((double)key_score(kk), my_E, dd);
+            if (pub != ~0u) T = fmin(T, (double)ord2f(pub));
+            const float h = my_pair < 0 ? __builtin_inff()
+                                        : row_h<METRIC>(s_lim<METRIC>(T, my_E, dd), my_qn, my_qnorm, R);
+            if (TRI && lane < 16) {
+                float2 ab = make_float2(-__builtin_inff(), __builtin_inff());  // never skip
+                const double F = 1.0 - (dd + 4.0) * kU;
+                if (my_pair < 0) {
+                    ab = make_float2(__builtin_inff(), -__builtin_inff());       // no query: always
+                } else if (T < 1e300 && F > 0.5) {
+                    const double rad = __builtin_sqrt((fmax(T, 0.0) + dd * 0x1p-140) / F) * (1.0 + 0x1p-40);
+                    double A = dq_s[my_row * 2] - rad, B = dq_s[my_row * 2 + 1] + rad;
+                    A -= __builtin_fabs(A) * 0x1p-50;
+                    B += __builtin_fabs(B) * 0x1p-50;
+                    ab = make_float2(__double2float_rd(A), __double2float_ru(B));
+                }
+                tri_s[par * QR + my_row] = ab;
+            }
+            __builtin_amdgcn_wave_barrier();
+            return h;
+        };
+        auto block_range = [&](int tb, float &lo, float &hi) {
+            const int ntv = min(kSBT, tb_end - tb);
+            lo = __builtin_inff();
+            hi = -__builtin_inff();
+            for (int i = 0; i < ntv; ++i) {
+                const float2 st = a.tstat[tile0 + tb + i];
+                lo = fminf(lo, st.x);
+                hi = fmaxf(hi, st.y);
+            }
+        };
+        // first block at or after t that some row may need (workgroup-uniform:
+        // every wave tests all 64 rows, one per lane, against the same LDS values)
+        auto skip_from = [&](int t, int par) {
+            if (TRI) {
+                const float2 ab = tri_s[par * QR + lane];
+                while (t < tb_end) {
+                    float lo, hi;
+                    block_range(t, lo, hi);
+                    if (!__all(hi < ab.x || lo > ab.y)) break;
+                    if (a.stats && tid == 0) atomicAdd(a.stats + 4, 1ull);
+                    t += kSBT;
+                }
+            }
+            return t;
+        };
+
         int slot = 0;
-        if (tb_begin < tb_end) stage(tb_begin, 0, 0);
+        int tb = tb_begin;
+        if (TRI) {
+            refresh(1);
+            __syncthreads();
+            tb = skip_from(tb_begin, 1);
+        }
+        if (tb < tb_end) stage(tb, 0, 0);
 
 #pragma unroll 1
-        for (int tb = tb_begin; tb < tb_end; tb += kSBT) {
+        for (int bi = 0, next_tb = tb_end; tb < tb_end; tb = next_tb, ++bi) {
             const int ntv = min(kSBT, tb_end - tb);
+            const float h_l = refresh(bi & 1);
             f4 xa[4];  // xadj of my 16 candidates: tile t, i = 0..3 (+inf: padding / past the block)
 #pragma unroll
             for (int t = 0; t < 4; ++t)
                 xa[t] = t < ntv ? *(const f4 *)&a.xadj[(int64_t)(tile0 + tb + t) * kTile + 4 * cj] : (f4)(__builtin_inff());
-            const uint32_t pub = a.qbound && my_q >= 0
-                ? __hip_atomic_load(a.qbound + my_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
+            // a wave whose 16 rows all skip the block computes nothing for it
+            bool wdead = false;
+            if (TRI) {
+                float lo, hi;
+                block_range(tb, lo, hi);
+                const float2 ab = tri_s[(bi & 1) * QR + wave * 16 + cj];
+                wdead = __all(hi < ab.x || lo > ab.y);
+            }
 
             f4v acc[16];
 #pragma unroll
@@ -766,38 +875,36 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen_m(ScreenArgs a) {
                     int njc = (c + 1) * kSDK, ntb = tb;
                     if (c + 1 == nchunk) {
                         njc = 0;
-                        ntb = tb + kSBT;
+                        ntb = skip_from(tb + kSBT, bi & 1);
+                        next_tb = ntb;
                     }
                     if (ntb < tb_end) stage(ntb, njc, slot ^ 1);
                 }
-                const float *sb = (const float *)((const char *)Xs + slot * (S::kXS + S::kQS));
-                const float *xb = sb + g * kTile + 4 * cj;                   // + t*1024 + 4s*64
-                const float *qa = sb + S::kXS / 4 + g * QR + wave * 16 + cj;  // + 4s*64
+                if (!wdead) {
+                    const float *sb = (const float *)((const char *)Xs + slot * (S::kXS + S::kQS));
+                    const float *xb = sb + g * kTile + 4 * cj;                   // + t*1024 + 4s*64
+                    const float *qa = sb + S::kXS / 4 + g * QR + wave * 16 + cj;  // + 4s*64
 #pragma unroll
-                for (int s4 = 0; s4 < kSDK / 4; ++s4) {
-                    const float av = qa[s4 * 4 * QR];
+                    for (int s4 = 0; s4 < kSDK / 4; ++s4) {
+                        const float av = qa[s4 * 4 * QR];
 #pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        const f4 bv = *(const f4 *)(xb + t * (kSDK * kTile) + s4 * 4 * kTile);
-                        acc[t * 4 + 0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv.x, acc[t * 4 + 0], 0, 0, 0);
-                        acc[t * 4 + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv.y, acc[t * 4 + 1], 0, 0, 0);
-                        acc[t * 4 + 2] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv.z, acc[t * 4 + 2], 0, 0, 0);
-                        acc[t * 4 + 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv.w, acc[t * 4 + 3], 0, 0, 0);
+                        for (int t = 0; t < 4; ++t) {
+                            const f4 bv = *(const f4 *)(xb + t * (kSDK * kTile) + s4 * 4 * kTile);
+                            acc[t * 4 + 0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv.x, acc[t * 4 + 0], 0, 0, 0);
+                            acc[t * 4 + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv.y, acc[t * 4 + 1], 0, 0, 0);
+                            acc[t * 4 + 2] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv.z, acc[t * 4 + 2], 0, 0, 0);
+                            acc[t * 4 + 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv.w, acc[t * 4 + 3], 0, 0, 0);
+                        }
                     }
                 }
                 slot ^= 1;
             }
-
-            // ---- thresholds (lanes 0..15: row 16w + lane), then per lane for its rows 4g + reg
-            float h_l;
-            {
-                const u64 kk = my_list[k - 1];
-                double T = kk == kEmptyKey ? __builtin_inf() : bound_P<METRIC>((double)key_score(kk), my_E, dd);
-                if (pub != ~0u) T = fmin(T, (double)ord2f(pub));
-                h_l = my_pair < 0 ? __builtin_inff()
-                                  : row_h<METRIC>(s_lim<METRIC>(T, my_E, dd), my_qn, my_qnorm, R);
+            if (a.stats && lane == 0) {
+                if (wave == 0) atomicAdd(a.stats + 2, 1ull);
+                if (!wdead) atomicAdd(a.stats + 0, 16ull * kSBT * kTile);  // (row, candidate) pairs screened
             }
-            if (a.stats && lane == 0 && wave == 0) atomicAdd(a.stats + 2, 1ull);
+            if (wdead) continue;
+
             float h_r[4];
 #pragma unroll
             for (int reg = 0; reg < 4; ++reg) h_r[reg] = __shfl(h_l, 4 * g + reg, 64);
@@ -1308,6 +1415,14 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     if (ev[1]) LIRA_HIP_TRY(hipEventRecord(ev[1], st));
 
     ScreenArgs a;
+    a.Q = q;
+    static const int tri_env = [] {
+        const char *e = getenv("LIRA_SCAN_PRUNE");
+        return e && e[0] == '0' ? 0 : 1;
+    }();
+    const bool tri = tri_env && !(flags & LIRA_SCAN_NO_PRUNE);
+    a.pivot = tri ? idx->pivot : nullptr;
+    a.tstat = tri ? idx->tstat : nullptr;
     a.X = idx->X;
     a.xadj = idx->xadj;
     a.rmax = idx->rmax;
