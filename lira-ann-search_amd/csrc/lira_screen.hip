@@ -80,6 +80,7 @@ struct ScreenArgs {
     const float *Q;
     const float *pivot;
     const float2 *tstat;
+    int dbg;  // timing experiments only (env LIRA_SCAN_DEBUG; results invalid): 1 = no MFMA, 2 = no selection
 };
 
 // ---- error model (double) -------------------------------------------------
@@ -172,17 +173,21 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
 }
 
 // ---- the screening kernel --------------------------------------------------
-template <int QR, int RL>
+template <int QR, int RL, bool MF = false>  // MF: the k_screen_m carve (xadj stage, block ranges)
 struct SSmem {
     static constexpr int RW = QR / 4, K2 = 32 * RL;
     static constexpr int kXS = kSBT * kSDK * kTile * 4;      // X chunk: 16 KiB
     static constexpr int kQS = kSDK * QR * 4;                // Q chunk: 4 / 2 KiB
-    static constexpr int kX = 2 * (kXS + kQS);               // 2-deep ring of both
+    static constexpr int kXA = MF ? kSBT * kTile * 4 : 0;    // the block's xadj (first chunk): 1 KiB
+    static constexpr int kStage = kXS + kQS + kXA;
+    static constexpr int kX = 2 * kStage;                    // 2-deep ring
     static constexpr int kLists = QR * K2 * 8;
     static constexpr int kBufs = QR * 32 * 8;
     // item; pair, bufc, (spare) per row; block-skip (A, B) x 2 parities and
-    // ||q - pivot|| (lo, hi) doubles per row
-    static constexpr int kMeta = 64 + QR * 4 * 3 + 2 * QR * 8 + QR * 16;
+    // ||q - pivot|| (lo, hi) doubles per row; (MF) the radius range of each of
+    // an item's first kBR blocks
+    static constexpr int kBR = MF ? 128 : 0;
+    static constexpr int kMeta = 64 + QR * 4 * 3 + 2 * QR * 8 + QR * 16 + kBR * 8;
     static constexpr int total = kX + kLists + kBufs + kMeta;
 };
 
@@ -437,7 +442,7 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen(ScreenArgs a) {
         auto stage = [&](int tb, int jc, int slot) {
             const int ntv = min(kSBT, tb_end - tb);
             const float4 *src = Xg + (int64_t)(tile0 + tb) * tstride + jc * (kTile / 4) + tid;
-            const uint32_t base = xs_lds + (uint32_t)(slot * (S::kXS + S::kQS));
+            const uint32_t base = xs_lds + (uint32_t)(slot * S::kStage);
             const uint32_t dst = __builtin_amdgcn_readfirstlane(base + (uint32_t)(wave * 256) * 4u);
 #pragma unroll
             for (int i = 0; i < kSBT; ++i)
@@ -474,7 +479,7 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen(ScreenArgs a) {
                     }
                     if (ntb < tb_end) stage(ntb, njc, slot ^ 1);
                 }
-                const float *sb = (const float *)((const char *)Xs + slot * (S::kXS + S::kQS));
+                const float *sb = (const float *)((const char *)Xs + slot * S::kStage);
                 const float *xp = sb + ti * (kSDK * kTile) + col;
                 const float *qp = sb + S::kXS / 4 + wave * RW;  // this wave's rows; broadcast reads
 #pragma unroll
@@ -665,7 +670,7 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 template <int METRIC, int RL, int OCC>
 __global__ __launch_bounds__(kSThreads, OCC) void k_screen_m(ScreenArgs a) {
     constexpr int QR = 64;
-    typedef SSmem<QR, RL> S;
+    typedef SSmem<QR, RL, true> S;
     constexpr int K2 = S::K2;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float *Xs = (float *)smem;  // [2] x {X: [4 tiles][16 dims][64], Q: [16 dims][64]}
@@ -675,6 +680,7 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen_m(ScreenArgs a) {
     int *m_pair = meta + 16, *m_bufc = meta + 16 + QR;
     float2 *tri_s = (float2 *)(meta + 16 + 3 * QR);         // [2][QR]
     double *dq_s = (double *)(meta + 16 + 3 * QR + 4 * QR); // [QR][2]
+    float2 *br_s = (float2 *)(dq_s + 2 * QR);               // [kBR] block radius ranges
     const bool TRI = METRIC == LIRA_METRIC_L2 && a.tstat != nullptr;
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -746,13 +752,16 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen_m(ScreenArgs a) {
         auto stage = [&](int tb, int jc, int slot) {
             const int ntv = min(kSBT, tb_end - tb);
             const float4 *src = Xg + (int64_t)(tile0 + tb) * tstride + jc * (kTile / 4) + tid;
-            const uint32_t base = xs_lds + (uint32_t)(slot * (S::kXS + S::kQS));
+            const uint32_t base = xs_lds + (uint32_t)(slot * S::kStage);
             const uint32_t dst = __builtin_amdgcn_readfirstlane(base + (uint32_t)(wave * 256) * 4u);
 #pragma unroll
             for (int i = 0; i < kSBT; ++i)
                 sglds16(src + min(i, ntv - 1) * tstride, dst + (uint32_t)(i * (kSDK * kTile) * 4));
             sglds16(qtg + (int64_t)jc * (QR / 4) + wave * 64 + lane,
                     __builtin_amdgcn_readfirstlane(base + (uint32_t)S::kXS + (uint32_t)wave * 1024u));
+            if (jc == 0 && wave == 0)  // the block's xadj rides along (tiles past its end: masked on read)
+                sglds16(a.xadj + (int64_t)(tile0 + tb + min(lane >> 4, ntv - 1)) * kTile + (lane & 15) * 4,
+                        __builtin_amdgcn_readfirstlane(base + (uint32_t)(S::kXS + S::kQS)));
         };
 
         // Triangle-inequality block skip (L2), as k_scan: ||q - x|| >= |
@@ -786,9 +795,11 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen_m(ScreenArgs a) {
         // dot-product test h, and (TRI) the row's skip interval into tri_s[par]
         // (two parities: a wave refreshing the next block's never races one
         // still testing with this block's).
+        // the query's published bound, read once per item (no global load on
+        // the per-block path: the chunk loop's vmcnt(0) would wait for it)
+        const uint32_t pub = a.qbound && my_q >= 0
+            ? __hip_atomic_load(a.qbound + my_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
         auto refresh = [&](int par) {
-            const uint32_t pub = a.qbound && my_q >= 0
-                ? __hip_atomic_load(a.qbound + my_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
             const u64 kk = my_list[k - 1];
             double T = kk == kEmptyKey ? __builtin_inf() : bound_P<METRIC>((double)key_score(kk), my_E, dd);
             if (pub != ~0u) T = fmin(T, (double)ord2f(pub));
@@ -811,7 +822,11 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen_m(ScreenArgs a) {
             __builtin_amdgcn_wave_barrier();
             return h;
         };
-        auto block_range = [&](int tb, float &lo, float &hi) {
+        // radius range of the block at tile tb: staged in LDS for the item's
+        // first kBR blocks (one round of loads per item), else from tstat
+        const int nblk = (tb_end - tb_begin + kSBT - 1) / kSBT;
+        const bool br_lds = TRI && nblk <= S::kBR;
+        auto block_range_g = [&](int tb, float &lo, float &hi) {
             const int ntv = min(kSBT, tb_end - tb);
             lo = __builtin_inff();
             hi = -__builtin_inff();
@@ -819,6 +834,23 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen_m(ScreenArgs a) {
                 const float2 st = a.tstat[tile0 + tb + i];
                 lo = fminf(lo, st.x);
                 hi = fmaxf(hi, st.y);
+            }
+        };
+        if (br_lds) {
+            for (int i = tid; i < nblk; i += kSThreads) {
+                float lo, hi;
+                block_range_g(tb_begin + i * kSBT, lo, hi);
+                br_s[i] = make_float2(lo, hi);
+            }
+            __syncthreads();
+        }
+        auto block_range = [&](int tb, float &lo, float &hi) {
+            if (br_lds) {
+                const float2 v = br_s[(tb - tb_begin) / kSBT];
+                lo = v.x;
+                hi = v.y;
+            } else {
+                block_range_g(tb, lo, hi);
             }
         };
         // first block at or after t that some row may need (workgroup-uniform:
@@ -850,10 +882,8 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen_m(ScreenArgs a) {
         for (int bi = 0, next_tb = tb_end; tb < tb_end; tb = next_tb, ++bi) {
             const int ntv = min(kSBT, tb_end - tb);
             const float h_l = refresh(bi & 1);
-            f4 xa[4];  // xadj of my 16 candidates: tile t, i = 0..3 (+inf: padding / past the block)
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-                xa[t] = t < ntv ? *(const f4 *)&a.xadj[(int64_t)(tile0 + tb + t) * kTile + 4 * cj] : (f4)(__builtin_inff());
+            f4 xa[4];  // xadj of my 16 candidates: tile t, i = 0..3 (+inf: padding / past the block);
+                       // read from the ring at chunk 0 (staged with it)
             // a wave whose 16 rows all skip the block computes nothing for it
             bool wdead = false;
             if (TRI) {
@@ -880,8 +910,14 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen_m(ScreenArgs a) {
                     }
                     if (ntb < tb_end) stage(ntb, njc, slot ^ 1);
                 }
-                if (!wdead) {
-                    const float *sb = (const float *)((const char *)Xs + slot * (S::kXS + S::kQS));
+                if (c == 0) {
+                    const float *xs = (const float *)((const char *)Xs + slot * S::kStage + S::kXS + S::kQS);
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        xa[t] = t < ntv ? *(const f4 *)(xs + t * kTile + 4 * cj) : (f4)(__builtin_inff());
+                }
+                if (!wdead && !(a.dbg & 1)) {
+                    const float *sb = (const float *)((const char *)Xs + slot * S::kStage);
                     const float *xb = sb + g * kTile + 4 * cj;                   // + t*1024 + 4s*64
                     const float *qa = sb + S::kXS / 4 + g * QR + wave * 16 + cj;  // + 4s*64
 #pragma unroll
@@ -903,7 +939,7 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen_m(ScreenArgs a) {
                 if (wave == 0) atomicAdd(a.stats + 2, 1ull);
                 if (!wdead) atomicAdd(a.stats + 0, 16ull * kSBT * kTile);  // (row, candidate) pairs screened
             }
-            if (wdead) continue;
+            if (wdead || (a.dbg & 2)) continue;
 
             float h_r[4];
 #pragma unroll
@@ -1231,7 +1267,8 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     pl.mfma = mfma_env == 2 ? pl.rl <= 4 : mfma_env && pl.rl <= 2;
     pl.qr = pl.mfma ? 64 : screen_qr(pl.rl);
     pl.K2 = 32 * pl.rl;
-    pl.smem = pl.mfma ? (pl.rl == 1 ? SSmem<64, 1>::total : pl.rl == 2 ? SSmem<64, 2>::total : SSmem<64, 4>::total)
+    pl.smem = pl.mfma ? (pl.rl == 1 ? SSmem<64, 1, true>::total : pl.rl == 2 ? SSmem<64, 2, true>::total
+                                                                  : SSmem<64, 4, true>::total)
                       : screen_smem(pl.qr, pl.rl);
     const int64_t npairs = nq * nprobe;
     pl.grid = cu_count_s(idx->device) * std::max(1, std::min(2, (160 * 1024) / pl.smem));
@@ -1298,7 +1335,7 @@ static hipError_t launch_screen(const ScreenArgs &a, const SPlan &pl, hipStream_
 
 template <int M, int RL>
 static hipError_t launch_screen_m(const ScreenArgs &a, const SPlan &pl, hipStream_t st) {
-    constexpr int OCC = (160 * 1024) / SSmem<64, RL>::total >= 2 ? 2 : 1;
+    constexpr int OCC = (160 * 1024) / SSmem<64, RL, true>::total >= 2 ? 2 : 1;
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute((const void *)k_screen_m<M, RL, OCC>,
@@ -1306,7 +1343,7 @@ static hipError_t launch_screen_m(const ScreenArgs &a, const SPlan &pl, hipStrea
         if (e != hipSuccess) return e;
         attr = true;
     }
-    constexpr int smem = SSmem<64, RL>::total;
+    constexpr int smem = SSmem<64, RL, true>::total;
     hipLaunchKernelGGL((k_screen_m<M, RL, OCC>), dim3(pl.grid), dim3(kSThreads), smem, st, a);
     return hipGetLastError();
 }
@@ -1423,6 +1460,11 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     const bool tri = tri_env && !(flags & LIRA_SCAN_NO_PRUNE);
     a.pivot = tri ? idx->pivot : nullptr;
     a.tstat = tri ? idx->tstat : nullptr;
+    static const int dbg_env = [] {
+        const char *e = getenv("LIRA_SCAN_DEBUG");
+        return e ? atoi(e) : 0;
+    }();
+    a.dbg = dbg_env;
     a.X = idx->X;
     a.xadj = idx->xadj;
     a.rmax = idx->rmax;

@@ -52,6 +52,9 @@ def main(d):
             # VALUBusy as rocprof defines it: 100*sum(ACTIVE_INST_VALU)/CU_NUM/GRBM_GUI_ACTIVE
             # (ACTIVE_INST_VALU in quad-cycles; GRBM summed over 8 XCDs)
             e["valu_busy_pct"] = 100 * p["SQ_ACTIVE_INST_VALU"] * 4 / 256 / (p["GRBM_GUI_ACTIVE"] / 8)
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in p and "GRBM_GUI_ACTIVE" in p and p["GRBM_GUI_ACTIVE"]:
+            # MFMA busy cycles (summed over SIMDs) per SIMD-cycle of the kernel
+            e["mfma_busy_pct"] = 100 * p["SQ_VALU_MFMA_BUSY_CYCLES"] / (256 * 4) / (p["GRBM_GUI_ACTIVE"] / 8)
         if "SQ_WAVE_CYCLES" in p and p["SQ_WAVE_CYCLES"]:
             w = p["SQ_WAVE_CYCLES"]
             e["wave_cycle_split"] = {
