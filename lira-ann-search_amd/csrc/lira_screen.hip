@@ -124,11 +124,13 @@ __device__ __forceinline__ float row_h(double lim, double qn, double qnorm, doub
 
 // ---- Q staging: transposed per-item query copy + norms ---------------------
 // Block b = one query block (virtual partition v, block qb of QR pairs).
+// QN.w = fl(||q - pivot_p||) (double sum, round to nearest: the true value is
+// within 1 ulp) for the triangle skip, when a pivot array is given.
 template <int QR>
 __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64_t dpad, int nprobe,
-                                                int n_virt, const int32_t *cnt, const int32_t *qoff,
-                                                const int32_t *qlist, const int32_t *qblk_off, float *QT,
-                                                float4 *QN) {
+                                                int n_virt, int n_lists, const int32_t *cnt, const int32_t *qoff,
+                                                const int32_t *qlist, const int32_t *qblk_off, const float *pivot,
+                                                float *QT, float4 *QN) {
     __shared__ int pairs[QR];
     __shared__ int s_v;
     const int b = blockIdx.x;
@@ -156,19 +158,27 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
     const int lane = threadIdx.x & 63;
     for (int r = threadIdx.x >> 6; r < QR; r += 4) {
         const int pr = pairs[r];
-        double s = 0.0;
+        double s = 0.0, t = 0.0;
         if (pr >= 0) {
             const float *qr = Q + (int64_t)(pr / nprobe) * d;
+            const float *pv = pivot ? pivot + (int64_t)(v >= n_lists ? v - n_lists : v) * d : nullptr;
             for (int64_t j = lane; j < d; j += 64) {
                 const double x = (double)qr[j];
                 s = __builtin_fma(x, x, s);
+                if (pv) {
+                    const double df = x - (double)pv[j];
+                    t = __builtin_fma(df, df, t);
+                }
             }
         }
 #pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+        for (int m = 32; m >= 1; m >>= 1) {
+            s += __shfl_xor(s, m, 64);
+            t += __shfl_xor(t, m, 64);
+        }
         if (lane == 0)
             QN[(int64_t)b * QR + r] = make_float4((float)s, __double2float_ru(__builtin_sqrt(s) * (1.0 + 0x1p-40)),
-                                                  __int_as_float(pr), 0.0f);
+                                                  __int_as_float(pr), (float)__builtin_sqrt(t));
     }
 }
 
@@ -770,27 +780,13 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen_m(ScreenArgs a) {
         // ||q_r - c_p|| cannot hold a pair with exact score <= T_r, rad_r =
         // sqrt((T_r + d 2^-140) / (1 - (d+4) 2^-24)).  ||q_r - c_p|| in double:
         // row = 16w + (lane & 15), 4 lanes per row.
-        if (TRI) {
-            const int rrow = wave * 16 + cj;
-            const int rp = m_pair[rrow];
-            double sq = 0.0;
-            if (rp >= 0) {
-                const float *qr = a.Q + (int64_t)(rp / a.nprobe) * a.d;
-                const float *pv = a.pivot + (int64_t)p * a.d;
-                for (int j = g; j < (int)a.d; j += 4) {
-                    const double df = (double)qr[j] - (double)pv[j];
-                    sq = __builtin_fma(df, df, sq);
-                }
-            }
-            sq += __shfl_xor(sq, 16, 64);
-            sq += __shfl_xor(sq, 32, 64);
-            if (g == 0) {
-                const double dq = __builtin_sqrt(sq), m = (double)(a.d + 8) * 0x1p-50;
-                dq_s[rrow * 2] = dq * (1.0 - m);
-                dq_s[rrow * 2 + 1] = dq * (1.0 + m);
-            }
-            __builtin_amdgcn_wave_barrier();
+        // ||q_r - c_p|| from k_qstage (QN.w, within 1 ulp), widened by 2^-22
+        if (TRI && g == 0) {
+            const double dq = (double)qrec.w;
+            dq_s[my_row * 2] = dq * (1.0 - 0x1p-22);
+            dq_s[my_row * 2 + 1] = dq * (1.0 + 0x1p-22);
         }
+        if (TRI) __builtin_amdgcn_wave_barrier();
         // Thresholds at a block's start (lanes 0..15: row 16w + lane): the
         // dot-product test h, and (TRI) the row's skip interval into tri_s[par]
         // (two parities: a wave refreshing the next block's never races one
@@ -950,14 +946,26 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen_m(ScreenArgs a) {
 #pragma unroll
             for (int reg = 0; reg < 4; ++reg) {
                 float h = h_r[reg];
-                int pm = 0;
+                float wv[16];  // fl(dot - xadj) of my 16 candidates
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
                     const f2 w0 = (f2){acc[t * 4 + 0][reg], acc[t * 4 + 1][reg]} - xa[t].xy;
                     const f2 w1 = (f2){acc[t * 4 + 2][reg], acc[t * 4 + 3][reg]} - xa[t].zw;
-                    pm |= ((w0.x >= h) | ((w0.y >= h) << 1) | ((w1.x >= h) << 2) | ((w1.y >= h) << 3)) << (4 * t);
+                    wv[4 * t + 0] = w0.x;
+                    wv[4 * t + 1] = w0.y;
+                    wv[4 * t + 2] = w1.x;
+                    wv[4 * t + 3] = w1.y;
                 }
-                if (!__any(pm)) continue;  // wave-uniform: none of the four rows has a candidate
+                // one compare per lane first (max3 tree; fmaxf drops NaN, which
+                // never passes the per-candidate test either)
+                const float m01 = fmaxf(fmaxf(wv[0], wv[1]), wv[2]), m02 = fmaxf(fmaxf(wv[3], wv[4]), wv[5]);
+                const float m03 = fmaxf(fmaxf(wv[6], wv[7]), wv[8]), m04 = fmaxf(fmaxf(wv[9], wv[10]), wv[11]);
+                const float m05 = fmaxf(fmaxf(wv[12], wv[13]), wv[14]);
+                const float mx = fmaxf(fmaxf(fmaxf(m01, m02), m03), fmaxf(fmaxf(m04, m05), wv[15]));
+                if (!__any(mx >= h)) continue;  // wave-uniform: none of the four rows has a candidate
+                int pm = 0;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) pm |= (wv[i] >= h) << i;
                 float sc[16];  // screened scores (+inf: padding)
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
@@ -1057,13 +1065,34 @@ __global__ __launch_bounds__(256) void k_seed(const float *Q, const int32_t *pro
     const int p = probe[q * nprobe];
     if (p < 0 || p >= n_lists) return;
     const int tile0 = tile_off[p], nt = min(kSeedTiles, tile_off[p + 1] - tile0);
+    if (nt <= 0) return;
     const float *qrow = Q + q * d;
+    // one candidate per tile per lane, dims outer so all of them are in flight;
+    // each accumulator is that candidate's own sequential sum (search.cpp order)
+    float acc[kSeedTiles];
+    const float *xp[kSeedTiles];
+#pragma unroll
+    for (int t = 0; t < kSeedTiles; ++t) {
+        acc[t] = 0.0f;
+        xp[t] = Xr + ((int64_t)(tile0 + min(t, nt - 1)) * kTile + lane) * d;
+    }
+    for (int64_t j = 0; j < d; ++j) {
+        const float qj = qrow[j];
+#pragma unroll
+        for (int t = 0; t < kSeedTiles; ++t) {
+            if (METRIC == LIRA_METRIC_L2) {
+                const float df = qj - xp[t][j];
+                acc[t] = acc[t] + df * df;
+            } else {
+                acc[t] = acc[t] + qj * xp[t][j];
+            }
+        }
+    }
     float m[4] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};  // 4 smallest
-    for (int t = 0; t < nt; ++t) {
-        const int pos = (tile0 + t) * kTile + lane;
-        if (ids[pos] < 0) continue;
-        float s = exact_score<METRIC>(qrow, Xr, d, pos);
-        if (!(s == s)) continue;
+#pragma unroll
+    for (int t = 0; t < kSeedTiles; ++t) {
+        float s = METRIC == LIRA_METRIC_L2 ? acc[t] : -acc[t];
+        if (t >= nt || ids[(tile0 + t) * kTile + lane] < 0 || !(s == s)) continue;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const float lo = fminf(m[i], s), hi = fmaxf(m[i], s);
@@ -1153,27 +1182,50 @@ __global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
             merge_batch_if<R>(lst, key);
         }
     };
-    // survivors of one list (pair slot s, chunk c) against the exact bound T
-    // survivors of one list (pair slot s, chunk c) against the exact bound T;
-    // a list whose K2-th key is still within lim may have dropped a needed
-    // candidate: the chunk is then re-scanned exactly instead
-    auto take_list = [&](const u64 *src, int p, int c, float T, double E) {
-        const double lim = s_lim<METRIC>((double)T, E, dd);
-        const u64 last = src[K2 - 1];
-        if (last != kEmptyKey && (double)key_score(last) <= lim) {
-            rescan(p, c, T);
-            return;
-        }
-        for (int e0 = 0; e0 < K2; e0 += 64) {
-            const u64 key = e0 + lane < K2 ? src[e0 + lane] : kEmptyKey;
-            const bool take = key != kEmptyKey && (double)key_score(key) <= lim;
-            add(take, (uint32_t)key);
-            if (!__any(take)) break;  // sorted: the rest is beyond lim
-        }
-    };
     auto list_bound = [&](const u64 *src, double E) {
         const u64 kk = src[k - 1];
         return kk == kEmptyKey ? __builtin_inff() : __double2float_ru(bound_P<METRIC>((double)key_score(kk), E, dd));
+    };
+
+    // Lists lane-parallel: lane i walks list i (pair slot s, chunk c) key by
+    // key while keys stay within lim -- one dependent load per round for all
+    // lists at once (sorted lists: the rest is beyond lim); a list whose K2-th
+    // key is within lim may have dropped a needed candidate and is re-scanned
+    // exactly instead.
+    auto take_lists = [&](int s_lo, int s_hi, float T) {
+        const int NC = a.nch_max, NL = (s_hi - s_lo) * NC;
+        for (int l0 = 0; l0 < NL; l0 += 64) {
+            const int li = l0 + lane, s = s_lo + li / NC, c = li % NC;
+            int p = -1;
+            if (li < NL) {
+                p = prow[s];
+                if (p < 0 || p >= a.n_lists || c >= a.nch[p]) p = -1;
+            }
+            const u64 *src = a.partial + ((q * a.nprobe + (p >= 0 ? s : 0)) * (int64_t)NC + (p >= 0 ? c : 0)) * K2;
+            double lim = 0.0;
+            bool over = false;
+            if (p >= 0) {
+                lim = s_lim<METRIC>((double)T, err_E<METRIC>(qnorm, (double)a.rmax[p], dd), dd);
+                const u64 last = src[K2 - 1];
+                over = last != kEmptyKey && (double)key_score(last) <= lim;
+            }
+            bool active = p >= 0 && !over;
+            for (int e = 0; __any(active); ++e) {
+                u64 key = kEmptyKey;
+                if (active) {
+                    key = e < K2 ? src[e] : kEmptyKey;
+                    active = key != kEmptyKey && (double)key_score(key) <= lim;
+                }
+                add(active, (uint32_t)key);
+            }
+            u64 ov = __ballot(over);
+            while (ov) {
+                const int ln = __builtin_ctzll(ov);
+                ov &= ov - 1;
+                const int li2 = l0 + ln;
+                rescan(prow[s_lo + li2 / NC], li2 % NC, T);
+            }
+        }
     };
 
     if (a.per_partition) {
@@ -1184,9 +1236,12 @@ __global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
                 ncand += a.list_size[p];
                 const double E = err_E<METRIC>(qnorm, (double)a.rmax[p], dd);
                 const u64 *base = a.partial + (q * a.nprobe + s) * (int64_t)a.nch_max * K2;
-                float T = __builtin_inff();
-                for (int c = 0; c < a.nch[p]; ++c) T = fminf(T, list_bound(base + (int64_t)c * K2, E));
-                for (int c = 0; c < a.nch[p]; ++c) take_list(base + (int64_t)c * K2, p, c, T, E);
+                float T = __builtin_inff();  // the pair's own bound: min over its chunk lists
+                for (int c0 = 0; c0 < a.nch[p]; c0 += 64)
+                    if (c0 + lane < a.nch[p]) T = fminf(T, list_bound(base + (int64_t)(c0 + lane) * K2, E));
+#pragma unroll
+                for (int m = 32; m >= 1; m >>= 1) T = fminf(T, __shfl_xor(T, m, 64));
+                take_lists(s, s + 1, T);
                 flush_pending();
             }
             const int64_t o = (q * a.nprobe + s) * (int64_t)k;
@@ -1194,8 +1249,7 @@ __global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
         }
     } else {
         reset();
-        float T = a.qbound ? ord2f(a.qbound[q]) : __builtin_inff();
-        if (a.qbound && a.qbound[q] == ~0u) T = __builtin_inff();
+        float T = a.qbound && a.qbound[q] != ~0u ? ord2f(a.qbound[q]) : __builtin_inff();
         if (!a.qbound) {
             for (int s = 0; s < a.nprobe; ++s) {
                 const int p = prow[s];
@@ -1207,12 +1261,9 @@ __global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
         }
         for (int s = 0; s < a.nprobe; ++s) {
             const int p = prow[s];
-            if (p < 0 || p >= a.n_lists) continue;
-            ncand += a.list_size[p];
-            const double E = err_E<METRIC>(qnorm, (double)a.rmax[p], dd);
-            const u64 *base = a.partial + (q * a.nprobe + s) * (int64_t)a.nch_max * K2;
-            for (int c = 0; c < a.nch[p]; ++c) take_list(base + (int64_t)c * K2, p, c, T, E);
+            if (p >= 0 && p < a.n_lists) ncand += a.list_size[p];
         }
+        take_lists(0, a.nprobe, T);
         flush_pending();
         emit_list<R>(lst, k, a.dedup, METRIC, a.D + q * k, a.I + q * k);
     }
@@ -1272,9 +1323,12 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
                       : screen_smem(pl.qr, pl.rl);
     const int64_t npairs = nq * nprobe;
     pl.grid = cu_count_s(idx->device) * std::max(1, std::min(2, (160 * 1024) / pl.smem));
+    // ~8 items per workgroup: fewer item prologues/epilogues and row lists to
+    // merge than k_scan's 16 (measured: SIFT1M scan + merge 1.47 -> 1.22 ms on
+    // the mixture, 4.80 -> 4.66 ms on latent data; 4 and 32 slower overall)
     static const int rounds = [] {
         const char *e = getenv("LIRA_SCAN_ROUNDS");
-        return e && atoi(e) > 0 ? atoi(e) : 16;
+        return e && atoi(e) > 0 ? atoi(e) : 8;
     }();
     const int64_t target = (int64_t)rounds * pl.grid;
     const int64_t est_items = (npairs + pl.qr - 1) / pl.qr + std::min<int64_t>(idx->n_lists, npairs);
@@ -1427,12 +1481,18 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     const int nvirt = groups * (int)idx->n_lists;
     LIRA_HIP_TRY(launch_plan(idx, probe, npairs, (int)nprobe, pl.bpc, pl.qr, groups, cnt, cursor, qoff, item_off,
                              nch, head, qlist, qblk, st));
+    static const int tri_env = [] {
+        const char *e = getenv("LIRA_SCAN_PRUNE");
+        return e && e[0] == '0' ? 0 : 1;
+    }();
+    const bool tri = tri_env && !(flags & LIRA_SCAN_NO_PRUNE) && pl.mfma && idx->pivot;
+    const float *tri_pivot = tri ? idx->pivot : nullptr;
     if (pl.qr == 64)
         hipLaunchKernelGGL(k_qstage<64>, dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
-                           (int)nprobe, nvirt, cnt, qoff, qlist, qblk, QT, QN);
+                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, QT, QN);
     else
         hipLaunchKernelGGL(k_qstage<32>, dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
-                           (int)nprobe, nvirt, cnt, qoff, qlist, qblk, QT, QN);
+                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, QT, QN);
     LIRA_HIP_TRY(hipGetLastError());
     static const int seed_env = [] {
         const char *e = getenv("LIRA_SCAN_SEED");
@@ -1453,11 +1513,6 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
 
     ScreenArgs a;
     a.Q = q;
-    static const int tri_env = [] {
-        const char *e = getenv("LIRA_SCAN_PRUNE");
-        return e && e[0] == '0' ? 0 : 1;
-    }();
-    const bool tri = tri_env && !(flags & LIRA_SCAN_NO_PRUNE);
     a.pivot = tri ? idx->pivot : nullptr;
     a.tstat = tri ? idx->tstat : nullptr;
     static const int dbg_env = [] {
