@@ -1496,7 +1496,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     LIRA_HIP_TRY(hipGetLastError());
     static const int seed_env = [] {
         const char *e = getenv("LIRA_SCAN_SEED");
-        return e && e[0] == '0' ? 0 : 1;
+        return e && e[0] == '1' ? 1 : 0;
     }();
     if (qbound && seed_env) {
         if (idx->metric == LIRA_METRIC_L2)
