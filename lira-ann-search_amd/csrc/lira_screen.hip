@@ -666,7 +666,8 @@ __device__ __forceinline__ float exact_score(const float *q, const float *Xr, in
 }
 
 // ---- the MFMA screening kernel (default) ------------------------------------
-// Same items, ring, thresholds and lists as k_screen (QR = 64), but the dot
+// Same items, ring, thresholds and lists as k_screen (QR = 64 or 128 queries
+// per item, QR/16 waves), but the dot
 // products run on v_mfma_f32_16x16x4_f32, which on gfx950 is bitwise an
 // fmaf chain in k order (cdna_hip_programming.md, FP32-input MFMA) -- the
 // screen's error model holds unchanged -- and reaches the f32 peak that the
@@ -677,9 +678,9 @@ __device__ __forceinline__ float exact_score(const float *q, const float *Xr, in
 // tile, rows 4g..4g+3 of column j: 16 candidates x 4 rows.
 typedef float f4v __attribute__((ext_vector_type(4)));
 
-template <int METRIC, int RL, int OCC>
-__global__ __launch_bounds__(kSThreads, OCC) void k_screen_m(ScreenArgs a) {
-    constexpr int QR = 64;
+template <int METRIC, int RL, int QR, int OCC>
+__global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
+    constexpr int NW = QR / 16, NT = QR * 4;  // waves of 16 rows each, threads
     typedef SSmem<QR, RL, true> S;
     constexpr int K2 = S::K2;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -736,7 +737,7 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen_m(ScreenArgs a) {
             m_pair[tid] = __float_as_int(a.QN[(int64_t)gqb * QR + tid].z);
             m_bufc[tid] = 0;
         }
-        for (int i = tid; i < QR * K2; i += kSThreads) lists[i] = kEmptyKey;
+        for (int i = tid; i < QR * K2; i += NT) lists[i] = kEmptyKey;
         __syncthreads();
 
         const int tile0 = __builtin_amdgcn_readfirstlane(a.tile_off[p]);
@@ -761,12 +762,16 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen_m(ScreenArgs a) {
         const float4 *qtg = (const float4 *)(a.QT + (int64_t)gqb * a.dpad * QR);
         auto stage = [&](int tb, int jc, int slot) {
             const int ntv = min(kSBT, tb_end - tb);
-            const float4 *src = Xg + (int64_t)(tile0 + tb) * tstride + jc * (kTile / 4) + tid;
             const uint32_t base = xs_lds + (uint32_t)(slot * S::kStage);
-            const uint32_t dst = __builtin_amdgcn_readfirstlane(base + (uint32_t)(wave * 256) * 4u);
+            // X: 16 pieces of 1 KiB per chunk (tile pc >> 2, dims jc + 4(pc & 3)
+            // .. +3); wave w moves pieces w, w + NW, ...
 #pragma unroll
-            for (int i = 0; i < kSBT; ++i)
-                sglds16(src + min(i, ntv - 1) * tstride, dst + (uint32_t)(i * (kSDK * kTile) * 4));
+            for (int m = 0; m < 16 / NW; ++m) {
+                const int pc = wave + NW * m, t = pc >> 2, qq = pc & 3;
+                sglds16(Xg + (int64_t)(tile0 + tb + min(t, ntv - 1)) * tstride + jc * (kTile / 4) + qq * 64 + lane,
+                        __builtin_amdgcn_readfirstlane(base + (uint32_t)(t * (kSDK * kTile * 4) + qq * 1024)));
+            }
+            // Q: QR/16 pieces of 1 KiB, one per wave
             sglds16(qtg + (int64_t)jc * (QR / 4) + wave * 64 + lane,
                     __builtin_amdgcn_readfirstlane(base + (uint32_t)S::kXS + (uint32_t)wave * 1024u));
             if (jc == 0 && wave == 0)  // the block's xadj rides along (tiles past its end: masked on read)
@@ -833,7 +838,7 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen_m(ScreenArgs a) {
             }
         };
         if (br_lds) {
-            for (int i = tid; i < nblk; i += kSThreads) {
+            for (int i = tid; i < nblk; i += NT) {
                 float lo, hi;
                 block_range_g(tb_begin + i * kSBT, lo, hi);
                 br_s[i] = make_float2(lo, hi);
@@ -850,14 +855,16 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen_m(ScreenArgs a) {
             }
         };
         // first block at or after t that some row may need (workgroup-uniform:
-        // every wave tests all 64 rows, one per lane, against the same LDS values)
+        // every wave tests all QR rows, QR/64 per lane, against the same LDS values)
         auto skip_from = [&](int t, int par) {
             if (TRI) {
                 const float2 ab = tri_s[par * QR + lane];
+                const float2 ab2 = QR > 64 ? tri_s[par * QR + (QR > 64 ? 64 : 0) + lane]
+                                           : make_float2(__builtin_inff(), -__builtin_inff());
                 while (t < tb_end) {
                     float lo, hi;
                     block_range(t, lo, hi);
-                    if (!__all(hi < ab.x || lo > ab.y)) break;
+                    if (!__all((hi < ab.x || lo > ab.y) && (hi < ab2.x || lo > ab2.y))) break;
                     if (a.stats && tid == 0) atomicAdd(a.stats + 4, 1ull);
                     t += kSBT;
                 }
@@ -880,9 +887,10 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen_m(ScreenArgs a) {
             const float h_l = refresh(bi & 1);
             f4 xa[4];  // xadj of my 16 candidates: tile t, i = 0..3 (+inf: padding / past the block);
                        // read from the ring at chunk 0 (staged with it)
-            // a wave whose 16 rows all skip the block computes nothing for it
-            bool wdead = false;
-            if (TRI) {
+            // a wave whose 16 rows all skip the block (or hold no query)
+            // computes nothing for it
+            bool wdead = !__any(lane < 16 && my_pair >= 0);
+            if (TRI && !wdead) {
                 float lo, hi;
                 block_range(tb, lo, hi);
                 const float2 ab = tri_s[(bi & 1) * QR + wave * 16 + cj];
@@ -1316,11 +1324,20 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // MFMA screen where its LDS (64-query lists) still fits 2 workgroups per
     // CU; larger k (RL 4: DEEP10M's k = 100) measured faster on the VALU one
     pl.mfma = mfma_env == 2 ? pl.rl <= 4 : mfma_env && pl.rl <= 2;
-    pl.qr = pl.mfma ? 64 : screen_qr(pl.rl);
+    // queries per item of the MFMA screen: 64 (4 waves); 128 (8 waves, k <= 56)
+    // halves the L2 -> LDS bytes per FMA but measured slower on every config
+    // (SIFT1M 1.10 -> 1.25 ms mixture, 4.45 -> 4.66 ms latent; GIST, BIGANN too)
+    static const int qr_env = [] {
+        const char *e = getenv("LIRA_SCAN_QR");
+        return e && atoi(e) == 128 ? 128 : 64;
+    }();
+    pl.qr = pl.mfma ? (pl.rl <= 2 ? qr_env : 64) : screen_qr(pl.rl);
     pl.K2 = 32 * pl.rl;
-    pl.smem = pl.mfma ? (pl.rl == 1 ? SSmem<64, 1, true>::total : pl.rl == 2 ? SSmem<64, 2, true>::total
-                                                                  : SSmem<64, 4, true>::total)
-                      : screen_smem(pl.qr, pl.rl);
+    pl.smem = !pl.mfma       ? screen_smem(pl.qr, pl.rl)
+              : pl.qr == 128 ? (pl.rl == 1 ? SSmem<128, 1, true>::total : SSmem<128, 2, true>::total)
+              : pl.rl == 1   ? SSmem<64, 1, true>::total
+              : pl.rl == 2   ? SSmem<64, 2, true>::total
+                             : SSmem<64, 4, true>::total;
     const int64_t npairs = nq * nprobe;
     pl.grid = cu_count_s(idx->device) * std::max(1, std::min(2, (160 * 1024) / pl.smem));
     // ~8 items per workgroup: fewer item prologues/epilogues and row lists to
@@ -1387,28 +1404,29 @@ static hipError_t launch_screen(const ScreenArgs &a, const SPlan &pl, hipStream_
     return hipGetLastError();
 }
 
-template <int M, int RL>
+template <int M, int RL, int QR>
 static hipError_t launch_screen_m(const ScreenArgs &a, const SPlan &pl, hipStream_t st) {
-    constexpr int OCC = (160 * 1024) / SSmem<64, RL, true>::total >= 2 ? 2 : 1;
+    constexpr int OCC = (160 * 1024) / SSmem<QR, RL, true>::total >= 2 ? 2 : 1;
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void *)k_screen_m<M, RL, OCC>,
+        hipError_t e = hipFuncSetAttribute((const void *)k_screen_m<M, RL, QR, OCC>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    constexpr int smem = SSmem<64, RL, true>::total;
-    hipLaunchKernelGGL((k_screen_m<M, RL, OCC>), dim3(pl.grid), dim3(kSThreads), smem, st, a);
+    constexpr int smem = SSmem<QR, RL, true>::total;
+    hipLaunchKernelGGL((k_screen_m<M, RL, QR, OCC>), dim3(pl.grid), dim3(QR * 4), smem, st, a);
     return hipGetLastError();
 }
 
 template <int M>
 static hipError_t launch_screen_rl(const ScreenArgs &a, const SPlan &pl, hipStream_t st) {
     if (pl.mfma) {
+        if (pl.qr == 128) return pl.rl == 1 ? launch_screen_m<M, 1, 128>(a, pl, st) : launch_screen_m<M, 2, 128>(a, pl, st);
         switch (pl.rl) {
-            case 1: return launch_screen_m<M, 1>(a, pl, st);
-            case 2: return launch_screen_m<M, 2>(a, pl, st);
-            default: return launch_screen_m<M, 4>(a, pl, st);
+            case 1: return launch_screen_m<M, 1, 64>(a, pl, st);
+            case 2: return launch_screen_m<M, 2, 64>(a, pl, st);
+            default: return launch_screen_m<M, 4, 64>(a, pl, st);
         }
     }
     switch (pl.rl) {
@@ -1487,7 +1505,10 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     }();
     const bool tri = tri_env && !(flags & LIRA_SCAN_NO_PRUNE) && pl.mfma && idx->pivot;
     const float *tri_pivot = tri ? idx->pivot : nullptr;
-    if (pl.qr == 64)
+    if (pl.qr == 128)
+        hipLaunchKernelGGL(k_qstage<128>, dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
+                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, QT, QN);
+    else if (pl.qr == 64)
         hipLaunchKernelGGL(k_qstage<64>, dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
                            (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, QT, QN);
     else

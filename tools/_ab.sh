@@ -7,9 +7,9 @@ one() {  # tag, env, args
     python3 -c "import json; j=json.loads(open('gpurun_out/ab_$1.log').read().strip().splitlines()[-1]); r=j['roofline']; e=r['exact_kernel']; print('$1', 'qps %.0f step %.3f scan_ms %.3f exact_ms %.3f same %s merge %.3f plan %.3f bitexact %s tflops %.1f surv %d' % (j['value'], j['ms_per_step'], j['kernels_ms_per_step']['scan'], e['scan_ms'], e['same_output_full_batch'], j['kernels_ms_per_step']['merge'], j['kernels_ms_per_step']['plan'], j['parity_bit_exact'], r['compute']['achieved'], r['work']['survivors']))"
 }
 one mix X=0 --config sift1m
-one mix_seed LIRA_SCAN_SEED=1 --config sift1m
+one mix_q64 LIRA_SCAN_QR=64 --config sift1m
 one lat X=0 --config sift1m --data latent
-one lat_seed LIRA_SCAN_SEED=1 --config sift1m --data latent
+one lat_q64 LIRA_SCAN_QR=64 --config sift1m --data latent
 one gist_lat X=0 --config gist1m --data latent
-
-one deep X=0 --config deep10m
+one gist_lat_q64 LIRA_SCAN_QR=64 --config gist1m --data latent
+one big X=0 --config bigann100m
