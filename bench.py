@@ -141,6 +141,8 @@ def main():
     index.set_stats(True)
     step()
     work = index.stats_read()
+    if os.environ.get("LIRA_SCAN_DEBUG"):
+        print("work_raw", work, file=sys.stderr)
     index.set_stats(False)
 
     # ---- the ranking GEMM alone (MFMA utilisation), outside the timed region ---

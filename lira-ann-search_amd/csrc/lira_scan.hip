@@ -111,7 +111,8 @@ __global__ __launch_bounds__(256) void k_count(const int32_t *probe, int64_t npa
 // qr = queries per work item; qblk_off (optional) = exclusive scan of the
 // query blocks ceil(cnt / qr) per virtual partition.
 __global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t *tile_off,
-                                               int n_lists, int n_virt, int bpc, int qr, int32_t *qoff,
+                                               int n_lists, int n_virt, int bpc, int bpc_near, int qr,
+                                               int32_t *qoff,
                                                int32_t *item_off, int32_t *nch, int32_t *head,
                                                int32_t *qblk_off) {
     __shared__ int32_t s_a[1024], s_b[1024], s_c[1024];
@@ -126,7 +127,8 @@ __global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t
             const int pp = p >= n_lists ? p - n_lists : p;
             int ntl = tile_off[pp + 1] - tile_off[pp];
             int nblk = (ntl + kBlockTiles - 1) / kBlockTiles;
-            int nc = (nblk + bpc - 1) / bpc;
+            const int b = n_virt > n_lists && p < n_lists ? bpc_near : bpc;  // group 0: bpc_near
+            int nc = (nblk + b - 1) / b;
             nch[p] = nc;
             nqb = (c + qr - 1) / qr;
             items = nqb * nc;
@@ -1033,7 +1035,7 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
     const size_t hf = nv <= kHistMax / 2 ? (size_t)nv * 8 : 0;
     hipLaunchKernelGGL(k_count, dim3(pg), dim3(256), hc, st, probe, npairs, nl, (int)nprobe, split, groups,
                        cnt, idx->err);
-    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, nv, pl.bpc, kQT, qoff,
+    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, nv, pl.bpc, pl.bpc, kQT, qoff,
                        item_off, nch, head, (int32_t *)nullptr);
     hipLaunchKernelGGL(k_fill, dim3(pg), dim3(256), hf, st, probe, npairs, nl, (int)nprobe, split, groups,
                        qoff, cursor, qlist);
@@ -1105,17 +1107,18 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
 
 // Plan kernels for another scan kernel (lira_screen.hip): `groups` groups of
 // virtual partitions (2: every query's first probe slot ahead of the rest),
-// `qr` queries per item, query-block offsets in qblk_off.
+// `qr` queries per item, query-block offsets in qblk_off; group 0's buckets
+// are cut into chunks of bpc_near blocks, the rest into chunks of bpc.
 // cnt, cursor and head must be zeroed by the caller.
 hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npairs, int nprobe, int bpc,
-                       int qr, int groups, int32_t *cnt, int32_t *cursor, int32_t *qoff, int32_t *item_off,
+                       int bpc_near, int qr, int groups, int32_t *cnt, int32_t *cursor, int32_t *qoff, int32_t *item_off,
                        int32_t *nch, int32_t *head, int32_t *qlist, int32_t *qblk_off, hipStream_t st) {
     const int nl = (int)idx->n_lists, nv = groups * nl;
     const unsigned pg = (unsigned)((npairs + kPairsPerBlock - 1) / kPairsPerBlock);
     const size_t hc = nv <= kHistMax ? (size_t)nv * 4 : 0;
     const size_t hf = nv <= kHistMax / 2 ? (size_t)nv * 8 : 0;
     hipLaunchKernelGGL(k_count, dim3(pg), dim3(256), hc, st, probe, npairs, nl, nprobe, 1, groups, cnt, idx->err);
-    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, nv, bpc, qr, qoff,
+    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, nv, bpc, bpc_near, qr, qoff,
                        item_off, nch, head, qblk_off);
     hipLaunchKernelGGL(k_fill, dim3(pg), dim3(256), hf, st, probe, npairs, nl, nprobe, 1, groups, qoff, cursor,
                        qlist);

@@ -50,6 +50,7 @@
 namespace lira {
 
 hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npairs, int nprobe, int bpc,
+                       int bpc_near,
                        int qr, int groups, int32_t *cnt, int32_t *cursor, int32_t *qoff, int32_t *item_off,
                        int32_t *nch, int32_t *head, int32_t *qlist, int32_t *qblk_off, hipStream_t st);
 
@@ -74,13 +75,17 @@ struct ScreenArgs {
     uint32_t *qbound;      // [nq] f2ord(bound on the final k-th exact score); NULL = off
     int64_t d, dpad;
     int n_lists, n_virt, nprobe, k, bpc, nch_max;  // n_virt = groups * n_lists (virtual partitions)
+    int bpc_near;  // blocks per chunk of group 0 (each query's nearest partition) when n_virt > n_lists
     unsigned long long *stats;  // NULL or lira_index_set_stats counters
     // L2 triangle-inequality block skip (k_screen_m): queries, per-list pivot,
     // per-tile radius bounds (lira_abi.hip k_list_pivot / k_tile_stats); NULL = off
     const float *Q;
     const float *pivot;
     const float2 *tstat;
-    int dbg;  // timing experiments only (env LIRA_SCAN_DEBUG; results invalid): 1 = no MFMA, 2 = no selection
+    int flush_at;  // a row's survivor buffer is merged into its list at this fill (<= 32)
+    int share;     // k_screen_m: publish/re-read the query bound every block (else once per item)
+    int dbg;  // timing experiments only (env LIRA_SCAN_DEBUG; results invalid): 1 = no MFMA, 2 = no selection,
+             // 4 = no X/Q staging, 8 = per-phase clocks into stats 1/3/6 (k_screen_m)
 };
 
 // ---- error model (double) -------------------------------------------------
@@ -133,6 +138,7 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
                                                 float *QT, float4 *QN) {
     __shared__ int pairs[QR];
     __shared__ int s_v;
+    __shared__ float tr[64][65];
     const int b = blockIdx.x;
     if (b >= qblk_off[n_virt]) return;
     if (threadIdx.x == 0) {
@@ -148,14 +154,24 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
     const int nval = min(QR, cnt[v] - qb * QR);
     if (threadIdx.x < QR) pairs[threadIdx.x] = (int)threadIdx.x < nval ? qlist[qoff[v] + qb * QR + threadIdx.x] : -1;
     __syncthreads();
-    for (int64_t i = threadIdx.x; i < (int64_t)QR * dpad; i += 256) {
-        const int r = (int)(i / dpad);
-        const int64_t j = i - (int64_t)r * dpad;
-        const int pr = pairs[r];
-        const float val = pr >= 0 && j < d ? Q[(int64_t)(pr / nprobe) * d + j] : 0.0f;
-        QT[((int64_t)b * dpad + j) * QR + r] = val;
+    // transpose through LDS, 64 rows x 64 dims at a time: reads along the
+    // query row, writes along QT's row axis, both coalesced
+    constexpr int RT = QR < 64 ? QR : 64;  // rows per transpose tile
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int r0 = 0; r0 < QR; r0 += RT) {
+        for (int64_t j0 = 0; j0 < dpad; j0 += 64) {
+            const int64_t j = j0 + lane;
+            for (int rr = wv; rr < RT; rr += 4) {
+                const int pr = pairs[r0 + rr];
+                tr[rr][lane] = pr >= 0 && j < d ? Q[(int64_t)(pr / nprobe) * d + j] : 0.0f;
+            }
+            __syncthreads();
+            if (lane < RT)
+                for (int jj = wv; jj < 64 && j0 + jj < dpad; jj += 4)
+                    QT[((int64_t)b * dpad + j0 + jj) * QR + r0 + lane] = tr[lane][jj];
+            __syncthreads();
+        }
     }
-    const int lane = threadIdx.x & 63;
     for (int r = threadIdx.x >> 6; r < QR; r += 4) {
         const int pr = pairs[r];
         double s = 0.0, t = 0.0;
@@ -324,53 +340,6 @@ __device__ __forceinline__ int s_append_n(u64 *L, u64 *buf, int bc, const u64 (&
     return bc;
 }
 
-// Four rows at once (MFMA layout): lane group g = lane>>4 appends its own
-// row (rowbase + 4g) from its 16 lanes' keys; a row whose buffer fills is
-// merged into its list (one row at a time, rare).
-template <int RL>
-__device__ __forceinline__ void s_append4(u64 *lists, u64 *bufs, int *m_bufc, int rowbase, const u64 (&key)[16],
-                                          int pm, unsigned long long *stats) {
-    constexpr int K2 = 32 * RL;
-    const int g = lane_id() >> 4;
-    const u64 gmask = 0xffffull << (16 * g);
-    const int row = rowbase + 4 * g;
-    u64 b[16];
-    int pos[16], tot = 0;
-#pragma unroll
-    for (int v = 0; v < 16; ++v) {
-        b[v] = __ballot((pm >> v) & 1) & gmask;
-        pos[v] = tot + mbcnt64(b[v]);
-        tot += popc64(b[v]);
-    }
-    if (stats && (lane_id() & 15) == 0 && tot) atomicAdd(stats + 7, (unsigned long long)tot);
-    int bc = m_bufc[row];
-    int consumed = 0;
-    for (;;) {
-        const int room = 32 - bc;
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-            const int rel = pos[v] - consumed;
-            if (((pm >> v) & 1) && rel >= 0 && rel < room) bufs[row * 32 + bc + rel] = key[v];
-        }
-        const int placed = min(room, tot - consumed);
-        bc += placed;
-        consumed += placed;
-        __builtin_amdgcn_wave_barrier();
-        // lanes 0, 16, 32, 48 vote for their group's row (bit 16g of a u64)
-        u64 full = __ballot(bc == 32 && (lane_id() & 15) == 0);
-        while (full) {
-            const int gg = __builtin_ctzll(full) >> 4;
-            full &= full - 1;
-            const int r = rowbase + 4 * gg;
-            s_flush<RL>(lists + r * K2, bufs + r * 32, 32);
-        }
-        if (bc == 32) bc = 0;
-        if (!__any(consumed < tot)) break;
-    }
-    if ((lane_id() & 15) == 0) m_bufc[row] = bc;
-    __builtin_amdgcn_wave_barrier();
-}
-
 template <int METRIC, int RL, int QR, int OCC>
 __global__ __launch_bounds__(kSThreads, OCC) void k_screen(ScreenArgs a) {
     typedef SSmem<QR, RL> S;
@@ -430,8 +399,9 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen(ScreenArgs a) {
 
         const int tile0 = __builtin_amdgcn_readfirstlane(a.tile_off[p]);
         const int ntl = __builtin_amdgcn_readfirstlane(a.tile_off[p + 1]) - tile0;
-        const int tb_begin = ch * a.bpc * kSBT;
-        const int tb_end = min(ntl, tb_begin + a.bpc * kSBT);
+        const int bpc = vp < a.n_lists && a.n_virt > a.n_lists ? a.bpc_near : a.bpc;
+        const int tb_begin = ch * bpc * kSBT;
+        const int tb_end = min(ntl, tb_begin + bpc * kSBT);
         const double R = (double)a.rmax[p];
 
         // this lane's row for threshold work: row = wave*RW + (lane % RW)
@@ -644,6 +614,7 @@ struct SMergeArgs {
     int64_t *ncand;
     int64_t nq, d, dpad;
     int n_lists, nprobe, k, K2, nch_max, bpc, dedup, per_partition;
+    int groups, bpc_near;  // groups == 2: slot 0 pairs are virtual partition p, chunked by bpc_near
     unsigned long long *stats;
 };
 
@@ -682,7 +653,7 @@ template <int METRIC, int RL, int QR, int OCC>
 __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
     constexpr int NW = QR / 16, NT = QR * 4;  // waves of 16 rows each, threads
     typedef SSmem<QR, RL, true> S;
-    constexpr int K2 = S::K2;
+    constexpr int K2 = S::K2, BC = 32;  // BC: survivor buffer keys per row
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float *Xs = (float *)smem;  // [2] x {X: [4 tiles][16 dims][64], Q: [16 dims][64]}
     u64 *lists = (u64 *)(smem + S::kX);
@@ -704,7 +675,9 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
     const int tstride = (int)a.dpad * (kTile / 4);
     const int nchunk = (int)(a.dpad / kSDK);
 
+    long long t_0 = 0, t_1 = 0, t_2 = 0;  // (a.dbg & 8) phase clocks, thread 0
     for (;;) {
+        if ((a.dbg & 8) && tid == 0) t_0 = clock64();
         if (tid == 0) {
             const int item = atomicAdd(&a.head[0], 1);
             const int ok = item < a.head[1];
@@ -742,8 +715,9 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
 
         const int tile0 = __builtin_amdgcn_readfirstlane(a.tile_off[p]);
         const int ntl = __builtin_amdgcn_readfirstlane(a.tile_off[p + 1]) - tile0;
-        const int tb_begin = ch * a.bpc * kSBT;
-        const int tb_end = min(ntl, tb_begin + a.bpc * kSBT);
+        const int bpc = vp < a.n_lists && a.n_virt > a.n_lists ? a.bpc_near : a.bpc;
+        const int tb_begin = ch * bpc * kSBT;
+        const int tb_end = min(ntl, tb_begin + bpc * kSBT);
         const double R = (double)a.rmax[p];
 
         // lanes 0..15 of wave w hold row 16w + lane's threshold state
@@ -761,6 +735,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
 
         const float4 *qtg = (const float4 *)(a.QT + (int64_t)gqb * a.dpad * QR);
         auto stage = [&](int tb, int jc, int slot) {
+            if (a.dbg & 4) return;  // timing experiment: no loads
             const int ntv = min(kSBT, tb_end - tb);
             const uint32_t base = xs_lds + (uint32_t)(slot * S::kStage);
             // X: 16 pieces of 1 KiB per chunk (tile pc >> 2, dims jc + 4(pc & 3)
@@ -798,12 +773,30 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
         // still testing with this block's).
         // the query's published bound, read once per item (no global load on
         // the per-block path: the chunk loop's vmcnt(0) would wait for it)
-        const uint32_t pub = a.qbound && my_q >= 0
+        uint32_t pub = a.qbound && my_q >= 0
             ? __hip_atomic_load(a.qbound + my_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
+        // with a.share: a row publishes its list's bound whenever it improves
+        // and re-reads the query's bound for the next block (the load
+        // completes under the next chunk's DMA wait), so concurrent items
+        // of one query -- the chunks of its nearest partition above all --
+        // prune with each other's progress
+        uint32_t own_pub = ~0u;
         auto refresh = [&](int par) {
             const u64 kk = my_list[k - 1];
             double T = kk == kEmptyKey ? __builtin_inf() : bound_P<METRIC>((double)key_score(kk), my_E, dd);
-            if (pub != ~0u) T = fmin(T, (double)ord2f(pub));
+            if (a.share && a.qbound && my_q >= 0) {
+                if (kk != kEmptyKey && lane < 16) {
+                    const uint32_t b = f2ord(__double2float_ru(T));
+                    if (b < own_pub) {
+                        atomicMin(a.qbound + my_q, b);
+                        own_pub = b;
+                    }
+                }
+                if (pub != ~0u) T = fmin(T, (double)ord2f(pub));
+                pub = __hip_atomic_load(a.qbound + my_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else if (pub != ~0u) {
+                T = fmin(T, (double)ord2f(pub));
+            }
             const float h = my_pair < 0 ? __builtin_inff()
                                         : row_h<METRIC>(s_lim<METRIC>(T, my_E, dd), my_qn, my_qnorm, R);
             if (TRI && lane < 16) {
@@ -881,6 +874,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
         }
         if (tb < tb_end) stage(tb, 0, 0);
 
+        if ((a.dbg & 8) && tid == 0) t_1 = clock64();
 #pragma unroll 1
         for (int bi = 0, next_tb = tb_end; tb < tb_end; tb = next_tb, ++bi) {
             const int ntv = min(kSBT, tb_end - tb);
@@ -971,28 +965,22 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                 const float m05 = fmaxf(fmaxf(wv[12], wv[13]), wv[14]);
                 const float mx = fmaxf(fmaxf(fmaxf(m01, m02), m03), fmaxf(fmaxf(m04, m05), wv[15]));
                 if (!__any(mx >= h)) continue;  // wave-uniform: none of the four rows has a candidate
-                int pm = 0;
+                int pm = 0;  // passing candidates (padding, xadj = +inf, never)
 #pragma unroll
-                for (int i = 0; i < 16; ++i) pm |= (wv[i] >= h) << i;
-                float sc[16];  // screened scores (+inf: padding)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const float av = xa[i >> 2][i & 3];
-                    const float dv = acc[i][reg];
-                    const bool real = av != __builtin_inff();
-                    if (METRIC == LIRA_METRIC_L2)
-                        sc[i] = real ? __builtin_fmaf(-2.0f, dv, qn_r[reg] + 2.0f * av) : __builtin_inff();
-                    else
-                        sc[i] = real ? -dv : __builtin_inff();
-                    if (!real) pm &= ~(1 << i);
-                }
+                for (int i = 0; i < 16; ++i) pm |= (wv[i] >= h && xa[i >> 2][i & 3] != __builtin_inff()) << i;
+                // screened score of candidate i (L2: qn + 2 xadj - 2 dot; IP: -dot)
+                auto score = [&](int i) {
+                    const float av = xa[i >> 2][i & 3], dv = acc[i][reg];
+                    return METRIC == LIRA_METRIC_L2 ? __builtin_fmaf(-2.0f, dv, qn_r[reg] + 2.0f * av) : -dv;
+                };
                 if (__any(h == -__builtin_inff()) && k <= 64) {
                     // a row without a bound yet: t = ceil(k/16) smallest of each
                     // of its 16 lanes, j = ceil(k/t) <= 16 over those lanes
                     float m4[4] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};
 #pragma unroll
                     for (int i = 0; i < 16; ++i) {
-                        float v = sc[i] == sc[i] ? sc[i] : __builtin_inff();
+                        const float sv = score(i);
+                        float v = xa[i >> 2][i & 3] != __builtin_inff() && sv == sv ? sv : __builtin_inff();
 #pragma unroll
                         for (int u = 0; u < 4; ++u) {
                             const float lo = fminf(m4[u], v), hi = fmaxf(m4[u], v);
@@ -1023,14 +1011,61 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                         pm &= pm2;
                     }
                 }
-                u64 key[16];
+                // append: lane group g adds its passing keys to row 4g + reg's
+                // buffer, lanes in order (offsets from a 16-lane prefix sum of
+                // the lanes' counts), each lane its own keys in column order --
+                // no per-column ballots.  A row whose buffer cannot take them is
+                // merged into its list first; more than BC keys (first blocks,
+                // loose bounds) go in rounds of BC, merging between rounds.  One
+                // merge site, so the reg loop still unrolls (acc[v][reg] static).
+                {
+                    const int row = wave * 16 + 4 * g + reg;
+                    const int bc0 = m_bufc[row];
+                    const int n_l = __builtin_popcount(pm);
+                    int inc = n_l;  // inclusive prefix over the group's 16 lanes
 #pragma unroll
-                for (int i = 0; i < 16; ++i)
-                    key[i] = ((u64)f2ord(sc[i]) << 32) | (uint32_t)((tile0 + tb + (i >> 2)) * kTile + 4 * cj + (i & 3));
-                s_append4<RL>(lists, bufs, m_bufc, wave * 16 + reg, key, pm, a.stats);
+                    for (int dl = 1; dl < 16; dl <<= 1) {
+                        const int o = __shfl_up(inc, dl, 16);
+                        if (cj >= dl) inc += o;
+                    }
+                    const int rowtot = __shfl(inc, 16 * g + 15, 64);
+                    const bool pre = bc0 > 0 && bc0 + rowtot > BC;  // merge the buffer first
+                    const int total = (pre ? 0 : bc0) + rowtot;    // the row's keys in buffer order
+                    const int base = (pre ? 0 : bc0) + inc - n_l;  // rank of my first key
+                    for (int r0 = 0;; r0 += BC) {
+                        // round 0: rows merging before appending; round r: rows
+                        // whose previous window filled
+                        u64 fl = __ballot((r0 == 0 ? pre : total > r0) && cj == 0);
+                        while (fl) {
+                            const int gg = __builtin_ctzll(fl) >> 4;
+                            fl &= fl - 1;
+                            const int r = wave * 16 + 4 * gg + reg;
+                            s_flush<RL>(lists + r * K2, bufs + r * BC, r0 == 0 ? __shfl(bc0, 16 * gg, 64) : BC);
+                        }
+                        int rank = base;
+#pragma unroll
+                        for (int v = 0; v < 16; ++v) {
+                            if ((pm >> v) & 1) {
+                                if (rank >= r0 && rank < r0 + BC)
+                                    bufs[row * BC + rank - r0] =
+                                        ((u64)f2ord(score(v)) << 32) |
+                                        (uint32_t)((tile0 + tb + (v >> 2)) * kTile + 4 * cj + (v & 3));
+                                ++rank;
+                            }
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                        if (!__any(total - r0 > BC)) break;
+                    }
+                    if (cj == 0) {
+                        m_bufc[row] = total <= BC ? total : total - BC * ((total - 1) / BC);
+                        if (a.stats && rowtot) atomicAdd(a.stats + 7, (unsigned long long)rowtot);
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
             }
         }
 
+        if ((a.dbg & 8) && tid == 0) t_2 = clock64();
         // ---- flush buffers, emit lists, publish bounds (wave-owned rows)
 #pragma unroll 1
         for (int r = 0; r < 16; ++r) {
@@ -1052,6 +1087,12 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
             }
         }
         __syncthreads();
+        if ((a.dbg & 8) && tid == 0 && a.stats) {  // timing experiment: cycles per phase
+            const long long t_3 = clock64();
+            atomicAdd(a.stats + 1, (unsigned long long)(t_1 - t_0));
+            atomicAdd(a.stats + 3, (unsigned long long)(t_2 - t_1));
+            atomicAdd(a.stats + 6, (unsigned long long)(t_3 - t_2));
+        }
     }
 }
 
@@ -1075,37 +1116,60 @@ __global__ __launch_bounds__(256) void k_seed(const float *Q, const int32_t *pro
     const int tile0 = tile_off[p], nt = min(kSeedTiles, tile_off[p + 1] - tile0);
     const float *qrow = Q + q * d;
     float m[4] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};  // 4 smallest
-    // two tiles at a time, dims outer (both tiles' loads in flight); each
-    // accumulator is its candidate's own sequential sum (search.cpp order)
-    for (int t0 = 0; t0 < nt; t0 += 2) {
-        const bool two = t0 + 1 < nt;
-        // tile layout: dim j of the tile's 64 candidates is one coalesced 256-B row
-        const float *x0 = X + (int64_t)(tile0 + t0) * dpad * kTile + lane;
-        const float *x1 = X + (int64_t)(tile0 + t0 + (two ? 1 : 0)) * dpad * kTile + lane;
-        float a0 = 0.0f, a1 = 0.0f;
-#pragma unroll 8
-        for (int64_t j = 0; j < d; ++j) {
-            const float qj = qrow[j];
-            if (METRIC == LIRA_METRIC_L2) {
-                const float d0 = qj - x0[j * kTile], d1 = qj - x1[j * kTile];
-                a0 = a0 + d0 * d0;
-                a1 = a1 + d1 * d1;
-            } else {
-                a0 = a0 + qj * x0[j * kTile];
-                a1 = a1 + qj * x1[j * kTile];
+    // all (up to 4) tiles at once, dims outer: 4 loads per dim in flight x 16
+    // dims unrolled; the query's dims come 64 at a time from one coalesced
+    // load (lane j) and are broadcast by readlane.  Each accumulator is its
+    // candidate's own sequential sum (search.cpp order).
+    const float *xt[kSeedTiles];
+#pragma unroll
+    for (int t = 0; t < kSeedTiles; ++t)  // tile layout: dim j of a tile's 64 candidates is one 256-B row
+        xt[t] = X + (int64_t)(tile0 + min(t, nt - 1)) * dpad * kTile + lane;
+    float acc[kSeedTiles];
+#pragma unroll
+    for (int t = 0; t < kSeedTiles; ++t) acc[t] = 0.0f;
+    for (int64_t j0 = 0; j0 < d; j0 += 64) {
+        const float qv = j0 + lane < d ? qrow[j0 + lane] : 0.0f;
+        const int nj = (int)min<int64_t>(64, d - j0);
+        if (nj == 64) {
+#pragma unroll 16
+            for (int jj = 0; jj < 64; ++jj) {
+                const float qj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qv), jj));
+#pragma unroll
+                for (int t = 0; t < kSeedTiles; ++t) {
+                    const float xv = xt[t][(j0 + jj) * kTile];
+                    if (METRIC == LIRA_METRIC_L2) {
+                        const float df = qj - xv;
+                        acc[t] = acc[t] + df * df;
+                    } else {
+                        acc[t] = acc[t] + qj * xv;
+                    }
+                }
+            }
+        } else {
+            for (int jj = 0; jj < nj; ++jj) {
+                const float qj = __shfl(qv, jj, 64);
+#pragma unroll
+                for (int t = 0; t < kSeedTiles; ++t) {
+                    const float xv = xt[t][(j0 + jj) * kTile];
+                    if (METRIC == LIRA_METRIC_L2) {
+                        const float df = qj - xv;
+                        acc[t] = acc[t] + df * df;
+                    } else {
+                        acc[t] = acc[t] + qj * xv;
+                    }
+                }
             }
         }
-        float sv[2] = {METRIC == LIRA_METRIC_L2 ? a0 : -a0, METRIC == LIRA_METRIC_L2 ? a1 : -a1};
+    }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            float s = sv[u];
-            if ((u == 1 && !two) || ids[(tile0 + t0 + u) * kTile + lane] < 0 || !(s == s)) continue;
+    for (int u = 0; u < kSeedTiles; ++u) {
+        float sc = METRIC == LIRA_METRIC_L2 ? acc[u] : -acc[u];
+        if (u >= nt || ids[(tile0 + u) * kTile + lane] < 0 || !(sc == sc)) continue;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float lo = fminf(m[i], s), hi = fmaxf(m[i], s);
-                m[i] = lo;
-                s = hi;
-            }
+        for (int i = 0; i < 4; ++i) {
+            const float lo = fminf(m[i], sc), hi = fmaxf(m[i], sc);
+            m[i] = lo;
+            sc = hi;
         }
     }
     const int t = (k + 63) / 64;
@@ -1174,11 +1238,12 @@ __global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
         __builtin_amdgcn_wave_barrier();
     };
     // the chunk's candidates, all exact (a list that may have dropped one)
-    auto rescan = [&](int p, int c, float T) {
+    auto rescan = [&](int s, int p, int c, float T) {
         ++n_rescans;
         flush_pending();
+        const int bpc = a.groups == 2 && s == 0 ? a.bpc_near : a.bpc;
         const int tile0 = a.tile_off[p], ntl = a.tile_off[p + 1] - tile0;
-        const int t0 = c * a.bpc * kSBT, t1 = min(ntl, t0 + a.bpc * kSBT);
+        const int t0 = c * bpc * kSBT, t1 = min(ntl, t0 + bpc * kSBT);
         for (int t = t0; t < t1; ++t) {
             const int pos = (tile0 + t) * kTile + lane;
             const int gid = a.ids[pos];
@@ -1190,6 +1255,8 @@ __global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
             merge_batch_if<R>(lst, key);
         }
     };
+    // chunk counts are per virtual partition (plan): slot 0 is group 0
+    auto vnch = [&](int s, int p) { return a.groups == 2 && s > 0 ? a.n_lists + p : p; };
     auto list_bound = [&](const u64 *src, double E) {
         const u64 kk = src[k - 1];
         return kk == kEmptyKey ? __builtin_inff() : __double2float_ru(bound_P<METRIC>((double)key_score(kk), E, dd));
@@ -1207,7 +1274,7 @@ __global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
             int p = -1;
             if (li < NL) {
                 p = prow[s];
-                if (p < 0 || p >= a.n_lists || c >= a.nch[p]) p = -1;
+                if (p < 0 || p >= a.n_lists || c >= a.nch[vnch(s, p)]) p = -1;
             }
             const u64 *src = a.partial + ((q * a.nprobe + (p >= 0 ? s : 0)) * (int64_t)NC + (p >= 0 ? c : 0)) * K2;
             double lim = 0.0;
@@ -1231,7 +1298,7 @@ __global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
                 const int ln = __builtin_ctzll(ov);
                 ov &= ov - 1;
                 const int li2 = l0 + ln;
-                rescan(prow[s_lo + li2 / NC], li2 % NC, T);
+                rescan(s_lo + li2 / NC, prow[s_lo + li2 / NC], li2 % NC, T);
             }
         }
     };
@@ -1245,8 +1312,9 @@ __global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
                 const double E = err_E<METRIC>(qnorm, (double)a.rmax[p], dd);
                 const u64 *base = a.partial + (q * a.nprobe + s) * (int64_t)a.nch_max * K2;
                 float T = __builtin_inff();  // the pair's own bound: min over its chunk lists
-                for (int c0 = 0; c0 < a.nch[p]; c0 += 64)
-                    if (c0 + lane < a.nch[p]) T = fminf(T, list_bound(base + (int64_t)(c0 + lane) * K2, E));
+                const int nc = a.nch[vnch(s, p)];
+                for (int c0 = 0; c0 < nc; c0 += 64)
+                    if (c0 + lane < nc) T = fminf(T, list_bound(base + (int64_t)(c0 + lane) * K2, E));
 #pragma unroll
                 for (int m = 32; m >= 1; m >>= 1) T = fminf(T, __shfl_xor(T, m, 64));
                 take_lists(s, s + 1, T);
@@ -1264,7 +1332,7 @@ __global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
                 if (p < 0 || p >= a.n_lists) continue;
                 const double E = err_E<METRIC>(qnorm, (double)a.rmax[p], dd);
                 const u64 *base = a.partial + (q * a.nprobe + s) * (int64_t)a.nch_max * K2;
-                for (int c = 0; c < a.nch[p]; ++c) T = fminf(T, list_bound(base + (int64_t)c * K2, E));
+                for (int c = 0; c < a.nch[vnch(s, p)]; ++c) T = fminf(T, list_bound(base + (int64_t)c * K2, E));
             }
         }
         for (int s = 0; s < a.nprobe; ++s) {
@@ -1305,10 +1373,9 @@ static int screen_smem(int qr, int rl) {
     return qr == 64 ? SSmem<64, 1>::total : rl == 2 ? SSmem<32, 2>::total : rl == 4 ? SSmem<32, 4>::total
                                                                           : SSmem<32, 8>::total;
 }
-static int screen_occ(int qr, int rl) { return std::max(1, std::min(2, (160 * 1024) / screen_smem(qr, rl))); }
 
 struct SPlan {
-    int rl = 1, qr = 64, K2 = 32, bpc = 1, nch_max = 1, grid = 1, smem = 0, mfma = 1;
+    int rl = 1, qr = 64, K2 = 32, bpc = 1, bpc_near = 1, nch_max = 1, grid = 1, smem = 0, mfma = 1;
     int64_t max_qblk = 0;
     size_t off_cnt, off_cursor, off_head, off_qoff, off_item, off_nch, off_qblk, off_qlist, off_qt, off_qn,
         off_partial, off_qbound, total;
@@ -1356,7 +1423,21 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
         const int64_t split = (target + est_items - 1) / std::max<int64_t>(1, est_items);
         pl.bpc = (int)std::max<int64_t>(1, (max_blocks + split - 1) / split);
     }
-    pl.nch_max = (int)((max_blocks + pl.bpc - 1) / pl.bpc);
+    // Group 0 (each query's nearest partition, where pruning leaves most of
+    // the work) is cut finer: its items are the heavy ones, and ~1.5 of them
+    // per workgroup left the slowest workgroup with two (env LIRA_SCAN_NEAR_ROUNDS;
+    // measured SIFT1M mixture scan 1.08 -> 1.04 ms at 2, slower at 4 and 8:
+    // more lists, more survivors)
+    static const int near_rounds = [] {
+        const char *e = getenv("LIRA_SCAN_NEAR_ROUNDS");
+        return e && atoi(e) > 0 ? atoi(e) : 2;
+    }();
+    {
+        const int64_t est0 = std::min<int64_t>(nq, (nq + pl.qr - 1) / pl.qr + idx->n_lists);
+        const int64_t split0 = std::max<int64_t>(1, ((int64_t)near_rounds * pl.grid + est0 - 1) / std::max<int64_t>(1, est0));
+        pl.bpc_near = (int)std::min<int64_t>(pl.bpc, std::max<int64_t>(1, (max_blocks + split0 - 1) / split0));
+    }
+    pl.nch_max = (int)((max_blocks + pl.bpc_near - 1) / pl.bpc_near);
     pl.max_qblk = npairs / pl.qr + std::min<int64_t>(2 * idx->n_lists, npairs) + 1;
     size_t o = 0;
     auto take = [&](size_t bytes) {
@@ -1488,16 +1569,22 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     if (qbound) LIRA_HIP_TRY(hipMemsetAsync(qbound, 0xff, (size_t)nq * 4, st));
     // Two groups (every query's first probe slot -- its nearest partition, where
     // most of its top-k lives -- queued ahead of the rest) when the bound is
-    // shared across a query's items and the first slots still fill blocks of
-    // QR queries per partition: later items then start from tight bounds.
+    // shared across a query's items: later items then start from tight bounds.
+    // Also when the first slots fill few query blocks per partition (BIGANN:
+    // ~10 queries per partition) but every partition still gets >= 4 blocks of
+    // pairs: the nearest-slot items then stream each bucket at most ~1/4 more
+    // often, and where pruning works the rest skip almost everything (measured:
+    // BIGANN-100M mixture scan 66 -> 16 ms; GIST1M's 1k queries, 2 blocks per
+    // partition, latent data: 3.2 -> 3.7 ms, so not there).
+    // LIRA_SCAN_TWO_PHASE: 0 off, 2 always, 1 (default) this rule.
     static const int groups_env = [] {
         const char *e = getenv("LIRA_SCAN_TWO_PHASE");
         return e ? atoi(e) : 1;
     }();
-    const int groups = qbound && groups_env && nprobe >= 2 &&
-                               (groups_env == 2 || nq >= (int64_t)pl.qr * idx->n_lists) ? 2 : 1;
+    const bool fill = nq >= (int64_t)pl.qr * idx->n_lists || nq * nprobe >= 4 * (int64_t)pl.qr * idx->n_lists;
+    const int groups = qbound && groups_env && nprobe >= 2 && (groups_env == 2 || fill) ? 2 : 1;
     const int nvirt = groups * (int)idx->n_lists;
-    LIRA_HIP_TRY(launch_plan(idx, probe, npairs, (int)nprobe, pl.bpc, pl.qr, groups, cnt, cursor, qoff, item_off,
+    LIRA_HIP_TRY(launch_plan(idx, probe, npairs, (int)nprobe, pl.bpc, groups == 2 ? pl.bpc_near : pl.bpc, pl.qr, groups, cnt, cursor, qoff, item_off,
                              nch, head, qlist, qblk, st));
     static const int tri_env = [] {
         const char *e = getenv("LIRA_SCAN_PRUNE");
@@ -1541,6 +1628,16 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
         return e ? atoi(e) : 0;
     }();
     a.dbg = dbg_env;
+    static const int flush_env = [] {
+        const char *e = getenv("LIRA_SCAN_FLUSH");
+        return e && atoi(e) >= 1 && atoi(e) <= 32 ? atoi(e) : 32;
+    }();
+    static const int share_env = [] {
+        const char *e = getenv("LIRA_SCAN_SHARE");
+        return e ? atoi(e) : 1;
+    }();
+    a.flush_at = flush_env;
+    a.share = share_env;
     a.X = idx->X;
     a.xadj = idx->xadj;
     a.rmax = idx->rmax;
@@ -1560,6 +1657,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     a.nprobe = (int)nprobe;
     a.k = (int)k;
     a.bpc = pl.bpc;
+    a.bpc_near = groups == 2 ? pl.bpc_near : pl.bpc;
     a.nch_max = pl.nch_max;
     a.stats = idx->stats_on ? (unsigned long long *)idx->stats : nullptr;
     hipError_t e = idx->metric == LIRA_METRIC_L2 ? launch_screen_rl<LIRA_METRIC_L2>(a, pl, st)
@@ -1590,6 +1688,8 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     m.K2 = pl.K2;
     m.nch_max = pl.nch_max;
     m.bpc = pl.bpc;
+    m.bpc_near = a.bpc_near;
+    m.groups = groups;
     m.dedup = dedup ? 1 : 0;
     m.per_partition = per_part ? 1 : 0;
     m.stats = a.stats;
