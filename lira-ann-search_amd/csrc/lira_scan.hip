@@ -114,7 +114,7 @@ __global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t
                                                int n_lists, int n_virt, int bpc, int bpc_near, int qr,
                                                int32_t *qoff,
                                                int32_t *item_off, int32_t *nch, int32_t *head,
-                                               int32_t *qblk_off) {
+                                               int32_t *qblk_off, int4 *itab) {
     __shared__ int32_t s_a[1024], s_b[1024], s_c[1024];
     __shared__ int32_t carry_a, carry_b, carry_c;
     if (threadIdx.x == 0) carry_a = carry_b = carry_c = 0;
@@ -151,6 +151,14 @@ __global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t
             qoff[p] = carry_a + s_a[threadIdx.x] - c;
             item_off[p] = carry_b + s_b[threadIdx.x] - items;
             if (qblk_off) qblk_off[p] = carry_c + s_c[threadIdx.x] - nqb;
+            // item table: item -> (v, query block, chunk, global query block),
+            // so a workgroup decodes its item with one load (no search)
+            if (itab && items) {
+                const int i0 = carry_b + s_b[threadIdx.x] - items, g0 = carry_c + s_c[threadIdx.x] - nqb;
+                const int nc = items / nqb;
+                for (int ch = 0; ch < nc; ++ch)
+                    for (int qb = 0; qb < nqb; ++qb) itab[i0 + ch * nqb + qb] = make_int4(p, qb, ch, g0 + qb);
+            }
         }
         __syncthreads();
         if (threadIdx.x == 1023) {
@@ -1036,7 +1044,7 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
     hipLaunchKernelGGL(k_count, dim3(pg), dim3(256), hc, st, probe, npairs, nl, (int)nprobe, split, groups,
                        cnt, idx->err);
     hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, nv, pl.bpc, pl.bpc, kQT, qoff,
-                       item_off, nch, head, (int32_t *)nullptr);
+                       item_off, nch, head, (int32_t *)nullptr, (int4 *)nullptr);
     hipLaunchKernelGGL(k_fill, dim3(pg), dim3(256), hf, st, probe, npairs, nl, (int)nprobe, split, groups,
                        qoff, cursor, qlist);
     LIRA_HIP_TRY(hipGetLastError());
@@ -1112,14 +1120,15 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
 // cnt, cursor and head must be zeroed by the caller.
 hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npairs, int nprobe, int bpc,
                        int bpc_near, int qr, int groups, int32_t *cnt, int32_t *cursor, int32_t *qoff, int32_t *item_off,
-                       int32_t *nch, int32_t *head, int32_t *qlist, int32_t *qblk_off, hipStream_t st) {
+                       int32_t *nch, int32_t *head, int32_t *qlist, int32_t *qblk_off, int4 *itab,
+                       hipStream_t st) {
     const int nl = (int)idx->n_lists, nv = groups * nl;
     const unsigned pg = (unsigned)((npairs + kPairsPerBlock - 1) / kPairsPerBlock);
     const size_t hc = nv <= kHistMax ? (size_t)nv * 4 : 0;
     const size_t hf = nv <= kHistMax / 2 ? (size_t)nv * 8 : 0;
     hipLaunchKernelGGL(k_count, dim3(pg), dim3(256), hc, st, probe, npairs, nl, nprobe, 1, groups, cnt, idx->err);
     hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, nv, bpc, bpc_near, qr, qoff,
-                       item_off, nch, head, qblk_off);
+                       item_off, nch, head, qblk_off, itab);
     hipLaunchKernelGGL(k_fill, dim3(pg), dim3(256), hf, st, probe, npairs, nl, nprobe, 1, groups, qoff, cursor,
                        qlist);
     return hipGetLastError();

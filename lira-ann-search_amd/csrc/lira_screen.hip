@@ -52,7 +52,8 @@ namespace lira {
 hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npairs, int nprobe, int bpc,
                        int bpc_near,
                        int qr, int groups, int32_t *cnt, int32_t *cursor, int32_t *qoff, int32_t *item_off,
-                       int32_t *nch, int32_t *head, int32_t *qlist, int32_t *qblk_off, hipStream_t st);
+                       int32_t *nch, int32_t *head, int32_t *qlist, int32_t *qblk_off, int4 *itab,
+                       hipStream_t st);
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -68,6 +69,7 @@ struct ScreenArgs {
     const float *xadj;     // [n_tiles*64]
     const float *rmax;     // [n_lists]
     const int32_t *tile_off, *cnt, *item_off, *qblk_off;
+    const int4 *itab;  // item -> (virtual partition, query block, chunk, global query block)
     int32_t *head;
     const float *QT;       // [qblk][dpad][QR]
     const float4 *QN;      // [qblk*QR]: qn, |q| (up), pair (int bits), 0
@@ -361,35 +363,30 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen(ScreenArgs a) {
     const int nchunk = (int)(a.dpad / kSDK);
     const int ti = lane >> 4, col = (lane & 15) * 4;   // this lane's 4 candidates of a block
 
+    int nxt = tid == 0 ? atomicAdd(&a.head[0], 1) : 0;  // thread 0: the claimed next item
     for (;;) {
         if (tid == 0) {
-            const int item = atomicAdd(&a.head[0], 1);
+            // the next item is claimed one item ahead (its atomic completes
+            // under this item's work); one table load decodes it
+            const int item = nxt;
             const int ok = item < a.head[1];
-            int v = 0, qb = 0, ch = 0;
+            int4 e = make_int4(0, 0, 0, 0);
             if (ok) {
-                int lo = 0, hi = a.n_virt - 1;
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (a.item_off[mid] <= item) lo = mid; else hi = mid - 1;
-                }
-                v = lo;
-                const int local = item - a.item_off[v];
-                const int nqb = (a.cnt[v] + QR - 1) / QR;
-                ch = local / nqb;
-                qb = local - ch * nqb;
+                e = a.itab[item];
+                nxt = atomicAdd(&a.head[0], 1);
             }
             meta[0] = ok;
-            meta[1] = v;
-            meta[2] = qb;
-            meta[3] = ch;
+            meta[1] = e.x;
+            meta[2] = e.y;
+            meta[3] = e.z;
+            meta[4] = e.w;
         }
         __syncthreads();
         if (!meta[0]) break;
         const int vp = __builtin_amdgcn_readfirstlane(meta[1]);  // virtual partition
         const int p = vp >= a.n_lists ? vp - a.n_lists : vp;
-        const int qb = __builtin_amdgcn_readfirstlane(meta[2]);
         const int ch = __builtin_amdgcn_readfirstlane(meta[3]);
-        const int gqb = __builtin_amdgcn_readfirstlane(a.qblk_off[vp]) + qb;
+        const int gqb = __builtin_amdgcn_readfirstlane(meta[4]);
         if (tid < QR) {
             m_pair[tid] = __float_as_int(a.QN[(int64_t)gqb * QR + tid].z);
             m_bufc[tid] = 0;
@@ -676,36 +673,31 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
     const int nchunk = (int)(a.dpad / kSDK);
 
     long long t_0 = 0, t_1 = 0, t_2 = 0;  // (a.dbg & 8) phase clocks, thread 0
+    int nxt = tid == 0 ? atomicAdd(&a.head[0], 1) : 0;  // thread 0: the claimed next item
     for (;;) {
         if ((a.dbg & 8) && tid == 0) t_0 = clock64();
         if (tid == 0) {
-            const int item = atomicAdd(&a.head[0], 1);
+            // the next item is claimed one item ahead (its atomic completes
+            // under this item's work); one table load decodes it
+            const int item = nxt;
             const int ok = item < a.head[1];
-            int v = 0, qb = 0, ch = 0;
+            int4 e = make_int4(0, 0, 0, 0);
             if (ok) {
-                int lo = 0, hi = a.n_virt - 1;
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (a.item_off[mid] <= item) lo = mid; else hi = mid - 1;
-                }
-                v = lo;
-                const int local = item - a.item_off[v];
-                const int nqb = (a.cnt[v] + QR - 1) / QR;
-                ch = local / nqb;
-                qb = local - ch * nqb;
+                e = a.itab[item];
+                nxt = atomicAdd(&a.head[0], 1);
             }
             meta[0] = ok;
-            meta[1] = v;
-            meta[2] = qb;
-            meta[3] = ch;
+            meta[1] = e.x;
+            meta[2] = e.y;
+            meta[3] = e.z;
+            meta[4] = e.w;
         }
         __syncthreads();
         if (!meta[0]) break;
         const int vp = __builtin_amdgcn_readfirstlane(meta[1]);  // virtual partition
         const int p = vp >= a.n_lists ? vp - a.n_lists : vp;
-        const int qb = __builtin_amdgcn_readfirstlane(meta[2]);
         const int ch = __builtin_amdgcn_readfirstlane(meta[3]);
-        const int gqb = __builtin_amdgcn_readfirstlane(a.qblk_off[vp]) + qb;
+        const int gqb = __builtin_amdgcn_readfirstlane(meta[4]);
         if (tid < QR) {
             m_pair[tid] = __float_as_int(a.QN[(int64_t)gqb * QR + tid].z);
             m_bufc[tid] = 0;
@@ -824,10 +816,13 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
             const int ntv = min(kSBT, tb_end - tb);
             lo = __builtin_inff();
             hi = -__builtin_inff();
-            for (int i = 0; i < ntv; ++i) {
-                const float2 st = a.tstat[tile0 + tb + i];
-                lo = fminf(lo, st.x);
-                hi = fmaxf(hi, st.y);
+#pragma unroll
+            for (int i = 0; i < kSBT; ++i) {  // (independent loads in flight together)
+                if (i < ntv) {
+                    const float2 st = a.tstat[tile0 + tb + i];
+                    lo = fminf(lo, st.x);
+                    hi = fmaxf(hi, st.y);
+                }
             }
         };
         if (br_lds) {
@@ -1377,7 +1372,7 @@ static int screen_smem(int qr, int rl) {
 struct SPlan {
     int rl = 1, qr = 64, K2 = 32, bpc = 1, bpc_near = 1, nch_max = 1, grid = 1, smem = 0, mfma = 1;
     int64_t max_qblk = 0;
-    size_t off_cnt, off_cursor, off_head, off_qoff, off_item, off_nch, off_qblk, off_qlist, off_qt, off_qn,
+    size_t off_cnt, off_cursor, off_head, off_qoff, off_item, off_nch, off_qblk, off_itab, off_qlist, off_qt, off_qn,
         off_partial, off_qbound, total;
 };
 
@@ -1453,6 +1448,7 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     pl.off_item = take((nl + 1) * 4);
     pl.off_nch = take(nl * 4);
     pl.off_qblk = take((nl + 1) * 4);
+    pl.off_itab = take((size_t)(pl.max_qblk + 1) * pl.nch_max * 16);  // items <= query blocks x chunks
     pl.off_qlist = take((size_t)npairs * 4);
     pl.off_qt = take((size_t)pl.max_qblk * pl.qr * idx->dpad * 4);
     pl.off_qn = take((size_t)pl.max_qblk * pl.qr * 16);
@@ -1557,6 +1553,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     int32_t *item_off = (int32_t *)(w + pl.off_item);
     int32_t *nch = (int32_t *)(w + pl.off_nch);
     int32_t *qblk = (int32_t *)(w + pl.off_qblk);
+    int4 *itab = (int4 *)(w + pl.off_itab);
     int32_t *qlist = (int32_t *)(w + pl.off_qlist);
     float *QT = (float *)(w + pl.off_qt);
     float4 *QN = (float4 *)(w + pl.off_qn);
@@ -1585,7 +1582,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     const int groups = qbound && groups_env && nprobe >= 2 && (groups_env == 2 || fill) ? 2 : 1;
     const int nvirt = groups * (int)idx->n_lists;
     LIRA_HIP_TRY(launch_plan(idx, probe, npairs, (int)nprobe, pl.bpc, groups == 2 ? pl.bpc_near : pl.bpc, pl.qr, groups, cnt, cursor, qoff, item_off,
-                             nch, head, qlist, qblk, st));
+                             nch, head, qlist, qblk, itab, st));
     static const int tri_env = [] {
         const char *e = getenv("LIRA_SCAN_PRUNE");
         return e && e[0] == '0' ? 0 : 1;
@@ -1645,6 +1642,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     a.cnt = cnt;
     a.item_off = item_off;
     a.qblk_off = qblk;
+    a.itab = itab;
     a.head = head;
     a.QT = QT;
     a.QN = QN;
