@@ -51,6 +51,9 @@ extern "C" {
                                       pairs already past the k-th score); same results, for A/B */
 #define LIRA_SCAN_EXACT 16u        /* use the all-exact scan (every candidate in search.cpp's arithmetic)
                                       instead of the default FMA screen + exact re-check; same results */
+#define LIRA_SCAN_NO_SPLIT 32u     /* screen with the fp32 MFMA (v_mfma_f32_16x16x4_f32) instead of the
+                                      split-bf16 one (v_mfma_f32_16x16x32_bf16, wider error bound); same
+                                      results, for A/B */
 
 /* lira_select_probes modes */
 #define LIRA_PROBE_NEAREST 0      /* nprobe smallest values, ties -> smaller bucket (IVF nprobe) */

@@ -145,6 +145,38 @@ __global__ __launch_bounds__(256) void k_rowmajor(const float *X, int64_t d, int
     }
 }
 
+// Xb: the split-bf16 copy of X for the MFMA screen (lira_screen.hip
+// k_screen_m<..., SPLIT>).  Per tile and 16-dim chunk c, 4 KiB = [g 4][p 64]
+// [8 bf16], g = 2 hl + h: the hi (hl = 0) or lo (hl = 1) round-to-nearest
+// bf16 part of dims 16c + 8h .. +7 of candidate row 4 (p & 15) + (p >> 4) (the
+// permutation makes a 16-lane group's B-fragment reads consecutive).  One
+// workgroup per (tile, chunk), one 16-B unit per thread.
+__device__ __forceinline__ uint32_t bf16_rne_b(float v) {
+    const uint32_t b = __float_as_uint(v);
+    return (b + 0x7fffu + ((b >> 16) & 1u)) >> 16;
+}
+__global__ __launch_bounds__(256) void k_split_tiles(const float *X, int64_t n_tiles, int64_t dpad, uint4 *Xb) {
+    const int64_t nch = dpad / 16, total = n_tiles * nch;
+    const int u = threadIdx.x, g = u >> 6, p = u & 63, r = 4 * (p & 15) + (p >> 4), h = g & 1, hl = g >> 1;
+    for (int64_t tc = blockIdx.x; tc < total; tc += gridDim.x) {
+        const int64_t t = tc / nch, c = tc % nch;
+        const float *src = X + (t * dpad + 16 * c + 8 * h) * kTile + r;
+        uint32_t w[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            uint32_t part[2];
+#pragma unroll
+            for (int f = 0; f < 2; ++f) {
+                const float v = src[(2 * e + f) * kTile];
+                const uint32_t hi = bf16_rne_b(v);
+                part[f] = hl ? bf16_rne_b(v - __uint_as_float(hi << 16)) : hi;
+            }
+            w[e] = part[0] | (part[1] << 16);
+        }
+        Xb[tc * 256 + u] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
 __global__ void k_check_ids(const int32_t *ids, int64_t n, int64_t n_rows, int32_t *bad) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x)
@@ -158,6 +190,8 @@ static void free_storage(lira_index *idx) {
     if (idx->list_size) hipFree(idx->list_size);
     if (idx->Xr) hipFree(idx->Xr);
     idx->Xr = nullptr;
+    if (idx->Xb) hipFree(idx->Xb);
+    idx->Xb = nullptr;
     if (idx->xadj) hipFree(idx->xadj);
     if (idx->rmax) hipFree(idx->rmax);
     idx->xadj = nullptr;
@@ -334,7 +368,8 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
         if (tiles > 0) {
             if (hipMalloc(&idx->xadj, (size_t)tiles * kTile * 4) != hipSuccess ||
                 hipMalloc(&idx->rmax, (size_t)n_lists * 4) != hipSuccess ||
-                hipMalloc(&idx->Xr, (size_t)tiles * kTile * idx->d * 4) != hipSuccess) {
+                hipMalloc(&idx->Xr, (size_t)tiles * kTile * idx->d * 4) != hipSuccess ||
+                hipMalloc(&idx->Xb, (size_t)tiles * kTile * idx->dpad * 4) != hipSuccess) {
                 rc = fail(LIRA_ENOMEM, "hipMalloc of the row-norm arrays failed");
                 break;
             }
@@ -345,6 +380,8 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
                                    idx->rmax);
                 hipLaunchKernelGGL(k_rowmajor, dim3((unsigned)tiles), dim3(256), 0, st, idx->X, idx->d, idx->dpad,
                                    idx->Xr);
+                hipLaunchKernelGGL(k_split_tiles, dim3((unsigned)std::min<int64_t>(tiles * (idx->dpad / 16), 1 << 20)),
+                                   dim3(256), 0, st, idx->X, tiles, idx->dpad, (uint4 *)idx->Xb);
                 e = hipGetLastError();
             }
             if (e == hipSuccess) e = hipStreamSynchronize(st);
@@ -412,7 +449,8 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes) {
     *bytes = idx->n_tiles * idx->dpad * kTile * 4 + idx->n_tiles * kTile * 4 + idx->n_lists * 8 +
              (idx->pivot ? idx->n_lists * idx->d * 4 + idx->n_tiles * 8 : 0) +
              (idx->xadj ? idx->n_tiles * kTile * 4 + idx->n_lists * 4 : 0) +
-             (idx->Xr ? idx->n_tiles * kTile * idx->d * 4 : 0);
+             (idx->Xr ? idx->n_tiles * kTile * idx->d * 4 : 0) +
+             (idx->Xb ? idx->n_tiles * kTile * idx->dpad * 4 : 0);
     return LIRA_OK;
 }
 
@@ -432,7 +470,7 @@ int lira_scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *p
     if (idx->n_lists == 0) return fail(LIRA_ESTATE, "index has no lists (add_partitions first)");
     if (nq < 0 || nprobe_max <= 0) return fail(LIRA_EINVAL, "need nq >= 0 and nprobe_max > 0");
     if (k <= 0 || k > 256) return fail(LIRA_EUNSUPPORTED, "k must be in [1, 256]");
-    if (flags & ~(LIRA_SCAN_DEDUP | LIRA_SCAN_PER_PARTITION | LIRA_SCAN_FMA | LIRA_SCAN_NO_PRUNE | LIRA_SCAN_EXACT)) return fail(LIRA_EINVAL, "unknown flags");
+    if (flags & ~(LIRA_SCAN_DEDUP | LIRA_SCAN_PER_PARTITION | LIRA_SCAN_FMA | LIRA_SCAN_NO_PRUNE | LIRA_SCAN_EXACT | LIRA_SCAN_NO_SPLIT)) return fail(LIRA_EINVAL, "unknown flags");
     if (nq > 0 && (!q || !probe || !out_D || !out_I)) return fail(LIRA_EINVAL, "NULL buffer");
     DeviceGuard g(idx->device);
     return scan_topk(idx, q, nq, probe, nprobe_max, k, flags, out_D, out_I, out_ncand, workspace,

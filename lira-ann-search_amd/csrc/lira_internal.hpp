@@ -55,6 +55,9 @@ struct lira_index_impl {
     // screened path's exact re-check reads one candidate's d values
     // contiguously (a tile column would cost one cache line per value).
     float *Xr = nullptr;
+    // Split-bf16 copy of the tiles for the MFMA screen (lira_abi.hip
+    // k_split_tiles; layout at k_screen_m<..., SPLIT>): same bytes as X.
+    uint16_t *Xb = nullptr;
     int32_t *err = nullptr;        // device error word
     void *ws = nullptr;            // cached scan workspace
     size_t ws_bytes = 0;

@@ -86,14 +86,33 @@ struct ScreenArgs {
     const float2 *tstat;
     int flush_at;  // a row's survivor buffer is merged into its list at this fill (<= 32)
     int share;     // k_screen_m: publish/re-read the query bound every block (else once per item)
+    int split;     // k_screen_m<..., SPLIT = 1>: X is the split-bf16 copy (Xb), QT in the split layout
     int dbg;  // timing experiments only (env LIRA_SCAN_DEBUG; results invalid): 1 = no MFMA, 2 = no selection,
              // 4 = no X/Q staging, 8 = per-phase clocks into stats 1/3/6 (k_screen_m)
 };
 
 // ---- error model (double) -------------------------------------------------
+// split != 0: the dot product came from the split-bf16 MFMA screen
+// (k_screen_m<..., SPLIT>): q = qh + ql + eq, x = xh + xl + ex with every part a
+// bf16 round-to-nearest (|eq| <= 2^-16 |q_i|, |ex| <= 2^-16 |x_i|), the four
+// exact products qh xh, qh xl, ql xh, ql xl summed in fp32 in an unspecified
+// order (4 dpad terms, <= 2^-22 relative per add: any rounding mode the
+// matrix core may use), so |dot~ - q.x| <= ed = (2.0001 2^-16 + 4 dpad 2^-22)
+// 1.02 |q| R + an absolute term for flushed subnormal parts (values below
+// 2^-100 lose at most 2^-100 (|q| + R) per product).  The rest of the L2
+// score's error (qn, xn, their sum, the final fma) stays <= 8.4 u (|q|+R)^2.
 template <int METRIC>
-__device__ __forceinline__ double err_E(double qnorm, double R, double d) {
+__device__ __forceinline__ double err_E(double qnorm, double R, double d, int split = 0, double dp = 0.0) {
     const double dl = d * 0x1p-140;
+    if (split) {
+        const double ed = (2.0001 * 0x1p-16 + 4.0 * dp * 0x1p-22) * 1.02 * qnorm * R +
+                          4.0 * dp * 0x1p-96 * (qnorm + R + 1.0);
+        if (METRIC == LIRA_METRIC_L2) {
+            const double s = qnorm + R;
+            return 2.0 * ed + 1.05 * 8.0 * kU * s * s + dl;
+        }
+        return 1.05 * ed + dl;
+    }
     if (METRIC == LIRA_METRIC_L2) {
         const double s = qnorm + R;
         return 1.05 * ((d + 8.0) * kU * s * s) + dl;
@@ -133,7 +152,22 @@ __device__ __forceinline__ float row_h(double lim, double qn, double qnorm, doub
 // Block b = one query block (virtual partition v, block qb of QR pairs).
 // QN.w = fl(||q - pivot_p||) (double sum, round to nearest: the true value is
 // within 1 ulp) for the triangle skip, when a pivot array is given.
-template <int QR>
+// round-to-nearest-even fp32 -> bf16 bits (finite inputs)
+__device__ __forceinline__ uint32_t bf16_rne(float v) {
+    const uint32_t b = __float_as_uint(v);
+    return (b + 0x7fffu + ((b >> 16) & 1u)) >> 16;
+}
+// the hi (hl = 0) or lo (hl = 1) bf16 part of v: v = hi + lo + e, |e| <= 2^-16 |v|
+// (v - hi is exact in fp32)
+__device__ __forceinline__ uint32_t bf16_part(float v, int hl) {
+    const uint32_t hi = bf16_rne(v);
+    return hl ? bf16_rne(v - __uint_as_float(hi << 16)) : hi;
+}
+
+// SPLIT: QT per query block and 16-dim chunk c is [g 4][QR rows][8 bf16]
+// (64 QR bytes, the fp32 chunk's size), g = 2 hl + h holding the hi/lo part
+// of dims 16c + 8h .. +7 of the row: the A fragments of k_screen_m<SPLIT>.
+template <int QR, bool SPLIT>
 __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64_t dpad, int nprobe,
                                                 int n_virt, int n_lists, const int32_t *cnt, const int32_t *qoff,
                                                 const int32_t *qlist, const int32_t *qblk_off, const float *pivot,
@@ -168,9 +202,25 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
                 tr[rr][lane] = pr >= 0 && j < d ? Q[(int64_t)(pr / nprobe) * d + j] : 0.0f;
             }
             __syncthreads();
-            if (lane < RT)
+            if (SPLIT) {
+                // units (chunk cc of the slab, g, row): 16 B each, rows fastest
+                for (int u = threadIdx.x; u < 16 * RT; u += 256) {
+                    const int row = u % RT, cg = u / RT, cc = cg >> 2, gg = cg & 3;
+                    const int64_t c0 = j0 + 16 * cc;
+                    if (c0 >= dpad) continue;
+                    uint32_t wd[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int j = 16 * cc + 8 * (gg & 1) + 2 * e;
+                        wd[e] = bf16_part(tr[row][j], gg >> 1) | (bf16_part(tr[row][j + 1], gg >> 1) << 16);
+                    }
+                    ((uint4 *)QT)[((int64_t)b * dpad + c0) * QR / 4 + (int64_t)gg * QR + r0 + row] =
+                        make_uint4(wd[0], wd[1], wd[2], wd[3]);
+                }
+            } else if (lane < RT) {
                 for (int jj = wv; jj < 64 && j0 + jj < dpad; jj += 4)
                     QT[((int64_t)b * dpad + j0 + jj) * QR + r0 + lane] = tr[lane][jj];
+            }
             __syncthreads();
         }
     }
@@ -612,6 +662,7 @@ struct SMergeArgs {
     int64_t nq, d, dpad;
     int n_lists, nprobe, k, K2, nch_max, bpc, dedup, per_partition;
     int groups, bpc_near;  // groups == 2: slot 0 pairs are virtual partition p, chunked by bpc_near
+    int split;             // the lists came from the split-bf16 screen (its error model)
     unsigned long long *stats;
 };
 
@@ -646,7 +697,18 @@ __device__ __forceinline__ float exact_score(const float *q, const float *Xr, in
 // tile, rows 4g..4g+3 of column j: 16 candidates x 4 rows.
 typedef float f4v __attribute__((ext_vector_type(4)));
 
-template <int METRIC, int RL, int QR, int OCC>
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// SPLIT: the split-bf16 form.  X is then Xb (lira_abi.hip k_split_tiles): per
+// tile and 16-dim chunk, [g 4][p 64][8 bf16] with g = 2 hl + h the hi/lo part
+// of dims 8h..8h+7 of candidate 4 (p & 15) + (p >> 4), and QT the split layout
+// of k_qstage<QR, true>.  One v_mfma_f32_16x16x32_bf16 per (tile, query part)
+// and 16 dims: lane group g supplies k-slots 8g..8g+7 = (x part hl, dims h),
+// the A operand the query's hi (then lo) part of the same dims, so the pair
+// sums qh.(xh + xl) + ql.(xh + xl): 2 MFMAs of 16 cycles where the fp32 form
+// needs 4 of 32, same LDS bytes, B fragments read once for both.  The error
+// model is err_E(split = 1).
+template <int METRIC, int RL, int QR, int OCC, bool SPLIT = false>
 __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
     constexpr int NW = QR / 16, NT = QR * 4;  // waves of 16 rows each, threads
     typedef SSmem<QR, RL, true> S;
@@ -718,7 +780,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
         const int my_pair = __float_as_int(qrec.z);
         const int my_q = my_pair >= 0 ? my_pair / a.nprobe : -1;
         const double my_qn = (double)qrec.x, my_qnorm = (double)qrec.y;
-        const double my_E = err_E<METRIC>(my_qnorm, R, dd);
+        const double my_E = err_E<METRIC>(my_qnorm, R, dd, SPLIT, (double)a.dpad);
         u64 *my_list = lists + my_row * K2;
         // this lane's 4 output rows 4g + reg: qn for the screened scores
         float qn_r[4];
@@ -909,7 +971,24 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                     for (int t = 0; t < 4; ++t)
                         xa[t] = t < ntv ? *(const f4 *)(xs + t * kTile + 4 * cj) : (f4)(__builtin_inff());
                 }
-                if (!wdead && !(a.dbg & 1)) {
+                if (SPLIT && !wdead && !(a.dbg & 1)) {
+                    const char *sb = (const char *)Xs + slot * S::kStage;
+                    const bf16x8 a_hi = *(const bf16x8 *)(sb + S::kXS + (((g & 1) * QR + wave * 16 + cj) << 4));
+                    const bf16x8 a_lo = *(const bf16x8 *)(sb + S::kXS + (((2 + (g & 1)) * QR + wave * 16 + cj) << 4));
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        bf16x8 bv[4];
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            bv[i] = *(const bf16x8 *)(sb + t * (kSDK * kTile * 4) + ((g * 64 + i * 16 + cj) << 4));
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            acc[t * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_hi, bv[i], acc[t * 4 + i], 0, 0, 0);
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            acc[t * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_lo, bv[i], acc[t * 4 + i], 0, 0, 0);
+                    }
+                } else if (!SPLIT && !wdead && !(a.dbg & 1)) {
                     const float *sb = (const float *)((const char *)Xs + slot * S::kStage);
                     const float *xb = sb + g * kTile + 4 * cj;                   // + t*1024 + 4s*64
                     const float *qa = sb + S::kXS / 4 + g * QR + wave * 16 + cj;  // + 4s*64
@@ -997,7 +1076,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                     const float B = ord2f((uint32_t)__shfl((int)key16, 16 * g + j - 1, 64));
                     if (h == -__builtin_inff() && B < __builtin_inff()) {
                         const double qnorm_r = (double)__shfl((float)my_qnorm, 4 * g + reg, 64);
-                        const double E_r = err_E<METRIC>(qnorm_r, R, dd);
+                        const double E_r = err_E<METRIC>(qnorm_r, R, dd, SPLIT, (double)a.dpad);
                         h = row_h<METRIC>(s_lim<METRIC>(bound_P<METRIC>((double)B, E_r, dd), E_r, dd),
                                           (double)qn_r[reg], qnorm_r, R);
                         int pm2 = 0;
@@ -1275,7 +1354,7 @@ __global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
             double lim = 0.0;
             bool over = false;
             if (p >= 0) {
-                lim = s_lim<METRIC>((double)T, err_E<METRIC>(qnorm, (double)a.rmax[p], dd), dd);
+                lim = s_lim<METRIC>((double)T, err_E<METRIC>(qnorm, (double)a.rmax[p], dd, a.split, (double)a.dpad), dd);
                 const u64 last = src[K2 - 1];
                 over = last != kEmptyKey && (double)key_score(last) <= lim;
             }
@@ -1304,7 +1383,7 @@ __global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
             reset();
             if (p >= 0 && p < a.n_lists) {
                 ncand += a.list_size[p];
-                const double E = err_E<METRIC>(qnorm, (double)a.rmax[p], dd);
+                const double E = err_E<METRIC>(qnorm, (double)a.rmax[p], dd, a.split, (double)a.dpad);
                 const u64 *base = a.partial + (q * a.nprobe + s) * (int64_t)a.nch_max * K2;
                 float T = __builtin_inff();  // the pair's own bound: min over its chunk lists
                 const int nc = a.nch[vnch(s, p)];
@@ -1325,7 +1404,7 @@ __global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
             for (int s = 0; s < a.nprobe; ++s) {
                 const int p = prow[s];
                 if (p < 0 || p >= a.n_lists) continue;
-                const double E = err_E<METRIC>(qnorm, (double)a.rmax[p], dd);
+                const double E = err_E<METRIC>(qnorm, (double)a.rmax[p], dd, a.split, (double)a.dpad);
                 const u64 *base = a.partial + (q * a.nprobe + s) * (int64_t)a.nch_max * K2;
                 for (int c = 0; c < a.nch[vnch(s, p)]; ++c) T = fminf(T, list_bound(base + (int64_t)c * K2, E));
             }
@@ -1370,7 +1449,7 @@ static int screen_smem(int qr, int rl) {
 }
 
 struct SPlan {
-    int rl = 1, qr = 64, K2 = 32, bpc = 1, bpc_near = 1, nch_max = 1, grid = 1, smem = 0, mfma = 1;
+    int rl = 1, qr = 64, K2 = 32, bpc = 1, bpc_near = 1, nch_max = 1, grid = 1, smem = 0, mfma = 1, split = 0;
     int64_t max_qblk = 0;
     size_t off_cnt, off_cursor, off_head, off_qoff, off_item, off_nch, off_qblk, off_itab, off_qlist, off_qt, off_qn,
         off_partial, off_qbound, total;
@@ -1394,6 +1473,13 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
         return e && atoi(e) == 128 ? 128 : 64;
     }();
     pl.qr = pl.mfma ? (pl.rl <= 2 ? qr_env : 64) : screen_qr(pl.rl);
+    // split-bf16 MFMA screen (k_screen_m<..., SPLIT>) where the index holds Xb;
+    // LIRA_SCAN_SPLIT=0 keeps the fp32 MFMA screen
+    static const int split_env = [] {
+        const char *e = getenv("LIRA_SCAN_SPLIT");
+        return e && e[0] == '0' ? 0 : 1;
+    }();
+    pl.split = split_env && pl.mfma && pl.qr == 64 && idx->Xb != nullptr;
     pl.K2 = 32 * pl.rl;
     pl.smem = !pl.mfma       ? screen_smem(pl.qr, pl.rl)
               : pl.qr == 128 ? (pl.rl == 1 ? SSmem<128, 1, true>::total : SSmem<128, 2, true>::total)
@@ -1481,18 +1567,18 @@ static hipError_t launch_screen(const ScreenArgs &a, const SPlan &pl, hipStream_
     return hipGetLastError();
 }
 
-template <int M, int RL, int QR>
+template <int M, int RL, int QR, bool SPLIT = false>
 static hipError_t launch_screen_m(const ScreenArgs &a, const SPlan &pl, hipStream_t st) {
     constexpr int OCC = (160 * 1024) / SSmem<QR, RL, true>::total >= 2 ? 2 : 1;
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void *)k_screen_m<M, RL, QR, OCC>,
+        hipError_t e = hipFuncSetAttribute((const void *)k_screen_m<M, RL, QR, OCC, SPLIT>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr = true;
     }
     constexpr int smem = SSmem<QR, RL, true>::total;
-    hipLaunchKernelGGL((k_screen_m<M, RL, QR, OCC>), dim3(pl.grid), dim3(QR * 4), smem, st, a);
+    hipLaunchKernelGGL((k_screen_m<M, RL, QR, OCC, SPLIT>), dim3(pl.grid), dim3(QR * 4), smem, st, a);
     return hipGetLastError();
 }
 
@@ -1500,6 +1586,11 @@ template <int M>
 static hipError_t launch_screen_rl(const ScreenArgs &a, const SPlan &pl, hipStream_t st) {
     if (pl.mfma) {
         if (pl.qr == 128) return pl.rl == 1 ? launch_screen_m<M, 1, 128>(a, pl, st) : launch_screen_m<M, 2, 128>(a, pl, st);
+        if (pl.split) switch (pl.rl) {
+            case 1: return launch_screen_m<M, 1, 64, true>(a, pl, st);
+            case 2: return launch_screen_m<M, 2, 64, true>(a, pl, st);
+            default: return launch_screen_m<M, 4, 64, true>(a, pl, st);
+        }
         switch (pl.rl) {
             case 1: return launch_screen_m<M, 1, 64>(a, pl, st);
             case 2: return launch_screen_m<M, 2, 64>(a, pl, st);
@@ -1532,7 +1623,8 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
                 size_t ws_bytes, hipStream_t st, hipEvent_t *ev) {
     const bool dedup = (flags & LIRA_SCAN_DEDUP) != 0;
     const bool per_part = (flags & LIRA_SCAN_PER_PARTITION) != 0;
-    const SPlan pl = make_splan(idx, nq, nprobe, k);
+    SPlan pl = make_splan(idx, nq, nprobe, k);
+    if (flags & LIRA_SCAN_NO_SPLIT) pl.split = 0;
     if (!ws) {
         if (idx->ws_bytes < pl.total) {
             if (idx->ws) hipFree(idx->ws);
@@ -1590,13 +1682,16 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     const bool tri = tri_env && !(flags & LIRA_SCAN_NO_PRUNE) && pl.mfma && idx->pivot;
     const float *tri_pivot = tri ? idx->pivot : nullptr;
     if (pl.qr == 128)
-        hipLaunchKernelGGL(k_qstage<128>, dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
+        hipLaunchKernelGGL((k_qstage<128, false>), dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
+                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, QT, QN);
+    else if (pl.qr == 64 && pl.split)
+        hipLaunchKernelGGL((k_qstage<64, true>), dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
                            (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, QT, QN);
     else if (pl.qr == 64)
-        hipLaunchKernelGGL(k_qstage<64>, dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
+        hipLaunchKernelGGL((k_qstage<64, false>), dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
                            (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, QT, QN);
     else
-        hipLaunchKernelGGL(k_qstage<32>, dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
+        hipLaunchKernelGGL((k_qstage<32, false>), dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
                            (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, QT, QN);
     LIRA_HIP_TRY(hipGetLastError());
     static const int seed_env = [] {
@@ -1635,7 +1730,8 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     }();
     a.flush_at = flush_env;
     a.share = share_env;
-    a.X = idx->X;
+    a.split = pl.split;
+    a.X = pl.split ? (const float *)idx->Xb : idx->X;
     a.xadj = idx->xadj;
     a.rmax = idx->rmax;
     a.tile_off = idx->tile_off;
@@ -1691,6 +1787,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     m.dedup = dedup ? 1 : 0;
     m.per_partition = per_part ? 1 : 0;
     m.stats = a.stats;
+    m.split = pl.split;
     if (idx->metric == LIRA_METRIC_L2)
         launch_smerge<LIRA_METRIC_L2>(Rm, m, st);
     else

@@ -22,6 +22,7 @@ LIRA_SCAN_PER_PARTITION = 2
 LIRA_SCAN_FMA = 4
 LIRA_SCAN_NO_PRUNE = 8
 LIRA_SCAN_EXACT = 16
+LIRA_SCAN_NO_SPLIT = 32
 LIRA_PROBE_NEAREST = 0
 LIRA_PROBE_THRESHOLD_GE = 1
 LIRA_PROBE_THRESHOLD_GT = 2

@@ -177,7 +177,7 @@ class PartitionedIndex:
     # --------------------------------------------------------------- search
     def search(self, q: torch.Tensor, probe: torch.Tensor, k: int, dedup: bool = True,
                per_partition: bool = False, out=None, stream=None, fma: bool = False,
-               prune: bool = True, exact: bool = False):
+               prune: bool = True, exact: bool = False, split: bool = True):
         """Scan the probed lists of every query; exact top-k.
 
         q (nq, d) fp32, probe (nq, nprobe_max) int32 (-1 = unused slot).
@@ -191,7 +191,10 @@ class PartitionedIndex:
         under a rigorous error bound and only possible top-k members are
         re-computed in search.cpp's arithmetic (same results); exact=True runs
         the all-exact scan instead (LIRA_SCAN_EXACT), prune=False additionally
-        turns off its L2 early abandon (same results; for A/B).
+        turns off its L2 early abandon (same results; for A/B).  The screen's
+        dot products run as split-bf16 MFMAs (hi/lo bf16 parts, fp32
+        accumulation); split=False uses the fp32 MFMA screen instead
+        (LIRA_SCAN_NO_SPLIT; same results).
         """
         q = _dev(q, torch.float32, self.device)
         probe = _dev(probe, torch.int32, self.device)
@@ -214,7 +217,8 @@ class PartitionedIndex:
             (_lib.LIRA_SCAN_PER_PARTITION if per_partition else 0) | \
             (_lib.LIRA_SCAN_FMA if fma else 0) | \
             (0 if prune else _lib.LIRA_SCAN_NO_PRUNE) | \
-            (_lib.LIRA_SCAN_EXACT if exact else 0)
+            (_lib.LIRA_SCAN_EXACT if exact else 0) | \
+            (0 if split else _lib.LIRA_SCAN_NO_SPLIT)
         with torch.cuda.device(self.device):
             _lib.call("lira_scan_topk", self._h, _lib.ptr(q), nq, _lib.ptr(probe), npm, int(k),
                       flags, _lib.ptr(D), _lib.ptr(I), _lib.ptr(ncand), None, 0,

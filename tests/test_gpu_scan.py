@@ -66,18 +66,18 @@ def random_case(seed, n, d, b, nq, nprobe, metric, red=0.0, uniform=False):
 
 
 def check_vs_oracle(x, q, d2b, probe, b, k, metric, dedup=True):
-    # both scan paths: the default FMA screen + exact re-check, and the
-    # all-exact kernel (exact=True)
+    # every scan path: the default split-bf16 MFMA screen + exact re-check,
+    # the fp32 MFMA screen (split=False), and the all-exact kernel (exact=True)
     idx = make_index(x, d2b, b, metric)
     off, ids = oracle.build_csr(d2b, b)
     vecs = oracle.gather_lists(x, off, ids)
     met = oracle.IP if metric == "inner_product" else oracle.L2
     rep = idx.max_replicas if dedup else 0
     Do, Io, nco = oracle.scan_topk(q, off, ids, vecs, probe, k, met, rep)
-    for exact in (False, True):
-        D, I, nc = run(idx, q, probe, k, dedup=dedup, exact=exact)
-        assert np.array_equal(I, Io), f"ids differ (exact={exact})"
-        assert np.array_equal(bits(D), bits(Do)), f"distances differ (exact={exact})"
+    for exact, split in ((False, True), (False, False), (True, True)):
+        D, I, nc = run(idx, q, probe, k, dedup=dedup, exact=exact, split=split)
+        assert np.array_equal(I, Io), f"ids differ (exact={exact}, split={split})"
+        assert np.array_equal(bits(D), bits(Do)), f"distances differ (exact={exact}, split={split})"
         assert np.array_equal(nc, nco)
     return idx
 
