@@ -30,6 +30,7 @@ import torch  # noqa: E402
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_F32_PEAK_TOPS = 78.64   # non-FMA fp32 lane ops/s: 157.3 TFLOP/s counts an FMA as 2
 MFMA_F32_PEAK_TFLOPS = 157.3  # v_mfma_f32_32x32x2_f32 dense peak (MI355X_MICROARCH.md)
+MFMA_BF16_PEAK_TFLOPS = 2516.6  # dense bf16 MFMA peak, 16 x the f32 rate (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -312,8 +313,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "accumulation": "fma (LIRA_SCAN_FMA, tolerance variant)" if args.fma
-            else "fp32 FMA screen (MFMA) under a rigorous error bound + exact re-check in search.cpp's "
-                 "sequential fp32 sub/mul/add: bit-exact",
+            else "split-bf16 MFMA screen (hi/lo bf16 parts, fp32 accumulation) under a rigorous error "
+                 "bound + exact re-check in search.cpp's sequential fp32 sub/mul/add: bit-exact",
             "data": (f"synthetic latent (intrinsic dim {LATENT_DIM[args.config]}, k-means partitions)"
                      if args.data == "latent" else
                      "synthetic Gaussian mixture (sigma 0.35, separated clusters, nearest-centre partitions)"),
@@ -328,11 +329,16 @@ def main():
                              "achieved": traffic / (scan_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": traffic / (scan_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                              "source": "profiles/pmc_scan_%s.json (rocprofv3 PMC)" % args.config},
-                         "compute": {"kernel": "k_screen_m (v_mfma_f32_16x16x4_f32) / k_screen (k > 56)",
+                         "compute": {"kernel": "k_screen_m<SPLIT> (v_mfma_f32_16x16x32_bf16, 4 bf16 products "
+                                               "per dim) / k_screen (k > 56, fp32 VALU)",
                                      "achieved": screen_tflops, "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
                                      "frac": screen_tflops / MFMA_F32_PEAK_TFLOPS,
                                      "flops_executed": screen_flops,
-                                     "note": "2 x (row, candidate) pairs screened x dpad (stats[0]); "
+                                     "bf16_mfma": {"achieved": 4 * screen_tflops, "peak": MFMA_BF16_PEAK_TFLOPS,
+                                                   "frac": 4 * screen_tflops / MFMA_BF16_PEAK_TFLOPS,
+                                                   "note": "the split form executes 4 bf16 products per "
+                                                           "fp32-equivalent multiply-add"} if k <= 56 else None,
+                                     "note": "fp32-equivalent: 2 x (row, candidate) pairs screened x dpad (stats[0]); "
                                              "the rest of the SURVEY 8(d) work is skipped exactly "
                                              "(triangle bound) or never needed (screen)"},
                          "exact_kernel": {"kernel": "k_scan (LIRA_SCAN_EXACT)", "scan_ms": scan_ex_ms,
