@@ -118,6 +118,45 @@ int lira_index_list_size(const lira_index *idx, int64_t list_no, int64_t *out);
 /* bytes of HBM the index holds */
 int lira_index_memory(const lira_index *idx, int64_t *bytes);
 
+/*
+ * Per-handle tuning options (no process environment is read by the library).
+ * None of them changes a result: every setting returns the same bits.
+ *   LIRA_OPT_KEEP_TILES  1 (default): keep the fp32 d-major tile copy that the
+ *                        all-exact scan (LIRA_SCAN_EXACT / _FMA) and the VALU
+ *                        screen read; 0: the index holds only the row-major
+ *                        copy + the split-bf16 screen copy (2 N d 4 bytes
+ *                        instead of 3), and scans that need the tiles return
+ *                        LIRA_EUNSUPPORTED.  Read by the next add/build.
+ *   LIRA_OPT_SCREEN      1: screened scan where supported (default); 0: always
+ *                        the all-exact kernel
+ *   LIRA_OPT_SPLIT       1: split-bf16 MFMA screen (default); 0: fp32 MFMA screen
+ *   LIRA_OPT_QR          queries per screen work item: 0 auto (default), 64, 128
+ *   LIRA_OPT_TWO_PHASE   nearest-probe group first: 1 auto (default), 0 off, 2 always
+ *   LIRA_OPT_PRUNE       L2 triangle-inequality block skip / exact early abandon (1)
+ *   LIRA_OPT_SEED        exact starting bound per query before the screen (1)
+ *   LIRA_OPT_SHARE       per-block exchange of query bounds between work items (1)
+ *   LIRA_OPT_ROUNDS      work items per workgroup target (0 = kernel default)
+ *   LIRA_OPT_NEAR_ROUNDS the same for the nearest-probe group (default 2)
+ *   LIRA_OPT_MFMA        screen engine: 1 auto (default), 0 VALU, 2 MFMA wherever it fits
+ *   LIRA_OPT_DEBUG       timing experiments only (results invalid): bit mask, see lira_screen.hip
+ */
+#define LIRA_OPT_KEEP_TILES 1
+#define LIRA_OPT_SCREEN 2
+#define LIRA_OPT_SPLIT 3
+#define LIRA_OPT_QR 4
+#define LIRA_OPT_TWO_PHASE 5
+#define LIRA_OPT_PRUNE 6
+#define LIRA_OPT_SEED 7
+#define LIRA_OPT_SHARE 8
+#define LIRA_OPT_ROUNDS 9
+#define LIRA_OPT_NEAR_ROUNDS 10
+#define LIRA_OPT_MFMA 11
+#define LIRA_OPT_DEBUG 12
+int lira_index_set_option(lira_index *idx, int option, int64_t value);
+int lira_index_get_option(const lira_index *idx, int option, int64_t *value);
+/* 1 if the index holds the fp32 tile copy (LIRA_OPT_KEEP_TILES at build time) */
+int lira_index_has_tiles(const lira_index *idx, int *out);
+
 /* ----------------------------------------------------------- ranking */
 /*
  * Query -> centroid Euclidean distances, exact fp32 in search.cpp's order:
@@ -192,6 +231,10 @@ int lira_scan_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe_m
 int lira_scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
                    int64_t nprobe_max, int64_t k, unsigned flags, float *out_D, int64_t *out_I,
                    int64_t *out_ncand, void *workspace, size_t workspace_bytes, void *stream);
+/* the scan kernel (and its plan) lira_scan_topk would run for this shape, as
+ * a NUL-terminated string into out (host, out_len bytes) -- for benchmarks */
+int lira_scan_describe(const lira_index *idx, int64_t nq, int64_t nprobe_max, int64_t k, unsigned flags,
+                       char *out, size_t out_len);
 
 /*
  * Kernel timing for benchmarks.  While enabled, every lira_scan_topk records

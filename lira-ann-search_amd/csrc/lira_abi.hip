@@ -23,50 +23,81 @@ int fail(int code, const std::string &msg) {
 
 int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
+hipError_t set_smem_attr_once(std::atomic<uint64_t> &mask, const void *fn, int bytes) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const uint64_t bit = dev < 64 ? 1ull << dev : 0;
+    if (bit && (mask.load(std::memory_order_acquire) & bit)) return hipSuccess;
+    // idempotent: two threads racing here both set the same attribute
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess && bit) mask.fetch_or(bit, std::memory_order_acq_rel);
+    return e;
+}
+
 // scan entry points (lira_scan.hip)
 int scan_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, size_t *bytes);
+std::string scan_describe(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, unsigned flags);
 int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe, int64_t nprobe,
               int64_t k, unsigned flags, float *out_D, int64_t *out_I, int64_t *out_ncand,
               void *ws, size_t ws_bytes, hipStream_t st);
 
-// Gather x[list_ids] into [tile][dpad][64]; one workgroup per tile, lane = row.
-__global__ __launch_bounds__(256) void k_tile_gather(const float *x, int64_t d, int64_t dpad,
-                                                     const int32_t *list_ids,
-                                                     const int64_t *list_off,
-                                                     const int32_t *tile_off,
-                                                     const int32_t *tile_list, int64_t n_tiles,
-                                                     float *X, int32_t *ids) {
-    const int l = threadIdx.x & 63, jg = threadIdx.x >> 6;
+// Build order (row-major first, so the fp32 tile copy is optional):
+//   Xr  [n_tiles*64][d] fp32 by storage row = x[list_ids] (k_row_gather); the
+//       screened path's exact re-check and k_seed read it, and every other
+//       copy / statistic below is derived from it;
+//   Xb  the split-bf16 screen copy (k_split_rows);
+//   X   [n_tiles][dpad][64] fp32 d-major tiles (k_tiles_from_rows), only with
+//       LIRA_OPT_KEEP_TILES: read by the all-exact scan and the VALU screen.
+// Storage row of a list's r-th row: tile_off[b]*64 + r; rows past the list's
+// end (padding) are zero with id -1.
+
+// one workgroup per tile, a wave per row, lanes along the row (coalesced)
+__global__ __launch_bounds__(256) void k_row_gather(const float *x, int64_t d, const int32_t *list_ids,
+                                                    const int64_t *list_off, const int32_t *tile_off,
+                                                    const int32_t *tile_list, int64_t n_tiles, float *Xr,
+                                                    int32_t *ids) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
         const int b = tile_list[t];
-        const int64_t r = (t - tile_off[b]) * kTile + l;
         const int64_t n = list_off[b + 1] - list_off[b];
-        const bool valid = r < n;
-        const int32_t gid = valid ? list_ids[list_off[b] + r] : -1;
-        const float *src = valid ? x + (int64_t)gid * d : nullptr;
-        float *dst = X + t * dpad * kTile + l;
-        for (int64_t j = jg; j < dpad; j += 4) dst[j * kTile] = (valid && j < d) ? src[j] : 0.0f;
-        if (jg == 0) ids[t * kTile + l] = gid;
+        const int64_t r0 = (t - tile_off[b]) * kTile;
+        for (int r = w; r < kTile; r += 4) {
+            const bool valid = r0 + r < n;
+            const int32_t gid = valid ? list_ids[list_off[b] + r0 + r] : -1;
+            const float *src = x + (int64_t)(valid ? gid : 0) * d;
+            float *dst = Xr + (t * kTile + r) * d;
+            for (int64_t j = lane; j < d; j += 64) dst[j] = valid ? src[j] : 0.0f;
+            if (lane == 0) ids[t * kTile + r] = gid;
+        }
     }
 }
 
-// Pivot of list b = mean of its rows (double sums; pad rows of X are zero).
-// One thread per (list, dim); rows read as float4 runs of a tile's dim row.
-__global__ __launch_bounds__(256) void k_list_pivot(const float *X, int64_t d, int64_t dpad,
-                                                    const int32_t *tile_off, const int64_t *list_off,
-                                                    float *pivot) {
+// Pivot of list b = mean of its rows, in double.  Pass 1: per segment of
+// kPivSeg rows of one list, per-dim sums (threads along the row: coalesced);
+// pass 2 adds a list's segments in order (deterministic).
+static constexpr int kPivSeg = 4096;
+__global__ __launch_bounds__(256) void k_pivot_partial(const float *Xr, int64_t d, const int32_t *seg_list,
+                                                       const int32_t *seg_first, const int32_t *tile_off,
+                                                       const int64_t *list_off, double *psum) {
+    const int s = blockIdx.x, b = seg_list[s];
+    const int64_t j = (int64_t)blockIdx.y * blockDim.x + threadIdx.x;
+    if (j >= d) return;
+    const int64_t n = list_off[b + 1] - list_off[b];
+    const int64_t r0 = (int64_t)(s - seg_first[b]) * kPivSeg, r1 = min(n, r0 + kPivSeg);
+    const float *base = Xr + (int64_t)tile_off[b] * kTile * d + j;
+    double acc = 0.0;
+#pragma unroll 8
+    for (int64_t r = r0; r < r1; ++r) acc += (double)base[r * d];
+    psum[(int64_t)s * d + j] = acc;
+}
+__global__ __launch_bounds__(256) void k_pivot_final(int64_t d, const int32_t *seg_first, const int64_t *list_off,
+                                                     const double *psum, float *pivot) {
     const int b = blockIdx.x;
     const int64_t j = (int64_t)blockIdx.y * blockDim.x + threadIdx.x;
     if (j >= d) return;
     double s = 0.0;
-    for (int t = tile_off[b]; t < tile_off[b + 1]; ++t) {
-        const float4 *row = (const float4 *)(X + ((int64_t)t * dpad + j) * kTile);
-#pragma unroll 4
-        for (int r = 0; r < kTile / 4; ++r) {
-            const float4 v = row[r];
-            s += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
-        }
-    }
+    for (int g = seg_first[b]; g < seg_first[b + 1]; ++g) s += psum[(int64_t)g * d + j];
     const int64_t n = list_off[b + 1] - list_off[b];
     pivot[(int64_t)b * d + j] = n > 0 ? (float)(s / (double)n) : 0.0f;
 }
@@ -76,18 +107,17 @@ __global__ __launch_bounds__(256) void k_list_pivot(const float *X, int64_t d, i
 // margin (the double sum's error is ~d * 2^-53), min/max over the tile's real
 // rows (NaN rows are ignored by fminf/fmaxf; they are never selected either).
 // A tile without real rows gets (+inf, -inf).
-__global__ __launch_bounds__(256) void k_tile_stats(const float *X, const int32_t *ids, int64_t d,
-                                                    int64_t dpad, const int32_t *tile_list,
-                                                    const float *pivot, int64_t n_tiles,
+__global__ __launch_bounds__(256) void k_tile_stats(const float *Xr, const int32_t *ids, int64_t d,
+                                                    const int32_t *tile_list, const float *pivot, int64_t n_tiles,
                                                     float2 *tstat) {
     const int lane = threadIdx.x & 63;
     const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (t >= n_tiles) return;
     const float *pv = pivot + (int64_t)tile_list[t] * d;
-    const float *x = X + t * dpad * kTile + lane;
+    const float *x = Xr + (t * kTile + lane) * d;
     double s = 0.0;
     for (int64_t j = 0; j < d; ++j) {
-        const double df = (double)x[j * kTile] - (double)pv[j];
+        const double df = (double)x[j] - (double)pv[j];
         s = __builtin_fma(df, df, s);
     }
     const double R = __builtin_sqrt(s);
@@ -105,16 +135,16 @@ __global__ __launch_bounds__(256) void k_tile_stats(const float *X, const int32_
 // Screening constants of every storage row (lane = row of a tile): xadj and
 // the list's rmax (atomicMax on the bits of a non-negative float).  Norms in
 // double; sqrt rounded up with a 2^-40 relative margin.
-__global__ __launch_bounds__(256) void k_row_norms(const float *X, const int32_t *ids, int64_t d, int64_t dpad,
+__global__ __launch_bounds__(256) void k_row_norms(const float *Xr, const int32_t *ids, int64_t d,
                                                    const int32_t *tile_list, int64_t n_tiles, int metric,
                                                    float *xadj, float *rmax) {
     const int lane = threadIdx.x & 63;
     const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (t >= n_tiles) return;
-    const float *x = X + t * dpad * kTile + lane;
+    const float *x = Xr + (t * kTile + lane) * d;
     double s = 0.0;
     for (int64_t j = 0; j < d; ++j) {
-        const double v = (double)x[j * kTile];
+        const double v = (double)x[j];
         s = __builtin_fma(v, v, s);
     }
     const bool real = ids[t * kTile + lane] >= 0;
@@ -126,50 +156,46 @@ __global__ __launch_bounds__(256) void k_row_norms(const float *X, const int32_t
     if (lane == 0 && r > 0.0f) atomicMax((unsigned int *)&rmax[tile_list[t]], __float_as_uint(r));
 }
 
-// Xr[pos][j] = X[tile][j][row]: one workgroup per tile, LDS transpose of
-// 64-dim slabs (reads and writes coalesced).
-__global__ __launch_bounds__(256) void k_rowmajor(const float *X, int64_t d, int64_t dpad, float *Xr) {
+// X[tile][j][row] = Xr[tile*64 + row][j]: one workgroup per tile, LDS
+// transpose of 64-dim slabs (reads and writes coalesced); dims d..dpad-1 = 0.
+__global__ __launch_bounds__(256) void k_tiles_from_rows(const float *Xr, int64_t d, int64_t dpad, float *X) {
     __shared__ float sl[64][65];
     const int64_t t = blockIdx.x;
-    for (int64_t j0 = 0; j0 < d; j0 += 64) {
+    for (int64_t j0 = 0; j0 < dpad; j0 += 64) {
         for (int i = threadIdx.x; i < 64 * 64; i += 256) {
-            const int jj = i >> 6, r = i & 63;
-            if (j0 + jj < d) sl[jj][r] = X[(t * dpad + j0 + jj) * kTile + r];
+            const int r = i >> 6, jj = i & 63;
+            sl[jj][r] = j0 + jj < d ? Xr[(t * kTile + r) * d + j0 + jj] : 0.0f;
         }
         __syncthreads();
         for (int i = threadIdx.x; i < 64 * 64; i += 256) {
-            const int r = i >> 6, jj = i & 63;
-            if (j0 + jj < d) Xr[(t * kTile + r) * d + j0 + jj] = sl[jj][r];
+            const int jj = i >> 6, r = i & 63;
+            if (j0 + jj < dpad) X[(t * dpad + j0 + jj) * kTile + r] = sl[jj][r];
         }
         __syncthreads();
     }
 }
 
-// Xb: the split-bf16 copy of X for the MFMA screen (lira_screen.hip
+// Xb: the split-bf16 copy for the MFMA screen (lira_screen.hip
 // k_screen_m<..., SPLIT>).  Per tile and 16-dim chunk c, 4 KiB = [g 4][p 64]
 // [8 bf16], g = 2 hl + h: the hi (hl = 0) or lo (hl = 1) round-to-nearest
 // bf16 part of dims 16c + 8h .. +7 of candidate row 4 (p & 15) + (p >> 4) (the
 // permutation makes a 16-lane group's B-fragment reads consecutive).  One
 // workgroup per (tile, chunk), one 16-B unit per thread.
-__device__ __forceinline__ uint32_t bf16_rne_b(float v) {
-    const uint32_t b = __float_as_uint(v);
-    return (b + 0x7fffu + ((b >> 16) & 1u)) >> 16;
-}
-__global__ __launch_bounds__(256) void k_split_tiles(const float *X, int64_t n_tiles, int64_t dpad, uint4 *Xb) {
+__global__ __launch_bounds__(256) void k_split_rows(const float *Xr, int64_t d, int64_t n_tiles, int64_t dpad,
+                                                   uint4 *Xb) {
     const int64_t nch = dpad / 16, total = n_tiles * nch;
     const int u = threadIdx.x, g = u >> 6, p = u & 63, r = 4 * (p & 15) + (p >> 4), h = g & 1, hl = g >> 1;
     for (int64_t tc = blockIdx.x; tc < total; tc += gridDim.x) {
         const int64_t t = tc / nch, c = tc % nch;
-        const float *src = X + (t * dpad + 16 * c + 8 * h) * kTile + r;
+        const float *src = Xr + (t * kTile + r) * d;
         uint32_t w[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             uint32_t part[2];
 #pragma unroll
             for (int f = 0; f < 2; ++f) {
-                const float v = src[(2 * e + f) * kTile];
-                const uint32_t hi = bf16_rne_b(v);
-                part[f] = hl ? bf16_rne_b(v - __uint_as_float(hi << 16)) : hi;
+                const int64_t j = 16 * c + 8 * h + 2 * e + f;
+                part[f] = bf16_split_part(j < d ? src[j] : 0.0f, hl);
             }
             w[e] = part[0] | (part[1] << 16);
         }
@@ -281,13 +307,14 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
                               int32_t max_replicas, void *stream) {
     if (!idx) return fail(LIRA_EINVAL, "index is NULL");
     if (n_lists <= 0 || !list_offsets) return fail(LIRA_EINVAL, "n_lists must be > 0 with offsets");
+    if (n_lists >= INT32_MAX) return fail(LIRA_EINVAL, "n_lists must be < 2^31");
     if (n_rows < 0) return fail(LIRA_EINVAL, "n_rows < 0");
     DeviceGuard g(idx->device);
     hipStream_t st = (hipStream_t)stream;
     if (list_offsets[0] != 0) return fail(LIRA_EINVAL, "list_offsets[0] must be 0");
     std::vector<int64_t> size(n_lists), toff(n_lists + 1);
-    std::vector<int32_t> toff32(n_lists + 1), size32(n_lists);
-    int64_t tiles = 0, mx = 0, mxt = 0;
+    std::vector<int32_t> toff32(n_lists + 1), size32(n_lists), seg_first(n_lists + 1);
+    int64_t tiles = 0, mx = 0, mxt = 0, segs = 0;
     for (int64_t b = 0; b < n_lists; ++b) {
         int64_t n = list_offsets[b + 1] - list_offsets[b];
         if (n < 0) return fail(LIRA_EINVAL, "list_offsets must be non-decreasing");
@@ -296,33 +323,40 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
         size32[b] = (int32_t)n;
         toff[b] = tiles;
         toff32[b] = (int32_t)tiles;
+        seg_first[b] = (int32_t)segs;
+        segs += (n + kPivSeg - 1) / kPivSeg;
         int64_t nt = (n + kTile - 1) / kTile;
         tiles += nt;
         mx = std::max(mx, n);
         mxt = std::max(mxt, nt);
     }
     toff[n_lists] = tiles;
-    if (tiles >= INT32_MAX) return fail(LIRA_EUNSUPPORTED, "more than 2^31 tiles");
+    seg_first[n_lists] = (int32_t)segs;
+    if (tiles >= INT32_MAX / kTile) return fail(LIRA_EUNSUPPORTED, "more than 2^31 storage rows");
     toff32[n_lists] = (int32_t)tiles;
     const int64_t total = list_offsets[n_lists];
     if (total > 0 && (!list_ids || !x)) return fail(LIRA_EINVAL, "list_ids / x is NULL");
     if (n_rows > INT32_MAX) return fail(LIRA_EUNSUPPORTED, "more than 2^31 base rows (int32 gids)");
 
     free_storage(idx);
-    std::vector<int32_t> tile_list(tiles);
-    for (int64_t b = 0; b < n_lists; ++b)
+    std::vector<int32_t> tile_list(tiles), seg_list(segs);
+    for (int64_t b = 0; b < n_lists; ++b) {
         for (int64_t t = toff[b]; t < toff[b + 1]; ++t) tile_list[t] = (int32_t)b;
-
-    const size_t xbytes = (size_t)std::max<int64_t>(tiles, 1) * idx->dpad * kTile * 4;
-    if (hipMalloc(&idx->X, xbytes) != hipSuccess ||
-        hipMalloc(&idx->ids, (size_t)std::max<int64_t>(tiles, 1) * kTile * 4) != hipSuccess ||
+        for (int32_t s = seg_first[b]; s < seg_first[b + 1]; ++s) seg_list[s] = (int32_t)b;
+    }
+    const int64_t d = idx->d, dpad = idx->dpad, rows = std::max<int64_t>(tiles, 1) * kTile;
+    // the row-major copy first: everything else derives from it (x may be freed afterwards)
+    if (hipMalloc(&idx->Xr, (size_t)rows * d * 4) != hipSuccess ||
+        hipMalloc(&idx->ids, (size_t)rows * 4) != hipSuccess ||
         hipMalloc(&idx->tile_off, (n_lists + 1) * 4) != hipSuccess ||
         hipMalloc(&idx->list_size, n_lists * 4) != hipSuccess) {
         free_storage(idx);
-        return fail(LIRA_ENOMEM, "hipMalloc of " + std::to_string(xbytes) + " bytes for the lists failed");
+        return fail(LIRA_ENOMEM, "hipMalloc of " + std::to_string((size_t)rows * d * 4) +
+                                     " bytes for the lists failed");
     }
     int64_t *d_loff = nullptr;
-    int32_t *d_tlist = nullptr, *d_bad = nullptr;
+    int32_t *d_tlist = nullptr, *d_bad = nullptr, *d_seg = nullptr, *d_segf = nullptr;
+    double *d_psum = nullptr;
     int rc = LIRA_OK;
     do {
         if (hipMalloc(&d_loff, (n_lists + 1) * 8) != hipSuccess ||
@@ -355,62 +389,97 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
             }
         }
         if (tiles > 0) {
-            int grid = (int)std::min<int64_t>(tiles, 65536);
-            hipLaunchKernelGGL(k_tile_gather, dim3(grid), dim3(256), 0, st, x, idx->d, idx->dpad,
-                               list_ids, d_loff, idx->tile_off, d_tlist, tiles, idx->X, idx->ids);
+            const int grid = (int)std::min<int64_t>(tiles, 65536);
+            hipLaunchKernelGGL(k_row_gather, dim3(grid), dim3(256), 0, st, x, d, list_ids, d_loff, idx->tile_off,
+                               d_tlist, tiles, idx->Xr, idx->ids);
         }
         e = hipGetLastError();
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) {
-            rc = fail(LIRA_EHIP, std::string("tile gather failed: ") + hipGetErrorString(e));
+            rc = fail(LIRA_EHIP, std::string("row gather failed: ") + hipGetErrorString(e));
             break;
         }
-        if (tiles > 0) {
-            if (hipMalloc(&idx->xadj, (size_t)tiles * kTile * 4) != hipSuccess ||
-                hipMalloc(&idx->rmax, (size_t)n_lists * 4) != hipSuccess ||
-                hipMalloc(&idx->Xr, (size_t)tiles * kTile * idx->d * 4) != hipSuccess ||
-                hipMalloc(&idx->Xb, (size_t)tiles * kTile * idx->dpad * 4) != hipSuccess) {
-                rc = fail(LIRA_ENOMEM, "hipMalloc of the row-norm arrays failed");
-                break;
-            }
-            e = hipMemsetAsync(idx->rmax, 0, (size_t)n_lists * 4, st);
-            if (e == hipSuccess) {
-                hipLaunchKernelGGL(k_row_norms, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, idx->X,
-                                   idx->ids, idx->d, idx->dpad, d_tlist, tiles, idx->metric, idx->xadj,
-                                   idx->rmax);
-                hipLaunchKernelGGL(k_rowmajor, dim3((unsigned)tiles), dim3(256), 0, st, idx->X, idx->d, idx->dpad,
-                                   idx->Xr);
-                hipLaunchKernelGGL(k_split_tiles, dim3((unsigned)std::min<int64_t>(tiles * (idx->dpad / 16), 1 << 20)),
-                                   dim3(256), 0, st, idx->X, tiles, idx->dpad, (uint4 *)idx->Xb);
-                e = hipGetLastError();
-            }
-            if (e == hipSuccess) e = hipStreamSynchronize(st);
-            if (e != hipSuccess) {
-                rc = fail(LIRA_EHIP, std::string("row norms failed: ") + hipGetErrorString(e));
-                break;
-            }
+        if (tiles == 0) {  // an empty index: the all-exact kernel (one zero tile) answers with pads
+            if (hipMalloc(&idx->X, (size_t)dpad * kTile * 4) != hipSuccess ||
+                hipMemsetAsync(idx->X, 0, (size_t)dpad * kTile * 4, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess)
+                rc = fail(LIRA_ENOMEM, "hipMalloc of the (empty) tile copy failed");
+            break;
         }
-        if (idx->metric == LIRA_METRIC_L2 && tiles > 0) {
-            if (hipMalloc(&idx->pivot, (size_t)n_lists * idx->d * 4) != hipSuccess ||
-                hipMalloc(&idx->tstat, (size_t)tiles * sizeof(float2)) != hipSuccess) {
+        if (hipMalloc(&idx->xadj, (size_t)tiles * kTile * 4) != hipSuccess ||
+            hipMalloc(&idx->rmax, (size_t)n_lists * 4) != hipSuccess) {
+            rc = fail(LIRA_ENOMEM, "hipMalloc of the row-norm arrays failed");
+            break;
+        }
+        e = hipMemsetAsync(idx->rmax, 0, (size_t)n_lists * 4, st);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_row_norms, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, idx->Xr, idx->ids,
+                               d, d_tlist, tiles, idx->metric, idx->xadj, idx->rmax);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess && idx->metric == LIRA_METRIC_L2) {
+            if (hipMalloc(&idx->pivot, (size_t)n_lists * d * 4) != hipSuccess ||
+                hipMalloc(&idx->tstat, (size_t)tiles * sizeof(float2)) != hipSuccess ||
+                hipMalloc(&d_seg, (size_t)std::max<int64_t>(segs, 1) * 4) != hipSuccess ||
+                hipMalloc(&d_segf, (size_t)(n_lists + 1) * 4) != hipSuccess ||
+                hipMalloc(&d_psum, (size_t)std::max<int64_t>(segs, 1) * d * 8) != hipSuccess) {
                 rc = fail(LIRA_ENOMEM, "hipMalloc of the pivot / tile radius arrays failed");
                 break;
             }
-            hipLaunchKernelGGL(k_list_pivot, dim3((unsigned)n_lists, (unsigned)((idx->d + 255) / 256)), dim3(256),
-                               0, st, idx->X, idx->d, idx->dpad, idx->tile_off, d_loff, idx->pivot);
-            hipLaunchKernelGGL(k_tile_stats, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, idx->X,
-                               idx->ids, idx->d, idx->dpad, d_tlist, idx->pivot, tiles, idx->tstat);
+            e = hipMemcpyAsync(d_seg, seg_list.data(), (size_t)segs * 4, hipMemcpyHostToDevice, st);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(d_segf, seg_first.data(), (size_t)(n_lists + 1) * 4, hipMemcpyHostToDevice, st);
+            const unsigned dy = (unsigned)((d + 255) / 256);
+            if (e == hipSuccess && segs > 0)
+                hipLaunchKernelGGL(k_pivot_partial, dim3((unsigned)segs, dy), dim3(256), 0, st, idx->Xr, d, d_seg,
+                                   d_segf, idx->tile_off, d_loff, d_psum);
+            if (e == hipSuccess) {
+                hipLaunchKernelGGL(k_pivot_final, dim3((unsigned)n_lists, dy), dim3(256), 0, st, d, d_segf, d_loff,
+                                   d_psum, idx->pivot);
+                hipLaunchKernelGGL(k_tile_stats, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, idx->Xr,
+                                   idx->ids, d, d_tlist, idx->pivot, tiles, idx->tstat);
+                e = hipGetLastError();
+            }
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) {
+            rc = fail(LIRA_EHIP, std::string("row norms / pivots failed: ") + hipGetErrorString(e));
+            break;
+        }
+        // the split-bf16 screen copy: best effort (without it the screen runs on fp32 MFMA / VALU)
+        if (hipMalloc(&idx->Xb, (size_t)tiles * kTile * dpad * 4) == hipSuccess) {
+            hipLaunchKernelGGL(k_split_rows, dim3((unsigned)std::min<int64_t>(tiles * (dpad / 16), 1 << 20)),
+                               dim3(256), 0, st, idx->Xr, d, tiles, dpad, (uint4 *)idx->Xb);
             e = hipGetLastError();
-            if (e == hipSuccess) e = hipStreamSynchronize(st);
-            if (e != hipSuccess) {
-                rc = fail(LIRA_EHIP, std::string("pivot / tile radius build failed: ") + hipGetErrorString(e));
+        } else {
+            (void)hipGetLastError();
+            idx->Xb = nullptr;
+        }
+        // the fp32 tile copy for the all-exact / VALU kernels (LIRA_OPT_KEEP_TILES)
+        if (e == hipSuccess && idx->opt.keep_tiles) {
+            if (hipMalloc(&idx->X, (size_t)tiles * dpad * kTile * 4) != hipSuccess) {
+                rc = fail(LIRA_ENOMEM, "hipMalloc of the fp32 tile copy failed (LIRA_OPT_KEEP_TILES = 0 drops it)");
                 break;
             }
+            hipLaunchKernelGGL(k_tiles_from_rows, dim3((unsigned)tiles), dim3(256), 0, st, idx->Xr, d, dpad, idx->X);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) {
+            rc = fail(LIRA_EHIP, std::string("screen / tile copies failed: ") + hipGetErrorString(e));
+            break;
+        }
+        if (!idx->X && !idx->Xb) {
+            rc = fail(LIRA_ENOMEM, "neither the split-bf16 screen copy nor the fp32 tiles could be allocated");
+            break;
         }
     } while (0);
     if (d_loff) hipFree(d_loff);
     if (d_tlist) hipFree(d_tlist);
     if (d_bad) hipFree(d_bad);
+    if (d_seg) hipFree(d_seg);
+    if (d_segf) hipFree(d_segf);
+    if (d_psum) hipFree(d_psum);
     if (rc != LIRA_OK) {
         free_storage(idx);
         return rc;
@@ -446,11 +515,63 @@ int lira_index_list_size(const lira_index *idx, int64_t list_no, int64_t *out) {
 
 int lira_index_memory(const lira_index *idx, int64_t *bytes) {
     if (!idx || !bytes) return fail(LIRA_EINVAL, "NULL argument");
-    *bytes = idx->n_tiles * idx->dpad * kTile * 4 + idx->n_tiles * kTile * 4 + idx->n_lists * 8 +
-             (idx->pivot ? idx->n_lists * idx->d * 4 + idx->n_tiles * 8 : 0) +
-             (idx->xadj ? idx->n_tiles * kTile * 4 + idx->n_lists * 4 : 0) +
-             (idx->Xr ? idx->n_tiles * kTile * idx->d * 4 : 0) +
-             (idx->Xb ? idx->n_tiles * kTile * idx->dpad * 4 : 0);
+    const int64_t rows = idx->n_tiles * kTile;
+    *bytes = rows * 4 + idx->n_lists * 8 +                                   // ids, tile_off + list_size
+             (idx->Xr ? rows * idx->d * 4 : 0) +                               // row-major copy
+             (idx->Xb ? rows * idx->dpad * 4 : 0) +                            // split-bf16 copy
+             (idx->X ? rows * idx->dpad * 4 : 0) +                             // fp32 tiles (optional)
+             (idx->xadj ? rows * 4 + idx->n_lists * 4 : 0) +                   // xadj, rmax
+             (idx->pivot ? idx->n_lists * idx->d * 4 + idx->n_tiles * 8 : 0);  // pivots, tile radii
+    return LIRA_OK;
+}
+
+int lira_index_set_option(lira_index *idx, int option, int64_t value) {
+    if (!idx) return fail(LIRA_EINVAL, "index is NULL");
+    lira_opts &o = idx->opt;
+    const int v = (int)value;
+    auto in = [&](int lo, int hi) { return value >= lo && value <= hi; };
+    switch (option) {
+        case LIRA_OPT_KEEP_TILES: if (!in(0, 1)) break; o.keep_tiles = v; return LIRA_OK;
+        case LIRA_OPT_SCREEN: if (!in(0, 1)) break; o.screen = v; return LIRA_OK;
+        case LIRA_OPT_SPLIT: if (!in(0, 1)) break; o.split = v; return LIRA_OK;
+        case LIRA_OPT_QR: if (value != 0 && value != 64 && value != 128) break; o.qr = v; return LIRA_OK;
+        case LIRA_OPT_TWO_PHASE: if (!in(0, 2)) break; o.two_phase = v; return LIRA_OK;
+        case LIRA_OPT_PRUNE: if (!in(0, 1)) break; o.prune = v; return LIRA_OK;
+        case LIRA_OPT_SEED: if (!in(0, 1)) break; o.seed = v; return LIRA_OK;
+        case LIRA_OPT_SHARE: if (!in(0, 1)) break; o.share = v; return LIRA_OK;
+        case LIRA_OPT_ROUNDS: if (!in(0, 1024)) break; o.rounds = v; return LIRA_OK;
+        case LIRA_OPT_NEAR_ROUNDS: if (!in(1, 1024)) break; o.near_rounds = v; return LIRA_OK;
+        case LIRA_OPT_MFMA: if (!in(0, 2)) break; o.mfma = v; return LIRA_OK;
+        case LIRA_OPT_DEBUG: if (!in(0, 255)) break; o.debug = v; return LIRA_OK;
+        default: return fail(LIRA_EINVAL, "unknown option " + std::to_string(option));
+    }
+    return fail(LIRA_EINVAL, "value " + std::to_string(value) + " out of range for option " + std::to_string(option));
+}
+
+int lira_index_get_option(const lira_index *idx, int option, int64_t *value) {
+    if (!idx || !value) return fail(LIRA_EINVAL, "NULL argument");
+    const lira_opts &o = idx->opt;
+    switch (option) {
+        case LIRA_OPT_KEEP_TILES: *value = o.keep_tiles; break;
+        case LIRA_OPT_SCREEN: *value = o.screen; break;
+        case LIRA_OPT_SPLIT: *value = o.split; break;
+        case LIRA_OPT_QR: *value = o.qr; break;
+        case LIRA_OPT_TWO_PHASE: *value = o.two_phase; break;
+        case LIRA_OPT_PRUNE: *value = o.prune; break;
+        case LIRA_OPT_SEED: *value = o.seed; break;
+        case LIRA_OPT_SHARE: *value = o.share; break;
+        case LIRA_OPT_ROUNDS: *value = o.rounds; break;
+        case LIRA_OPT_NEAR_ROUNDS: *value = o.near_rounds; break;
+        case LIRA_OPT_MFMA: *value = o.mfma; break;
+        case LIRA_OPT_DEBUG: *value = o.debug; break;
+        default: return fail(LIRA_EINVAL, "unknown option " + std::to_string(option));
+    }
+    return LIRA_OK;
+}
+
+int lira_index_has_tiles(const lira_index *idx, int *out) {
+    if (!idx || !out) return fail(LIRA_EINVAL, "NULL argument");
+    *out = idx->X != nullptr;
     return LIRA_OK;
 }
 
@@ -461,6 +582,18 @@ int lira_scan_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe_m
     if (nq < 0 || nprobe_max <= 0 || k <= 0 || k > 256)
         return fail(LIRA_EINVAL, "need nq >= 0, nprobe_max > 0, 1 <= k <= 256");
     return scan_workspace_size(idx, nq, nprobe_max, k, bytes);
+}
+
+int lira_scan_describe(const lira_index *idx, int64_t nq, int64_t nprobe_max, int64_t k, unsigned flags,
+                       char *out, size_t out_len) {
+    if (!idx || !out || out_len == 0) return fail(LIRA_EINVAL, "NULL argument");
+    if (idx->n_lists == 0) return fail(LIRA_ESTATE, "index has no lists (add_partitions first)");
+    if (nq < 0 || nprobe_max <= 0 || k <= 0 || k > 256) return fail(LIRA_EINVAL, "need nq >= 0, nprobe_max > 0, 1 <= k <= 256");
+    const std::string s = scan_describe(idx, nq, nprobe_max, k, flags);
+    const size_t n = std::min(out_len - 1, s.size());
+    std::memcpy(out, s.data(), n);
+    out[n] = 0;
+    return LIRA_OK;
 }
 
 int lira_scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,

@@ -234,6 +234,25 @@ __device__ __forceinline__ u64 wave_list_at(const u64 (&list)[R], int e) {
     return shfl64(x, e & 63);
 }
 
+// ---- split-bf16 parts (the MFMA screen's operands) ----
+// fp32 -> bf16 bits, round to nearest even.  A finite value that would round
+// to infinity saturates to the largest finite bf16 (0x7f7f, sign kept), so its
+// lo part below stays finite and hi + lo + e = v with |e| <= 2^-16 |v| still
+// holds; a NaN stays a (quiet) NaN; infinities pass through.
+__device__ __forceinline__ uint32_t bf16_rne_sat(float v) {
+    const uint32_t b = __float_as_uint(v);
+    if ((b & 0x7fffffffu) > 0x7f800000u) return (b >> 16) | 0x40u;  // NaN
+    uint32_t r = (b + 0x7fffu + ((b >> 16) & 1u)) >> 16;
+    if ((r & 0x7fffu) == 0x7f80u && (b & 0x7f800000u) != 0x7f800000u) r = (r & 0x8000u) | 0x7f7fu;
+    return r;
+}
+// the hi (hl = 0) or lo (hl = 1) bf16 part of v: v = hi + lo + e, |e| <= 2^-16 |v|
+// (v - hi is exact in fp32: Sterbenz, or hi = 0)
+__device__ __forceinline__ uint32_t bf16_split_part(float v, int hl) {
+    const uint32_t hi = bf16_rne_sat(v);
+    return hl ? bf16_rne_sat(v - __uint_as_float(hi << 16)) : hi;
+}
+
 __device__ __forceinline__ int popc64(u64 m) { return __popcll(m); }
 // number of set bits of m in lanes below this lane
 __device__ __forceinline__ int mbcnt64(u64 m) {

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -30,7 +31,28 @@ int fail(int code, const std::string &msg);
 static constexpr int kTile = 64;
 static constexpr int kDimChunk = 32;
 
+// lira_index_set_option values (include/lira_hip.h LIRA_OPT_*)
+struct lira_opts {
+    int keep_tiles = 1;
+    int screen = 1;
+    int split = 1;
+    int qr = 0;
+    int two_phase = 1;
+    int prune = 1;
+    int seed = 1;
+    int share = 1;
+    int rounds = 0;
+    int near_rounds = 2;
+    int mfma = 1;
+    int debug = 0;
+};
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device):
+// `mask` is the kernel's own latch, one bit per device ordinal.
+hipError_t set_smem_attr_once(std::atomic<uint64_t> &mask, const void *fn, int bytes);
+
 struct lira_index_impl {
+    lira_opts opt;
     int device = 0;
     int64_t d = 0, dpad = 0;
     int metric = LIRA_METRIC_L2;

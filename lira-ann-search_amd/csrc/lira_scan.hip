@@ -878,10 +878,7 @@ static ScanPlan make_plan(const lira_index *idx, int64_t nq, int64_t nprobe, int
     // Split buckets into chunks until the persistent grid sees ~`rounds` items
     // per workgroup, so the last, partly filled round of items is a small
     // fraction of the run (the tail); LIRA_SCAN_ROUNDS overrides (tuning).
-    static const int rounds = [] {
-        const char *e = getenv("LIRA_SCAN_ROUNDS");
-        return e && atoi(e) > 0 ? atoi(e) : 16;
-    }();
+    const int rounds = idx->opt.rounds > 0 ? idx->opt.rounds : 16;
     const int64_t target = (int64_t)rounds * pl.grid;
     const int64_t est_items = (npairs + kQT - 1) / kQT + std::min<int64_t>(idx->n_lists, npairs);
     const int64_t max_blocks = std::max<int64_t>(1, (idx->max_list_tiles + kBlockTiles - 1) / kBlockTiles);
@@ -915,13 +912,9 @@ static ScanPlan make_plan(const lira_index *idx, int64_t nq, int64_t nprobe, int
 template <int RL, int M, bool FMA>
 static hipError_t launch_scan(const ScanArgs &a, const ScanPlan &pl, hipStream_t st) {
     constexpr int OCC = ScanOcc<RL>::value;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void *)k_scan<RL, M, OCC, FMA>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
+    static std::atomic<uint64_t> attr{0};
+    hipError_t e = set_smem_attr_once(attr, (const void *)k_scan<RL, M, OCC, FMA>, 160 * 1024);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_scan<RL, M, OCC, FMA>), dim3(pl.grid), dim3(kScanThreads), pl.smem, st, a);
     return hipGetLastError();
 }
@@ -945,13 +938,10 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
                 size_t ws_bytes, hipStream_t st, hipEvent_t *ev);
 
 // the screened scan (lira_screen.hip) is the default; LIRA_SCAN_EXACT,
-// LIRA_SCAN_FMA or env LIRA_SCAN_SCREEN=0 select the all-exact k_scan
+// LIRA_SCAN_FMA or LIRA_OPT_SCREEN = 0 select the all-exact k_scan (which
+// reads the fp32 tiles: LIRA_OPT_KEEP_TILES)
 static bool use_screen(const lira_index *idx, int64_t k, unsigned flags) {
-    static const int env = [] {
-        const char *e = getenv("LIRA_SCAN_SCREEN");
-        return e && e[0] == '0' ? 0 : 1;
-    }();
-    return env && !(flags & (LIRA_SCAN_FMA | LIRA_SCAN_EXACT)) && screen_supported(idx, k);
+    return (idx->opt.screen || !idx->X) && !(flags & (LIRA_SCAN_FMA | LIRA_SCAN_EXACT)) && screen_supported(idx, k);
 }
 
 int scan_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k,
@@ -961,32 +951,12 @@ int scan_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     return LIRA_OK;
 }
 
-int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe, int64_t nprobe,
-              int64_t k, unsigned flags, float *out_D, int64_t *out_I, int64_t *out_ncand,
-              void *ws, size_t ws_bytes, hipStream_t st) {
+static int exact_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe, int64_t nprobe,
+                      int64_t k, unsigned flags, int Rm, float *out_D, int64_t *out_I, int64_t *out_ncand,
+                      void *ws, size_t ws_bytes, hipStream_t st, hipEvent_t *ev) {
     const bool dedup = (flags & LIRA_SCAN_DEDUP) != 0;
     const bool per_part = (flags & LIRA_SCAN_PER_PARTITION) != 0;
     const int RL = scan_rl(k);
-    int64_t kpm = std::max<int64_t>(64, per_part ? k : (dedup ? k * std::max(1, idx->max_replicas) : k));
-    int Rm = merge_r(kpm);
-    if (Rm < 0)
-        return fail(LIRA_EUNSUPPORTED,
-                    "k * max_replicas = " + std::to_string(k * idx->max_replicas) +
-                        " exceeds the 512-key merge list");
-    if (nq == 0) return LIRA_OK;
-    if (nq * nprobe > INT32_MAX) return fail(LIRA_EUNSUPPORTED, "nq * nprobe_max must be < 2^31");
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    if (idx->profiling) {
-        while (idx->ev_pool.size() < idx->ev_used + 4) {
-            hipEvent_t e;
-            LIRA_HIP_TRY(hipEventCreate(&e));
-            idx->ev_pool.push_back(e);
-        }
-        for (int i = 0; i < 4; ++i) ev[i] = idx->ev_pool[idx->ev_used + i];
-        idx->ev_used += 4;
-    }
-    if (use_screen(idx, k, flags))
-        return screen_topk(idx, q, nq, probe, nprobe, k, flags, Rm, out_D, out_I, out_ncand, ws, ws_bytes, st, ev);
     ScanPlan pl = make_plan(idx, nq, nprobe, k);
     if (!ws) {
         if (idx->ws_bytes < pl.total) {
@@ -1024,14 +994,8 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
     // One launch, so there is no tail between the groups.  With m = ceil(32 *
     // n_lists / nq) > 1 first-slot blocks would be part-filled; measured slower
     // there (GIST1M, BIGANN), so one group.
-    static const int prune_env = [] {
-        const char *e = getenv("LIRA_SCAN_PRUNE");
-        return e && e[0] == '0' ? 0 : 1;
-    }();
-    static const int two_group_env = [] {
-        const char *e = getenv("LIRA_SCAN_TWO_PHASE");
-        return e ? atoi(e) : 1;
-    }();
+    const int prune_env = idx->opt.prune;
+    const int two_group_env = idx->opt.two_phase;
     const int64_t m1 = (kQT * (int64_t)nl + nq - 1) / nq;
     const bool l2_prune = idx->metric == LIRA_METRIC_L2 && prune_env && !(flags & LIRA_SCAN_NO_PRUNE);
     const int groups = qbound && two_group_env && (m1 == 1 || l2_prune || two_group_env == 2) && nprobe >= 2
@@ -1111,6 +1075,53 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
     LIRA_HIP_TRY(hipGetLastError());
     if (ev[3]) LIRA_HIP_TRY(hipEventRecord(ev[3], st));
     return LIRA_OK;
+}
+
+std::string screen_describe(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, unsigned flags);
+
+std::string scan_describe(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, unsigned flags) {
+    if (use_screen(idx, k, flags)) return screen_describe(idx, nq, nprobe, k, flags);
+    if (!idx->X) return "unsupported (needs the fp32 tiles)";
+    ScanPlan pl = make_plan(idx, nq, nprobe, k);
+    return std::string("k_scan exact VALU") + ((flags & LIRA_SCAN_FMA) ? " FMA" : "") + " RL=" +
+           std::to_string(scan_rl(k)) + " grid=" + std::to_string(pl.grid) + " smem=" + std::to_string(pl.smem);
+}
+
+int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe, int64_t nprobe,
+              int64_t k, unsigned flags, float *out_D, int64_t *out_I, int64_t *out_ncand,
+              void *ws, size_t ws_bytes, hipStream_t st) {
+    const bool dedup = (flags & LIRA_SCAN_DEDUP) != 0;
+    const bool per_part = (flags & LIRA_SCAN_PER_PARTITION) != 0;
+    int64_t kpm = std::max<int64_t>(64, per_part ? k : (dedup ? k * std::max(1, idx->max_replicas) : k));
+    int Rm = merge_r(kpm);
+    if (Rm < 0)
+        return fail(LIRA_EUNSUPPORTED,
+                    "k * max_replicas = " + std::to_string(k * idx->max_replicas) +
+                        " exceeds the 512-key merge list");
+    if (nq == 0) return LIRA_OK;
+    if (nq * nprobe > INT32_MAX) return fail(LIRA_EUNSUPPORTED, "nq * nprobe_max must be < 2^31");
+    const bool scr = use_screen(idx, k, flags);
+    if (!scr && !idx->X)
+        return fail(LIRA_EUNSUPPORTED, (flags & (LIRA_SCAN_FMA | LIRA_SCAN_EXACT))
+                                           ? "LIRA_SCAN_EXACT / LIRA_SCAN_FMA need the fp32 tiles (LIRA_OPT_KEEP_TILES)"
+                                           : "k = " + std::to_string(k) +
+                                                 " needs the fp32 tiles (LIRA_OPT_KEEP_TILES) or k <= 120");
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    if (idx->profiling) {
+        while (idx->ev_pool.size() < idx->ev_used + 4) {
+            hipEvent_t e;
+            LIRA_HIP_TRY(hipEventCreate(&e));
+            idx->ev_pool.push_back(e);
+        }
+        for (int i = 0; i < 4; ++i) ev[i] = idx->ev_pool[idx->ev_used + i];
+        idx->ev_used += 4;
+    }
+    const int rc = scr ? screen_topk(idx, q, nq, probe, nprobe, k, flags, Rm, out_D, out_I, out_ncand, ws, ws_bytes,
+                                     st, ev)
+                       : exact_topk(idx, q, nq, probe, nprobe, k, flags, Rm, out_D, out_I, out_ncand, ws, ws_bytes,
+                                    st, ev);
+    if (rc != LIRA_OK && ev[0]) idx->ev_used -= 4;  // this call's events were not all recorded
+    return rc;
 }
 
 // Plan kernels for another scan kernel (lira_screen.hip): `groups` groups of

@@ -84,7 +84,6 @@ struct ScreenArgs {
     const float *Q;
     const float *pivot;
     const float2 *tstat;
-    int flush_at;  // a row's survivor buffer is merged into its list at this fill (<= 32)
     int share;     // k_screen_m: publish/re-read the query bound every block (else once per item)
     int split;     // k_screen_m<..., SPLIT = 1>: X is the split-bf16 copy (Xb), QT in the split layout
     int dbg;  // timing experiments only (env LIRA_SCAN_DEBUG; results invalid): 1 = no MFMA, 2 = no selection,
@@ -111,7 +110,10 @@ __device__ __forceinline__ double err_E(double qnorm, double R, double d, int sp
             const double s = qnorm + R;
             return 2.0 * ed + 1.05 * 8.0 * kU * s * s + dl;
         }
-        return 1.05 * ed + dl;
+        // IP: bound_P / s_lim carry no (1 +- g) factor, so E also covers
+        // search.cpp's own rounding of the exact sum, (d+2) u |q| R (L2 needs
+        // no such term: that error is the g of bound_P / s_lim)
+        return 1.05 * (ed + (d + 2.0) * kU * qnorm * R) + dl;
     }
     if (METRIC == LIRA_METRIC_L2) {
         const double s = qnorm + R;
@@ -152,18 +154,6 @@ __device__ __forceinline__ float row_h(double lim, double qn, double qnorm, doub
 // Block b = one query block (virtual partition v, block qb of QR pairs).
 // QN.w = fl(||q - pivot_p||) (double sum, round to nearest: the true value is
 // within 1 ulp) for the triangle skip, when a pivot array is given.
-// round-to-nearest-even fp32 -> bf16 bits (finite inputs)
-__device__ __forceinline__ uint32_t bf16_rne(float v) {
-    const uint32_t b = __float_as_uint(v);
-    return (b + 0x7fffu + ((b >> 16) & 1u)) >> 16;
-}
-// the hi (hl = 0) or lo (hl = 1) bf16 part of v: v = hi + lo + e, |e| <= 2^-16 |v|
-// (v - hi is exact in fp32)
-__device__ __forceinline__ uint32_t bf16_part(float v, int hl) {
-    const uint32_t hi = bf16_rne(v);
-    return hl ? bf16_rne(v - __uint_as_float(hi << 16)) : hi;
-}
-
 // SPLIT: QT per query block and 16-dim chunk c is [g 4][QR rows][8 bf16]
 // (64 QR bytes, the fp32 chunk's size), g = 2 hl + h holding the hi/lo part
 // of dims 16c + 8h .. +7 of the row: the A fragments of k_screen_m<SPLIT>.
@@ -212,7 +202,7 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const int j = 16 * cc + 8 * (gg & 1) + 2 * e;
-                        wd[e] = bf16_part(tr[row][j], gg >> 1) | (bf16_part(tr[row][j + 1], gg >> 1) << 16);
+                        wd[e] = bf16_split_part(tr[row][j], gg >> 1) | (bf16_split_part(tr[row][j + 1], gg >> 1) << 16);
                     }
                     ((uint4 *)QT)[((int64_t)b * dpad + c0) * QR / 4 + (int64_t)gg * QR + r0 + row] =
                         make_uint4(wd[0], wd[1], wd[2], wd[3]);
@@ -1178,63 +1168,73 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
 // before k_screen, so no item starts unbounded (which would push a whole
 // first block per row through the selection).
 static constexpr int kSeedTiles = 4;
+// One wave per query; the (up to 4) tiles' rows are read from the row-major
+// copy 16 dims at a time, coalesced (a tile's 64 rows are contiguous: lane l
+// loads 16-B pieces of rows l/4 + 16 i), transposed through a per-wave LDS
+// slab [tile][row][17] (odd stride: conflict-free column reads), and lane r
+// accumulates row r of every tile in search.cpp's order.
+static constexpr int kSeedSlab = kSeedTiles * 64 * 17;  // floats per wave
 template <int METRIC>
 __global__ __launch_bounds__(256) void k_seed(const float *Q, const int32_t *probe, int nprobe, int n_lists,
-                                              const int32_t *tile_off, const int32_t *ids, const float *X,
-                                              int64_t d, int64_t dpad, int64_t nq, int k, uint32_t *qbound) {
-    const int lane = threadIdx.x & 63;
-    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+                                              const int32_t *tile_off, const int32_t *ids, const float *Xr,
+                                              int64_t d, int64_t nq, int k, uint32_t *qbound) {
+    __shared__ float slab_all[4][kSeedSlab];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t q = (int64_t)blockIdx.x * 4 + w;
     if (q >= nq) return;
     const int p = probe[q * nprobe];
     if (p < 0 || p >= n_lists) return;
     const int tile0 = tile_off[p], nt = min(kSeedTiles, tile_off[p + 1] - tile0);
+    if (nt <= 0) return;
+    float *slab = slab_all[w];
     const float *qrow = Q + q * d;
-    float m[4] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};  // 4 smallest
-    // all (up to 4) tiles at once, dims outer: 4 loads per dim in flight x 16
-    // dims unrolled; the query's dims come 64 at a time from one coalesced
-    // load (lane j) and are broadcast by readlane.  Each accumulator is its
-    // candidate's own sequential sum (search.cpp order).
-    const float *xt[kSeedTiles];
-#pragma unroll
-    for (int t = 0; t < kSeedTiles; ++t)  // tile layout: dim j of a tile's 64 candidates is one 256-B row
-        xt[t] = X + (int64_t)(tile0 + min(t, nt - 1)) * dpad * kTile + lane;
+    const float *rows = Xr + (int64_t)tile0 * kTile * d;  // the nt tiles' rows, contiguous
+    const bool v4 = (d & 3) == 0;
     float acc[kSeedTiles];
 #pragma unroll
     for (int t = 0; t < kSeedTiles; ++t) acc[t] = 0.0f;
-    for (int64_t j0 = 0; j0 < d; j0 += 64) {
-        const float qv = j0 + lane < d ? qrow[j0 + lane] : 0.0f;
-        const int nj = (int)min<int64_t>(64, d - j0);
-        if (nj == 64) {
-#pragma unroll 16
-            for (int jj = 0; jj < 64; ++jj) {
-                const float qj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qv), jj));
+    for (int64_t j0 = 0; j0 < d; j0 += 16) {
+        const int nj = (int)min<int64_t>(16, d - j0);
+        // stage dims j0 .. j0+nj-1 of the nt x 64 rows
 #pragma unroll
-                for (int t = 0; t < kSeedTiles; ++t) {
-                    const float xv = xt[t][(j0 + jj) * kTile];
-                    if (METRIC == LIRA_METRIC_L2) {
-                        const float df = qj - xv;
-                        acc[t] = acc[t] + df * df;
-                    } else {
-                        acc[t] = acc[t] + qj * xv;
-                    }
+        for (int t = 0; t < kSeedTiles; ++t) {
+            if (t >= nt) break;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = (lane >> 2) + 16 * i, c = 4 * (lane & 3);
+                const float *src = rows + ((int64_t)t * kTile + r) * d + j0 + c;
+                float v[4];
+                if (v4 && c + 4 <= nj) {
+                    const float4 f = *(const float4 *)src;
+                    v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) v[u] = c + u < nj ? src[u] : 0.0f;
                 }
-            }
-        } else {
-            for (int jj = 0; jj < nj; ++jj) {
-                const float qj = __shfl(qv, jj, 64);
 #pragma unroll
-                for (int t = 0; t < kSeedTiles; ++t) {
-                    const float xv = xt[t][(j0 + jj) * kTile];
-                    if (METRIC == LIRA_METRIC_L2) {
-                        const float df = qj - xv;
-                        acc[t] = acc[t] + df * df;
-                    } else {
-                        acc[t] = acc[t] + qj * xv;
-                    }
+                for (int u = 0; u < 4; ++u) slab[(t * 64 + r) * 17 + c + u] = v[u];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        const float qv = lane < nj ? qrow[j0 + lane] : 0.0f;
+        for (int jj = 0; jj < nj; ++jj) {
+            const float qj = __shfl(qv, jj, 64);
+#pragma unroll
+            for (int t = 0; t < kSeedTiles; ++t) {
+                const float xv = slab[(t * 64 + lane) * 17 + jj];
+                if (METRIC == LIRA_METRIC_L2) {
+                    const float df = qj - xv;
+                    acc[t] = acc[t] + df * df;
+                } else {
+                    acc[t] = acc[t] + qj * xv;
                 }
             }
         }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
+    float m[4] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};  // 4 smallest
 #pragma unroll
     for (int u = 0; u < kSeedTiles; ++u) {
         float sc = METRIC == LIRA_METRIC_L2 ? acc[u] : -acc[u];
@@ -1457,29 +1457,21 @@ struct SPlan {
 
 static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k) {
     SPlan pl;
-    static const int mfma_env = [] {
-        const char *e = getenv("LIRA_SCAN_MFMA");  // 0 = VALU screen, 2 = MFMA for every k it supports
-        return e ? atoi(e) : 1;
-    }();
+    const lira_opts &op = idx->opt;
     pl.rl = screen_rl(k);
     // MFMA screen where its LDS (64-query lists) still fits 2 workgroups per
-    // CU; larger k (RL 4: DEEP10M's k = 100) measured faster on the VALU one
-    pl.mfma = mfma_env == 2 ? pl.rl <= 4 : mfma_env && pl.rl <= 2;
+    // CU; larger k (RL 4: DEEP10M's k = 100) measured faster on the VALU one,
+    // which needs the fp32 tiles (without them: MFMA up to RL 4)
+    const int mfma_opt = idx->X ? op.mfma : 2;
+    pl.mfma = mfma_opt == 2 ? pl.rl <= 4 : mfma_opt && pl.rl <= 2;
     // queries per item of the MFMA screen: 64 (4 waves); 128 (8 waves, k <= 56)
     // halves the L2 -> LDS bytes per FMA but measured slower on every config
     // (SIFT1M 1.10 -> 1.25 ms mixture, 4.45 -> 4.66 ms latent; GIST, BIGANN too)
-    static const int qr_env = [] {
-        const char *e = getenv("LIRA_SCAN_QR");
-        return e && atoi(e) == 128 ? 128 : 64;
-    }();
-    pl.qr = pl.mfma ? (pl.rl <= 2 ? qr_env : 64) : screen_qr(pl.rl);
+    const int qr_opt = op.qr == 128 ? 128 : 64;
+    pl.qr = pl.mfma ? (pl.rl <= 2 ? qr_opt : 64) : screen_qr(pl.rl);
     // split-bf16 MFMA screen (k_screen_m<..., SPLIT>) where the index holds Xb;
-    // LIRA_SCAN_SPLIT=0 keeps the fp32 MFMA screen
-    static const int split_env = [] {
-        const char *e = getenv("LIRA_SCAN_SPLIT");
-        return e && e[0] == '0' ? 0 : 1;
-    }();
-    pl.split = split_env && pl.mfma && pl.qr == 64 && idx->Xb != nullptr;
+    // LIRA_OPT_SPLIT = 0 keeps the fp32 MFMA screen (which reads the fp32 tiles)
+    pl.split = (op.split || !idx->X) && pl.mfma && pl.qr == 64 && idx->Xb != nullptr;
     pl.K2 = 32 * pl.rl;
     pl.smem = !pl.mfma       ? screen_smem(pl.qr, pl.rl)
               : pl.qr == 128 ? (pl.rl == 1 ? SSmem<128, 1, true>::total : SSmem<128, 2, true>::total)
@@ -1491,10 +1483,7 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // ~8 items per workgroup: fewer item prologues/epilogues and row lists to
     // merge than k_scan's 16 (measured: SIFT1M scan + merge 1.47 -> 1.22 ms on
     // the mixture, 4.80 -> 4.66 ms on latent data; 4 and 32 slower overall)
-    static const int rounds = [] {
-        const char *e = getenv("LIRA_SCAN_ROUNDS");
-        return e && atoi(e) > 0 ? atoi(e) : 8;
-    }();
+    const int rounds = op.rounds > 0 ? op.rounds : 8;
     const int64_t target = (int64_t)rounds * pl.grid;
     const int64_t est_items = (npairs + pl.qr - 1) / pl.qr + std::min<int64_t>(idx->n_lists, npairs);
     const int64_t max_blocks = std::max<int64_t>(1, (idx->max_list_tiles + kSBT - 1) / kSBT);
@@ -1509,10 +1498,7 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // per workgroup left the slowest workgroup with two (env LIRA_SCAN_NEAR_ROUNDS;
     // measured SIFT1M mixture scan 1.08 -> 1.04 ms at 2, slower at 4 and 8:
     // more lists, more survivors)
-    static const int near_rounds = [] {
-        const char *e = getenv("LIRA_SCAN_NEAR_ROUNDS");
-        return e && atoi(e) > 0 ? atoi(e) : 2;
-    }();
+    const int near_rounds = op.near_rounds > 0 ? op.near_rounds : 2;
     {
         const int64_t est0 = std::min<int64_t>(nq, (nq + pl.qr - 1) / pl.qr + idx->n_lists);
         const int64_t split0 = std::max<int64_t>(1, ((int64_t)near_rounds * pl.grid + est0 - 1) / std::max<int64_t>(1, est0));
@@ -1544,24 +1530,35 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     return pl;
 }
 
+// the screen needs the fp32 tiles (VALU / fp32 MFMA) or the split copy (split
+// MFMA, k <= 120); without the tiles it is the only scan there is
 bool screen_supported(const lira_index *idx, int64_t k) {
-    return screen_rl(k) > 0 && idx->xadj != nullptr && idx->Xr != nullptr && idx->n_lists <= 16384 / 2;
+    if (screen_rl(k) <= 0 || !idx->xadj || !idx->Xr || idx->n_lists > 16384 / 2) return false;
+    return idx->X != nullptr || (idx->Xb != nullptr && screen_rl(k) <= 4);
 }
 
 size_t screen_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k) {
     return make_splan(idx, nq, nprobe, k).total;
 }
 
+// the kernel a screened scan of this shape runs (lira_scan_describe)
+std::string screen_describe(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, unsigned flags) {
+    SPlan pl = make_splan(idx, nq, nprobe, k);
+    if ((flags & LIRA_SCAN_NO_SPLIT) && idx->X) pl.split = 0;
+    std::string s = pl.mfma ? (pl.split ? "k_screen_m split-bf16 v_mfma_f32_16x16x32_bf16"
+                                        : "k_screen_m fp32 v_mfma_f32_16x16x4_f32")
+                            : "k_screen VALU v_pk_fma_f32";
+    s += " RL=" + std::to_string(pl.rl) + " QR=" + std::to_string(pl.qr) + " K2=" + std::to_string(pl.K2) +
+         " grid=" + std::to_string(pl.grid) + " smem=" + std::to_string(pl.smem);
+    return s;
+}
+
 template <int M, int RL, int QR>
 static hipError_t launch_screen(const ScreenArgs &a, const SPlan &pl, hipStream_t st) {
     constexpr int OCC = (160 * 1024) / SSmem<QR, RL>::total >= 2 ? 2 : 1;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void *)k_screen<M, RL, QR, OCC>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
+    static std::atomic<uint64_t> attr{0};
+    hipError_t e = set_smem_attr_once(attr, (const void *)k_screen<M, RL, QR, OCC>, 160 * 1024);
+    if (e != hipSuccess) return e;
     constexpr int smem = SSmem<QR, RL>::total;
     hipLaunchKernelGGL((k_screen<M, RL, QR, OCC>), dim3(pl.grid), dim3(kSThreads), smem, st, a);
     return hipGetLastError();
@@ -1570,13 +1567,9 @@ static hipError_t launch_screen(const ScreenArgs &a, const SPlan &pl, hipStream_
 template <int M, int RL, int QR, bool SPLIT = false>
 static hipError_t launch_screen_m(const ScreenArgs &a, const SPlan &pl, hipStream_t st) {
     constexpr int OCC = (160 * 1024) / SSmem<QR, RL, true>::total >= 2 ? 2 : 1;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void *)k_screen_m<M, RL, QR, OCC, SPLIT>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
+    static std::atomic<uint64_t> attr{0};
+    hipError_t e = set_smem_attr_once(attr, (const void *)k_screen_m<M, RL, QR, OCC, SPLIT>, 160 * 1024);
+    if (e != hipSuccess) return e;
     constexpr int smem = SSmem<QR, RL, true>::total;
     hipLaunchKernelGGL((k_screen_m<M, RL, QR, OCC, SPLIT>), dim3(pl.grid), dim3(QR * 4), smem, st, a);
     return hipGetLastError();
@@ -1624,7 +1617,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     const bool dedup = (flags & LIRA_SCAN_DEDUP) != 0;
     const bool per_part = (flags & LIRA_SCAN_PER_PARTITION) != 0;
     SPlan pl = make_splan(idx, nq, nprobe, k);
-    if (flags & LIRA_SCAN_NO_SPLIT) pl.split = 0;
+    if ((flags & LIRA_SCAN_NO_SPLIT) && idx->X) pl.split = 0;  // (no tiles: the split copy is the only one)
     if (!ws) {
         if (idx->ws_bytes < pl.total) {
             if (idx->ws) hipFree(idx->ws);
@@ -1666,20 +1659,14 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     // BIGANN-100M mixture scan 66 -> 16 ms; GIST1M's 1k queries, 2 blocks per
     // partition, latent data: 3.2 -> 3.7 ms, so not there).
     // LIRA_SCAN_TWO_PHASE: 0 off, 2 always, 1 (default) this rule.
-    static const int groups_env = [] {
-        const char *e = getenv("LIRA_SCAN_TWO_PHASE");
-        return e ? atoi(e) : 1;
-    }();
+    const lira_opts &o = idx->opt;
+    const int groups_env = o.two_phase;
     const bool fill = nq >= (int64_t)pl.qr * idx->n_lists || nq * nprobe >= 4 * (int64_t)pl.qr * idx->n_lists;
     const int groups = qbound && groups_env && nprobe >= 2 && (groups_env == 2 || fill) ? 2 : 1;
     const int nvirt = groups * (int)idx->n_lists;
     LIRA_HIP_TRY(launch_plan(idx, probe, npairs, (int)nprobe, pl.bpc, groups == 2 ? pl.bpc_near : pl.bpc, pl.qr, groups, cnt, cursor, qoff, item_off,
                              nch, head, qlist, qblk, itab, st));
-    static const int tri_env = [] {
-        const char *e = getenv("LIRA_SCAN_PRUNE");
-        return e && e[0] == '0' ? 0 : 1;
-    }();
-    const bool tri = tri_env && !(flags & LIRA_SCAN_NO_PRUNE) && pl.mfma && idx->pivot;
+    const bool tri = o.prune && !(flags & LIRA_SCAN_NO_PRUNE) && pl.mfma && idx->pivot;
     const float *tri_pivot = tri ? idx->pivot : nullptr;
     if (pl.qr == 128)
         hipLaunchKernelGGL((k_qstage<128, false>), dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
@@ -1694,18 +1681,15 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
         hipLaunchKernelGGL((k_qstage<32, false>), dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
                            (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, QT, QN);
     LIRA_HIP_TRY(hipGetLastError());
-    static const int seed_env = [] {
-        const char *e = getenv("LIRA_SCAN_SEED");  // measured: SIFT1M mixture 1.70 -> 1.44 ms, latent +1 %
-        return e && e[0] == '0' ? 0 : 1;
-    }();
-    if (qbound && seed_env) {
+    // (measured: SIFT1M mixture 1.70 -> 1.44 ms, latent +1 %)
+    if (qbound && o.seed) {
         if (idx->metric == LIRA_METRIC_L2)
             hipLaunchKernelGGL(k_seed<LIRA_METRIC_L2>, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, q, probe,
-                               (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq,
+                               (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->Xr, idx->d, nq,
                                (int)k, qbound);
         else
             hipLaunchKernelGGL(k_seed<LIRA_METRIC_IP>, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, q, probe,
-                               (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq,
+                               (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->Xr, idx->d, nq,
                                (int)k, qbound);
         LIRA_HIP_TRY(hipGetLastError());
     }
@@ -1715,21 +1699,8 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     a.Q = q;
     a.pivot = tri ? idx->pivot : nullptr;
     a.tstat = tri ? idx->tstat : nullptr;
-    static const int dbg_env = [] {
-        const char *e = getenv("LIRA_SCAN_DEBUG");
-        return e ? atoi(e) : 0;
-    }();
-    a.dbg = dbg_env;
-    static const int flush_env = [] {
-        const char *e = getenv("LIRA_SCAN_FLUSH");
-        return e && atoi(e) >= 1 && atoi(e) <= 32 ? atoi(e) : 32;
-    }();
-    static const int share_env = [] {
-        const char *e = getenv("LIRA_SCAN_SHARE");
-        return e ? atoi(e) : 1;
-    }();
-    a.flush_at = flush_env;
-    a.share = share_env;
+    a.dbg = o.debug;
+    a.share = o.share;
     a.split = pl.split;
     a.X = pl.split ? (const float *)idx->Xb : idx->X;
     a.xadj = idx->xadj;

@@ -23,6 +23,9 @@ LIRA_SCAN_FMA = 4
 LIRA_SCAN_NO_PRUNE = 8
 LIRA_SCAN_EXACT = 16
 LIRA_SCAN_NO_SPLIT = 32
+# lira_index_set_option keys (include/lira_hip.h LIRA_OPT_*)
+OPTIONS = {"keep_tiles": 1, "screen": 2, "split": 3, "qr": 4, "two_phase": 5, "prune": 6, "seed": 7,
+           "share": 8, "rounds": 9, "near_rounds": 10, "mfma": 11, "debug": 12}
 LIRA_PROBE_NEAREST = 0
 LIRA_PROBE_THRESHOLD_GE = 1
 LIRA_PROBE_THRESHOLD_GT = 2
@@ -56,6 +59,9 @@ SIGNATURES = {
                                ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I64)]),
     "lira_index_list_size": (_INT, [_P, _I64, ctypes.POINTER(_I64)]),
     "lira_index_memory": (_INT, [_P, ctypes.POINTER(_I64)]),
+    "lira_index_set_option": (_INT, [_P, _INT, _I64]),
+    "lira_index_get_option": (_INT, [_P, _INT, ctypes.POINTER(_I64)]),
+    "lira_index_has_tiles": (_INT, [_P, ctypes.POINTER(_INT)]),
     "lira_centroid_dist": (_INT, [_P, _I64, _P, _I64, _I64, _P, _P, _P, _P]),
     "lira_centroid_gemm": (_INT, [_P, _I64, _P, _I64, _I64, _P, _P, _P]),
     "lira_rank_workspace_size": (_INT, [_I64, _I64, ctypes.POINTER(_SZ)]),
@@ -63,6 +69,7 @@ SIGNATURES = {
     "lira_select_probes": (_INT, [_P, _I64, _I64, _INT, _F, _I64, _P, _P, _P]),
     "lira_scan_workspace_size": (_INT, [_P, _I64, _I64, _I64, ctypes.c_uint, ctypes.POINTER(_SZ)]),
     "lira_scan_topk": (_INT, [_P, _P, _I64, _P, _I64, _I64, ctypes.c_uint, _P, _P, _P, _P, _SZ, _P]),
+    "lira_scan_describe": (_INT, [_P, _I64, _I64, _I64, ctypes.c_uint, ctypes.c_char_p, _SZ]),
     "lira_index_check": (_INT, [_P, _P]),
     "lira_index_set_profiling": (_INT, [_P, _INT]),
     "lira_index_set_stats": (_INT, [_P, _INT]),

@@ -44,9 +44,12 @@ def all_gather_rows(t: torch.Tensor, n_total: int, world: int, group=None) -> to
     return torch.cat(out)
 
 
-def sharded_search(search_fn, q_all: torch.Tensor, group=None):
+def sharded_search(search_fn, q_all: torch.Tensor, group=None, gather_device=None):
     """Run `search_fn(q_slice, start) -> (D, I)` on this rank's slice of q_all
-    (rows start .. start + len) and return the whole batch's (D, I) on every rank."""
+    (rows start .. start + len) and return the whole batch's (D, I) on every rank.
+
+    The gather runs on the result tensors' device (RCCL for GPU tensors under
+    the "nccl" backend) or on ``gather_device`` (e.g. "cpu" under gloo)."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     n = q_all.shape[0]
@@ -54,4 +57,6 @@ def sharded_search(search_fn, q_all: torch.Tensor, group=None):
     D, I = search_fn(q_all[s:e], s)
     if world == 1:
         return D, I
+    if gather_device is not None:
+        D, I = D.to(gather_device), I.to(gather_device)
     return all_gather_rows(D, n, world, group), all_gather_rows(I, n, world, group)

@@ -64,10 +64,14 @@ class PartitionedIndex:
     """Inverted lists of fp32 vectors on one GPU, searched by the HIP scan.
 
     Parameters mirror search.cpp's Args (search.cpp:18-31): d, metric
-    ("L2" | "inner_product").
+    ("L2" | "inner_product").  ``options`` are per-index tuning knobs
+    (include/lira_hip.h LIRA_OPT_*: keep_tiles, split, qr, ...); none changes a
+    result.  ``keep_tiles=False`` drops the fp32 tile copy (2 instead of 3
+    copies of the data in HBM; the all-exact scan is then unavailable).
     """
 
-    def __init__(self, d: int, metric: str = "L2", device: int | torch.device | None = None):
+    def __init__(self, d: int, metric: str = "L2", device: int | torch.device | None = None,
+                 **options):
         self.d = int(d)
         self.metric = normalize_metric(metric)
         if device is None:
@@ -77,6 +81,8 @@ class PartitionedIndex:
         _lib.call("lira_index_create", self.device.index, self.d, METRICS[self.metric],
                   ctypes.byref(h))
         self._h = h
+        for name, value in options.items():
+            self.set_option(name, value)
         self.n_lists = 0
         self.ntotal = 0
         self.list_sizes = np.zeros(0, dtype=np.int64)
@@ -156,13 +162,13 @@ class PartitionedIndex:
         return out
 
     @classmethod
-    def from_assignment(cls, x_d, data_2_bkt, n_bkt: int, metric: str = "L2", device=None):
+    def from_assignment(cls, x_d, data_2_bkt, n_bkt: int, metric: str = "L2", device=None, **options):
         """search.cpp:366-404: lists from data_2_bkt (N, n_mul) over base vectors x_d."""
-        idx = cls(x_d.shape[1], metric, device)
+        idx = cls(x_d.shape[1], metric, device, **options)
         return idx.build(data_2_bkt, x_d, n_bkt)
 
     @classmethod
-    def from_cluster_ids(cls, x_d, cluster_ids, metric: str = "L2", device=None):
+    def from_cluster_ids(cls, x_d, cluster_ids, metric: str = "L2", device=None, **options):
         """From LIRA's ``cluster_ids`` (list of per-bucket id lists, utils.py:327-329)."""
         sizes = np.array([len(c) for c in cluster_ids], dtype=np.int64)
         offsets = np.zeros(len(cluster_ids) + 1, dtype=np.int64)
@@ -170,7 +176,7 @@ class PartitionedIndex:
         flat = np.concatenate([np.asarray(c, dtype=np.int64) for c in cluster_ids]) \
             if offsets[-1] else np.zeros(0, dtype=np.int64)
         rep = int(np.bincount(flat).max()) if flat.size else 1
-        idx = cls(x_d.shape[1], metric, device)
+        idx = cls(x_d.shape[1], metric, device, **options)
         idx.add_lists(offsets, torch.from_numpy(flat.astype(np.int32)), x_d, rep)
         return idx
 
@@ -225,6 +231,13 @@ class PartitionedIndex:
                       _lib.stream_ptr(stream))
         return D, I, ncand
 
+    def describe(self, nq: int, nprobe: int, k: int, dedup: bool = True, exact: bool = False) -> str:
+        """The scan kernel a search of this shape runs (lira_scan_describe)."""
+        flags = (_lib.LIRA_SCAN_DEDUP if dedup else 0) | (_lib.LIRA_SCAN_EXACT if exact else 0)
+        buf = ctypes.create_string_buffer(256)
+        _lib.call("lira_scan_describe", self._h, int(nq), int(nprobe), int(k), flags, buf, 256)
+        return buf.value.decode()
+
     def check(self, stream=None):
         """Raise if the last searches hit an out-of-range probe id."""
         with torch.cuda.device(self.device):
@@ -256,6 +269,24 @@ class PartitionedIndex:
             _lib.call("lira_index_stats_read", self._h, v)
         return {"chunks_computed": v[0], "chunks_nominal": v[1], "blocks": v[2], "blocks_dropped": v[3],
                 "blocks_skipped": v[4], "rechecked": v[5], "rescans": v[6], "survivors": v[7]}
+
+    def set_option(self, name: str, value) -> None:
+        """Set one LIRA_OPT_* knob by name (see include/lira_hip.h)."""
+        if name not in _lib.OPTIONS:
+            raise ValueError(f"unknown option {name!r}: one of {sorted(_lib.OPTIONS)}")
+        _lib.call("lira_index_set_option", self._h, _lib.OPTIONS[name], int(value))
+
+    def get_option(self, name: str) -> int:
+        v = ctypes.c_int64()
+        _lib.call("lira_index_get_option", self._h, _lib.OPTIONS[name], ctypes.byref(v))
+        return v.value
+
+    @property
+    def has_tiles(self) -> bool:
+        """True if the fp32 tile copy (all-exact scan) is resident."""
+        v = ctypes.c_int()
+        _lib.call("lira_index_has_tiles", self._h, ctypes.byref(v))
+        return bool(v.value)
 
     def memory_bytes(self) -> int:
         v = ctypes.c_int64()

@@ -2,7 +2,7 @@
 
 Two distributions, both fp32:
 
-* ``latent`` (the bench default): x = z A + 0.1 * N(0,1)^d with z ~ N(0,1)^m,
+* ``latent``: x = z A + 0.1 * N(0,1)^d with z ~ N(0,1)^m,
   A a fixed random m x d basis / sqrt(m) -- full-rank vectors of low intrinsic
   dimension m, like real descriptors.  Partitions come from k-means over the
   data (``lira_amd.knn.Kmeans``, as utils.py:321-330 does with faiss), so their
@@ -14,8 +14,9 @@ Two distributions, both fp32:
 * ``mixture``: B centres ~ N(0,1)^d, point = centre[uniform label] +
   sigma * N(0,1)^d (sigma = 0.35), nearest-centre partitions.  In high d these
   clusters are perfectly separated (recall 1.0 at any nprobe >= 1), so exact
-  pruning skips nearly every non-nearest partition: an easy best case, kept
-  for tests and as a contrast, never the headline.
+  pruning skips nearly every non-nearest partition: an easy best case.  It is
+  SURVEY.md 8(d)'s prescribed distribution, so bench.py's headline uses it
+  and reports the ``latent`` run beside it (``contrast_data``).
 """
 from __future__ import annotations
 
@@ -29,6 +30,10 @@ CONFIGS = {
     "deep10m": (10_000_000, 96, 256, 32, 100, "inner_product", 10_000),
     "bigann100m": (100_000_000, 128, 1024, 32, 10, "L2", 10_000),
 }
+# buckets per base row: LIRA_largescale.py's full redundancy (n_mul = 2,
+# LIRA_largescale.py:37-39) for the BIGANN-100M path, here each row's n_mul
+# nearest centroids; 1 (plain partitions) elsewhere
+N_MUL = {"bigann100m": 2}
 # intrinsic dimension of the ``latent`` distribution per config (see above)
 LATENT_DIM = {"sift1m": 12, "gist1m": 16, "deep10m": 20, "bigann100m": 12}
 NORMALISED = {"deep10m"}
@@ -90,28 +95,41 @@ def latent_torch(n, basis, seed, device, noise=0.1, normalise=False, chunk=1 << 
     return x
 
 
-def workload(config: str, seed: int, device, data: str = "latent", n_override=None, kmeans_iter: int = 10):
-    """(x, centroids, assignment (N,) int32, make_queries(nq, seed)) for a config.
+def nearest_m(x: torch.Tensor, centres: torch.Tensor, m: int, chunk=1 << 20) -> torch.Tensor:
+    """(N, m) int32: each row's m nearest centres by search.cpp's exact distance
+    (lira_rank_nearest; ties -> smaller id) -- the data_2_bkt of n_mul = m."""
+    from .index import RankWorkspace, rank_nearest
+    out = torch.empty((x.shape[0], m), dtype=torch.int32, device=x.device)
+    ws = RankWorkspace(min(chunk, x.shape[0]), centres.shape[0], x.device)
+    for s in range(0, x.shape[0], chunk):
+        rank_nearest(x[s:s + chunk], centres, m, out=out[s:s + chunk], workspace=ws)
+    return out
 
+
+def workload(config: str, seed: int, device, data: str = "latent", n_override=None, kmeans_iter: int = 10):
+    """(x, centroids, assignment, make_queries(nq, seed)) for a config.
+
+    assignment: (N,) int32, or (N, n_mul) for the configs of N_MUL.
     ``latent``: k-means centroids (lira_amd.knn.Kmeans, subsample of 256 points
     per centroid as faiss) and exact nearest-centroid assignment.
     ``mixture``: generating centres and nearest-centre assignment."""
     N, d, B, _, _, _, _ = CONFIGS[config]
     N = n_override or N
+    n_mul = N_MUL.get(config, 1)
     if data == "mixture":
         x, c = mixture_torch(N, d, B, seed, device)
-        return x, c, nearest_centre(x, c), lambda nq, s: mixture_torch(nq, d, B, s, device, centres=c)[0]
+        assign = nearest_centre(x, c) if n_mul == 1 else nearest_m(x, c, n_mul)
+        return x, c, assign, lambda nq, s: mixture_torch(nq, d, B, s, device, centres=c)[0]
     if data != "latent":
         raise ValueError(f"unknown synthetic distribution {data!r}")
     from .knn import Kmeans
-    from .index import rank_nearest
     basis = latent_basis(d, LATENT_DIM[config], seed, device)
     norm = config in NORMALISED
     x = latent_torch(N, basis, seed + 1, device, normalise=norm)
     km = Kmeans(d, B, niter=kmeans_iter, seed=seed, device=device.index)
     km.train(x)
     c = torch.from_numpy(km.centroids).to(device)
-    assign = torch.empty(N, dtype=torch.int32, device=device)
-    for s in range(0, N, 1 << 22):
-        assign[s:s + (1 << 22)] = rank_nearest(x[s:s + (1 << 22)], c, 1)[:, 0]
+    assign = nearest_m(x, c, n_mul)
+    if n_mul == 1:
+        assign = assign[:, 0]
     return x, c, assign, lambda nq, s: latent_torch(nq, basis, s, device, normalise=norm)

@@ -162,6 +162,47 @@ def scan_topk(q, offsets, ids, vecs, probe, k, metric=L2, dedup=0):
     return D, I, nc
 
 
+def scan_topk_sampled(q, probe, list_ids, gather, k, metric=L2, dedup=0, threads=8):
+    """scan_topk of each query over its own probed lists only (a per-query
+    sub-CSR), for indexes too large to copy to the host whole.
+
+    q (n, d) and probe (n, nprobe) host arrays; list_ids(b) -> the bucket's
+    ids (int32, list order); gather(ids) -> their vectors (host fp32 array).
+    Inputs are prepared one query at a time in the calling thread (gather is
+    called per bucket, so the caller's device memory holds one list at a
+    time) and scanned by `threads` worker threads (the C call releases the
+    GIL), at most 2 x threads queries in flight.  Returns (D, I)."""
+    import threading
+    from concurrent.futures import ThreadPoolExecutor
+    q = _c(q, np.float32)
+    probe = np.asarray(probe)
+    gate = threading.Semaphore(2 * max(1, threads))
+
+    def run(args):
+        try:
+            qi, off, ids, vecs, sub = args
+            D, I, _ = scan_topk(qi, off, ids, vecs, sub, k, metric, dedup)
+            return D[0], I[0]
+        finally:
+            gate.release()
+
+    futs = []
+    with ThreadPoolExecutor(max(1, threads)) as ex:
+        for i in range(q.shape[0]):
+            bs = [int(b) for b in probe[i] if b >= 0]
+            ls = [np.asarray(list_ids(b), dtype=np.int32) for b in bs]
+            off = np.zeros(len(ls) + 1, dtype=np.int64)
+            off[1:] = np.cumsum([len(l) for l in ls])
+            ids = np.concatenate(ls) if ls else np.zeros(0, np.int32)
+            vecs = np.concatenate([gather(l) for l in ls]) if ls else np.zeros((0, q.shape[1]), np.float32)
+            gate.acquire()
+            futs.append(ex.submit(run, (q[i:i + 1], off, ids, vecs, np.arange(len(ls), dtype=np.int32)[None, :])))
+        res = [f.result() for f in futs]
+    if not res:
+        return np.zeros((0, k), np.float32), np.zeros((0, k), np.int64)
+    return np.stack([r[0] for r in res]), np.stack([r[1] for r in res])
+
+
 def scan_per_partition(q, offsets, ids, vecs, probe, k, metric=L2):
     """LIRA_smallscale.py:145-174: k best per probed bucket, (nq, nprobe, k)."""
     q = _c(q, np.float32)

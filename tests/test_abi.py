@@ -62,6 +62,17 @@ def test_abi_version_and_errors(lib):
     assert lib.lira_rank_nearest(None, 1, None, 64, 16, 0, None, None, 0, None) == -6
     assert lib.lira_select_probes(None, 1, 8, 9, 0.0, 4, None, None, None) == -1
     assert lib.lira_centroid_dist(None, 4, None, 8, 16, None, ctypes.c_void_p(1), None, None) == -1
+    v = ctypes.c_int64()
+    assert lib.lira_index_set_option(None, 1, 0) == -1
+    assert lib.lira_index_get_option(None, 1, ctypes.byref(v)) == -1
+    assert lib.lira_index_has_tiles(None, ctypes.byref(ctypes.c_int())) == -1
+
+
+def test_option_names_match_header():
+    from lira_amd import _lib
+    txt = open(HEADER).read()
+    keys = dict((m.lower(), int(v)) for m, v in re.findall(r"#define LIRA_OPT_([A-Z_]+) (\d+)", txt))
+    assert keys == _lib.OPTIONS
 
 
 def test_python_error_mapping(lib):

@@ -16,10 +16,10 @@ def bits(a):
     return np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
 
 
-def make_index(x, d2b, n_bkt, metric):
+def make_index(x, d2b, n_bkt, metric, **options):
     from lira_amd import PartitionedIndex
     return PartitionedIndex.from_assignment(torch.from_numpy(x).cuda(), torch.from_numpy(d2b).cuda(),
-                                            n_bkt, metric)
+                                            n_bkt, metric, **options)
 
 
 def run(idx, q, probe, k, **kw):
@@ -78,6 +78,14 @@ def check_vs_oracle(x, q, d2b, probe, b, k, metric, dedup=True):
         D, I, nc = run(idx, q, probe, k, dedup=dedup, exact=exact, split=split)
         assert np.array_equal(I, Io), f"ids differ (exact={exact}, split={split})"
         assert np.array_equal(bits(D), bits(Do)), f"distances differ (exact={exact}, split={split})"
+        assert np.array_equal(nc, nco)
+    if k <= 120:
+        # the compact index (no fp32 tiles: row-major + split-bf16 copies only)
+        idc = make_index(x, d2b, b, metric, keep_tiles=False)
+        assert not idc.has_tiles and idc.memory_bytes() < idx.memory_bytes()
+        D, I, nc = run(idc, q, probe, k, dedup=dedup)
+        assert np.array_equal(I, Io), "ids differ (compact index)"
+        assert np.array_equal(bits(D), bits(Do)), "distances differ (compact index)"
         assert np.array_equal(nc, nco)
     return idx
 
@@ -315,3 +323,58 @@ def test_screen_duplicate_rows_force_exact_rescan(metric):
     Dq, Iq = oracle.scan_per_partition(q, off, ids, oracle.gather_lists(x, off, ids), probe, 10, met)
     D, I, _ = run(idx2, q, probe, 10, per_partition=True, dedup=False)
     assert np.array_equal(I, Iq) and np.array_equal(bits(D), bits(Dq))
+
+
+def test_compact_index_refuses_tile_paths():
+    from lira_amd import LiraError
+    x, q, d2b, probe = random_case(11, 3000, 24, 6, 20, 3, "L2")
+    idc = make_index(x, d2b, 6, "L2", keep_tiles=False)
+    assert idc.get_option("keep_tiles") == 0
+    for kw in ({"exact": True}, {"fma": True}):
+        with pytest.raises(LiraError, match="EUNSUPPORTED"):
+            run(idc, q, probe, 10, **kw)
+    with pytest.raises(LiraError, match="EUNSUPPORTED"):
+        run(idc, q, probe, 121)
+    idc.set_profiling(True)  # a refused call leaves no half-recorded events behind
+    with pytest.raises(LiraError):
+        run(idc, q, probe, 10, exact=True)
+    run(idc, q, probe, 10)
+    assert idc.profile_read()["calls"] == 1
+    with pytest.raises(LiraError, match="EINVAL"):
+        idc.set_option("qr", 96)
+
+
+@pytest.mark.parametrize("metric", ["L2", "inner_product"])
+def test_options_do_not_change_results(metric):
+    x, q, d2b, probe = clustered_case(61, 20000, 48, 8, 700, 3)
+    idx = make_index(x, d2b, 8, metric)
+    ref = run(idx, q, probe, 10)
+    for name, vals in (("qr", (128,)), ("two_phase", (0, 2)), ("seed", (0,)), ("share", (0,)),
+                       ("prune", (0,)), ("split", (0,)), ("mfma", (0, 2)), ("rounds", (1, 64)),
+                       ("near_rounds", (8,)), ("screen", (0,))):
+        old = idx.get_option(name)
+        for v in vals:
+            idx.set_option(name, v)
+            D, I, nc = run(idx, q, probe, 10)
+            assert np.array_equal(I, ref[1]) and np.array_equal(bits(D), bits(ref[0])), (name, v)
+        idx.set_option(name, old)
+
+
+@pytest.mark.parametrize("metric", ["L2", "inner_product"])
+def test_split_screen_extreme_values(metric):
+    # split-bf16 parts of values near FLT_MAX (the hi part saturates to the
+    # largest finite bf16 instead of rounding to infinity) and of subnormals
+    rng = np.random.default_rng(71)
+    n, d, b = 4000, 16, 4
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    q = rng.standard_normal((40, d)).astype(np.float32)
+    if metric == "inner_product":
+        big = rng.random(n) < 0.05
+        x[big, 3] = np.float32(3.399e38) * np.sign(rng.standard_normal(big.sum())).astype(np.float32)
+        q *= np.float32(1e-3)
+    tiny = rng.random(n) < 0.05
+    x[tiny] *= np.float32(1e-40)
+    q[:5] *= np.float32(1e-39)
+    d2b = rng.integers(0, b, (n, 1)).astype(np.int32)
+    probe = np.tile(np.arange(b, dtype=np.int32), (q.shape[0], 1))
+    check_vs_oracle(x, q, d2b, probe, b, 10, metric)

@@ -1,10 +1,11 @@
 #!/bin/bash
-# Same-box sweep: tools/ab_env.sh <config> <variant> VAR v1 v2 ...  (bench per value of env VAR)
-cfg=$1; v=$2; var=$3; shift 3
+# Same-box sweep of one index option (include/lira_hip.h LIRA_OPT_*):
+#   tools/ab_env.sh <config> <data> <option> v1 v2 ...
+cfg=$1; data=$2; opt=$3; shift 3
 mkdir -p gpurun_out
 for val in "$@"; do
-  env "$var=$val" LIRA_HIP_LIB=variants/$v.so timeout -k 10 150 python bench.py --config "$cfg" --steps 20 --warmup 3 \
-      --no-cpu-baseline > gpurun_out/abenv.log 2>&1 || { echo "$v $var=$val failed"; tail -5 gpurun_out/abenv.log; exit 1; }
-  python3 -c "import json; j=json.loads(open('gpurun_out/abenv.log').read().strip().splitlines()[-1]); \
-print('$cfg $v $var=$val', 'qps %.0f scan_ms %.3f merge_ms %.3f exact %s' % (j['value'], j['kernels_ms_per_step']['scan'], j['kernels_ms_per_step']['merge'], j['parity_bit_exact']))" | tee -a gpurun_out/ab.txt
+  timeout -k 10 200 python bench.py --config "$cfg" --data "$data" --steps 20 --warmup 3 --no-cpu-baseline \
+      --no-exact --contrast none --opt "$opt=$val" $BENCH_ARGS > gpurun_out/abenv.log 2>&1 || { echo "$opt=$val failed"; tail -5 gpurun_out/abenv.log; exit 1; }
+  python3 -c "import json; j=json.loads(open('gpurun_out/abenv.log').read().strip().splitlines()[-1]); k=j['kernels_ms_per_step']; \
+print('$cfg/$data $opt=$val', 'qps %.0f scan %.3f merge %.3f plan %.3f exact %s' % (j['value'], k['scan'], k['merge'], k['plan'], j['parity_bit_exact']))" | tee -a gpurun_out/ab.txt
 done

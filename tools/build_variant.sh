@@ -1,15 +1,20 @@
 #!/bin/bash
-# Build liblira_hip.so with an alternative lira_scan.hip into variants/<name>.so
-# (for same-box A/B timing via LIRA_HIP_LIB=variants/<name>.so).
+# Build liblira_hip.so with one csrc file replaced into variants/<name>.so (for
+# same-box A/B timing via tools/ab.sh):  tools/build_variant.sh <csrc name> <alt source> <name>
+#   e.g. tools/build_variant.sh lira_screen.hip /tmp/screen_qr128.hip qr128
 set -e
-src=$1; name=$2
+file=$1; src=$2; name=$3
 root=$(cd "$(dirname "$0")/.." && pwd)
 pkg=$root/lira-ann-search_amd
+make -s -C "$pkg"
 mkdir -p "$root/variants/obj_$name"
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -I$root/include -I$pkg/csrc"
-cp "$src" "$pkg/csrc/_variant_scan.hip"
-/opt/rocm/bin/hipcc $F -c "$pkg/csrc/_variant_scan.hip" -o "$root/variants/obj_$name/scan.o"
-rm -f "$pkg/csrc/_variant_scan.hip"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC "$pkg/build/lira_abi.o" "$root/variants/obj_$name/scan.o" \
-    "$pkg/build/lira_rank.o" "$pkg/build/lira_build.o" -o "$root/variants/$name.so"
+cp "$src" "$pkg/csrc/_variant.hip"
+/opt/rocm/bin/hipcc $F -c "$pkg/csrc/_variant.hip" -o "$root/variants/obj_$name/variant.o"
+rm -f "$pkg/csrc/_variant.hip"
+objs=""
+for o in "$pkg"/build/*.o; do
+  [ "$(basename "$o" .o).hip" = "$file" ] || objs="$objs $o"
+done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $objs "$root/variants/obj_$name/variant.o" -o "$root/variants/$name.so"
 echo "built variants/$name.so"

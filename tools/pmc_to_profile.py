@@ -1,7 +1,10 @@
-"""Turn a tools/profile_box.sh summary into the per-config record bench.py
-reads (profiles/pmc_scan_<config>.json) and copy the evidence into profiles/.
+"""Turn a tools/profile_box.sh summary into the per-(config, data) record
+bench.py reads (profiles/pmc_scan_<config>_<data>.json) and copy the evidence
+into profiles/.  The record names the scan kernel and plan (lira_scan_describe,
+from the profiled bench's own JSON line) and the batch size, so bench.py uses
+it only for the same kernel on the same shape.
 
-usage: python tools/pmc_to_profile.py <config> <gpurun_out/prof_TAG> <round tag, e.g. r01>
+usage: python tools/pmc_to_profile.py <config> <data> <gpurun_out/prof_DIR> <round tag, e.g. r02>
 """
 import json
 import os
@@ -12,13 +15,22 @@ WORKLOADS = {
     "sift1m": "sift1m (N=1M d=128 B=64 nprobe=8 k=10 L2, 10k queries)",
     "gist1m": "gist1m (N=1M d=960 B=128 nprobe=16 k=10 L2, 1k queries)",
     "deep10m": "deep10m (N=10M d=96 B=256 nprobe=32 k=100 IP, 10k queries)",
-    "bigann100m": "bigann100m (N=100M d=128 B=1024 nprobe=32 k=10 L2, 10k queries)",
+    "bigann100m": "bigann100m (N=100M n_mul=2 d=128 B=1024 nprobe=32 k=10 L2, 10k queries)",
 }
 
 
-def main(cfg, src, tag):
+def bench_line(path):
+    for line in open(path):
+        line = line.strip()
+        if line.startswith("{") and '"metric"' in line:
+            return json.loads(line)
+    return {}
+
+
+def main(cfg, data, src, tag):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     summ = json.load(open(os.path.join(src, "summary.json")))
+    bl = bench_line(os.path.join(src, "trace.log"))
     # the default path's scan kernel (screened: k_screen_m / k_screen), else the
     # all-exact k_scan; the one with the most total time
     scan = [(k, v) for k, v in summ.items() if k.startswith("lira::k_screen")] or \
@@ -30,27 +42,32 @@ def main(cfg, src, tag):
     p = e.get("pmc", {})
     rec = {
         "kernel": name,
-        "workload": WORKLOADS.get(cfg, cfg),
+        "kernel_desc": bl.get("kernel"),
+        "nq": (bl.get("config") or {}).get("queries_per_rank"),
+        "workload": WORKLOADS.get(cfg, cfg) + f", {data} data",
         "hbm_bytes_per_launch": e.get("hbm_bytes_per_launch"),
         "avg_ns_trace": e.get("trace", {}).get("avg_ns"),
+        "bench_kernel_ms": ((bl.get("roofline") or {}).get("kernel_ms")),
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes with "
                   "--kernel-trace; bytes = (2*FETCH_SIZE + WRITE_SIZE) KiB (gfx950 FETCH_SIZE "
                   "counts half of 16-B/lane streaming reads incl. LDS-DMA loads, "
                   "MI355X_MICROARCH.md HBM section)",
         "FETCH_SIZE_KiB": p.get("FETCH_SIZE"),
         "WRITE_SIZE_KiB": p.get("WRITE_SIZE"),
-        "SQ_INSTS_VALU": p.get("SQ_INSTS_VALU"),
+        "mfma_busy_pct": e.get("mfma_busy_pct"),
+        "valu_busy_pct": e.get("valu_busy_pct"),
         "wave_cycle_split": e.get("wave_cycle_split"),
-        "source": f"profiles/{tag}_{cfg}_pmc_summary.json",
+        "lds_bank_conflicts": p.get("SQ_LDS_BANK_CONFLICT"),
+        "source": f"profiles/{tag}_{cfg}_{data}_pmc_summary.json",
     }
     out = os.path.join(root, "profiles")
-    json.dump(rec, open(os.path.join(out, f"pmc_scan_{cfg}.json"), "w"), indent=1)
-    shutil.copy(os.path.join(src, "summary.json"), os.path.join(out, f"{tag}_{cfg}_pmc_summary.json"))
+    json.dump(rec, open(os.path.join(out, f"pmc_scan_{cfg}_{data}.json"), "w"), indent=1)
+    shutil.copy(os.path.join(src, "summary.json"), os.path.join(out, f"{tag}_{cfg}_{data}_pmc_summary.json"))
     st = os.path.join(src, "trace", "run_kernel_stats.csv")
     if os.path.exists(st):
-        shutil.copy(st, os.path.join(out, f"{tag}_{cfg}_kernel_stats.csv"))
+        shutil.copy(st, os.path.join(out, f"{tag}_{cfg}_{data}_kernel_stats.csv"))
     print(json.dumps(rec, indent=1))
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])

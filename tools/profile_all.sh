@@ -1,9 +1,10 @@
 #!/bin/bash
-# On the GPU box: rocprof evidence for each config (tools/profile_box.sh), then
-# the default bench with its CPU baseline.  usage: tools/profile_all.sh <tag> cfg...
+# On the GPU box: rocprof evidence for configs x distributions
+# (tools/profile_box.sh).  usage: tools/profile_all.sh <tag> cfg:data[:passes] ...
 set -euo pipefail
 TAG=$1; shift
-for cfg in "$@"; do
-  bash tools/profile_box.sh "${TAG}_$cfg" --config "$cfg" > /dev/null
-  echo "profiled $cfg"
+for spec in "$@"; do
+  IFS=: read -r cfg data passes <<< "$spec"
+  bash tools/profile_box.sh "$TAG" "$cfg" "$data" "${passes:-all}" > /dev/null
+  echo "profiled $cfg/$data"
 done
