@@ -156,6 +156,30 @@ __global__ __launch_bounds__(256) void k_row_norms(const float *Xr, const int32_
     if (lane == 0 && r > 0.0f) atomicMax((unsigned int *)&rmax[tile_list[t]], __float_as_uint(r));
 }
 
+// Centred screening constants (L2, for the split-bf16 copy): per row
+// xadjc = fl(||fl(x - c)||^2) / 2 and the list's rmaxc >= max ||fl(x - c)||,
+// c = the list's pivot, fl(x - c) exactly the fp32 values k_split_rows splits.
+__global__ __launch_bounds__(256) void k_row_norms_c(const float *Xr, const int32_t *ids, int64_t d,
+                                                     const int32_t *tile_list, const float *pivot, int64_t n_tiles,
+                                                     float *xadjc, float *rmaxc) {
+    const int lane = threadIdx.x & 63;
+    const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= n_tiles) return;
+    const float *x = Xr + (t * kTile + lane) * d;
+    const float *pv = pivot + (int64_t)tile_list[t] * d;
+    double s = 0.0;
+    for (int64_t j = 0; j < d; ++j) {
+        const double v = (double)(x[j] - pv[j]);
+        s = __builtin_fma(v, v, s);
+    }
+    const bool real = ids[t * kTile + lane] >= 0;
+    xadjc[t * kTile + lane] = real ? (float)s * 0.5f : __builtin_inff();
+    float r = real ? __double2float_ru(__builtin_sqrt(s) * (1.0 + 0x1p-40)) : 0.0f;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) r = fmaxf(r, __shfl_xor(r, m, 64));
+    if (lane == 0 && r > 0.0f) atomicMax((unsigned int *)&rmaxc[tile_list[t]], __float_as_uint(r));
+}
+
 // X[tile][j][row] = Xr[tile*64 + row][j]: one workgroup per tile, LDS
 // transpose of 64-dim slabs (reads and writes coalesced); dims d..dpad-1 = 0.
 __global__ __launch_bounds__(256) void k_tiles_from_rows(const float *Xr, int64_t d, int64_t dpad, float *X) {
@@ -181,13 +205,15 @@ __global__ __launch_bounds__(256) void k_tiles_from_rows(const float *Xr, int64_
 // bf16 part of dims 16c + 8h .. +7 of candidate row 4 (p & 15) + (p >> 4) (the
 // permutation makes a 16-lane group's B-fragment reads consecutive).  One
 // workgroup per (tile, chunk), one 16-B unit per thread.
+// With pivot (L2): the parts of fl(x - c), c = the row's list pivot.
 __global__ __launch_bounds__(256) void k_split_rows(const float *Xr, int64_t d, int64_t n_tiles, int64_t dpad,
-                                                   uint4 *Xb) {
+                                                   const float *pivot, const int32_t *tile_list, uint4 *Xb) {
     const int64_t nch = dpad / 16, total = n_tiles * nch;
     const int u = threadIdx.x, g = u >> 6, p = u & 63, r = 4 * (p & 15) + (p >> 4), h = g & 1, hl = g >> 1;
     for (int64_t tc = blockIdx.x; tc < total; tc += gridDim.x) {
         const int64_t t = tc / nch, c = tc % nch;
         const float *src = Xr + (t * kTile + r) * d;
+        const float *pv = pivot ? pivot + (int64_t)tile_list[t] * d : nullptr;
         uint32_t w[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -195,7 +221,7 @@ __global__ __launch_bounds__(256) void k_split_rows(const float *Xr, int64_t d, 
 #pragma unroll
             for (int f = 0; f < 2; ++f) {
                 const int64_t j = 16 * c + 8 * h + 2 * e + f;
-                part[f] = bf16_split_part(j < d ? src[j] : 0.0f, hl);
+                part[f] = bf16_split_part(j < d ? (pv ? src[j] - pv[j] : src[j]) : 0.0f, hl);
             }
             w[e] = part[0] | (part[1] << 16);
         }
@@ -220,8 +246,12 @@ static void free_storage(lira_index *idx) {
     idx->Xb = nullptr;
     if (idx->xadj) hipFree(idx->xadj);
     if (idx->rmax) hipFree(idx->rmax);
+    if (idx->xadjc) hipFree(idx->xadjc);
+    if (idx->rmaxc) hipFree(idx->rmaxc);
     idx->xadj = nullptr;
     idx->rmax = nullptr;
+    idx->xadjc = nullptr;
+    idx->rmaxc = nullptr;
     if (idx->pivot) hipFree(idx->pivot);
     if (idx->tstat) hipFree(idx->tstat);
     idx->pivot = nullptr;
@@ -446,11 +476,24 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
             rc = fail(LIRA_EHIP, std::string("row norms / pivots failed: ") + hipGetErrorString(e));
             break;
         }
-        // the split-bf16 screen copy: best effort (without it the screen runs on fp32 MFMA / VALU)
+        // the split-bf16 screen copy: best effort (without it the screen runs on fp32 MFMA / VALU);
+        // L2: of x - pivot, with its own (centred) norms
         if (hipMalloc(&idx->Xb, (size_t)tiles * kTile * dpad * 4) == hipSuccess) {
-            hipLaunchKernelGGL(k_split_rows, dim3((unsigned)std::min<int64_t>(tiles * (dpad / 16), 1 << 20)),
-                               dim3(256), 0, st, idx->Xr, d, tiles, dpad, (uint4 *)idx->Xb);
-            e = hipGetLastError();
+            if (idx->pivot) {
+                if (hipMalloc(&idx->xadjc, (size_t)tiles * kTile * 4) != hipSuccess ||
+                    hipMalloc(&idx->rmaxc, (size_t)n_lists * 4) != hipSuccess) {
+                    rc = fail(LIRA_ENOMEM, "hipMalloc of the centred row-norm arrays failed");
+                    break;
+                }
+                e = hipMemsetAsync(idx->rmaxc, 0, (size_t)n_lists * 4, st);
+                if (e == hipSuccess)
+                    hipLaunchKernelGGL(k_row_norms_c, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, idx->Xr,
+                                       idx->ids, d, d_tlist, idx->pivot, tiles, idx->xadjc, idx->rmaxc);
+            }
+            if (e == hipSuccess)
+                hipLaunchKernelGGL(k_split_rows, dim3((unsigned)std::min<int64_t>(tiles * (dpad / 16), 1 << 20)),
+                                   dim3(256), 0, st, idx->Xr, d, tiles, dpad, idx->pivot, d_tlist, (uint4 *)idx->Xb);
+            if (e == hipSuccess) e = hipGetLastError();
         } else {
             (void)hipGetLastError();
             idx->Xb = nullptr;
@@ -521,6 +564,7 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes) {
              (idx->Xb ? rows * idx->dpad * 4 : 0) +                            // split-bf16 copy
              (idx->X ? rows * idx->dpad * 4 : 0) +                             // fp32 tiles (optional)
              (idx->xadj ? rows * 4 + idx->n_lists * 4 : 0) +                   // xadj, rmax
+             (idx->xadjc ? rows * 4 + idx->n_lists * 4 : 0) +                  // centred xadj, rmax
              (idx->pivot ? idx->n_lists * idx->d * 4 + idx->n_tiles * 8 : 0);  // pivots, tile radii
     return LIRA_OK;
 }

@@ -73,6 +73,12 @@ struct lira_index_impl {
     // padding rows; per list rmax >= max ||x|| over its rows (rounded up).
     float *xadj = nullptr;
     float *rmax = nullptr;
+    // The same for the split-bf16 copy, which holds x - pivot of its list (L2:
+    // the screen works on centred vectors, whose norms and hence error bounds
+    // are smaller): xadjc = ||fl(x - c)||^2 / 2, rmaxc >= max ||fl(x - c)||.
+    // NULL for IP (no centring) -- the split screen then uses xadj / rmax.
+    float *xadjc = nullptr;
+    float *rmaxc = nullptr;
     // Row-major copy of the tiles, [n_tiles*64][d] fp32 by storage row: the
     // screened path's exact re-check reads one candidate's d values
     // contiguously (a tile column would cost one cache line per value).

@@ -86,6 +86,7 @@ struct ScreenArgs {
     const float2 *tstat;
     int share;     // k_screen_m: publish/re-read the query bound every block (else once per item)
     int split;     // k_screen_m<..., SPLIT = 1>: X is the split-bf16 copy (Xb), QT in the split layout
+    int centred;   // (L2, split) Xb / QT hold x - c / q - c of the list's pivot; xadj, rmax, QN are theirs
     int dbg;  // timing experiments only (env LIRA_SCAN_DEBUG; results invalid): 1 = no MFMA, 2 = no selection,
              // 4 = no X/Q staging, 8 = per-phase clocks into stats 1/3/6 (k_screen_m)
 };
@@ -100,15 +101,22 @@ struct ScreenArgs {
 // 1.02 |q| R + an absolute term for flushed subnormal parts (values below
 // 2^-100 lose at most 2^-100 (|q| + R) per product).  The rest of the L2
 // score's error (qn, xn, their sum, the final fma) stays <= 8.4 u (|q|+R)^2.
+//
+// centred (L2, split screen): q' = fl(q - c), x' = fl(x - c) for the list's
+// pivot c, and qnorm, R the norms of q', x'.  Then (q' - x') - (q - x) =
+// (q - c) e1 - (x - c) e2 with |e| <= u per component, so ||q'-x'||^2 differs
+// from D = ||q-x||^2 by at most u s (2 + u) s (1 + u) <= 2.01 u s^2, s = qnorm
+// + R, on top of the screen's own error for q', x'.
 template <int METRIC>
-__device__ __forceinline__ double err_E(double qnorm, double R, double d, int split = 0, double dp = 0.0) {
+__device__ __forceinline__ double err_E(double qnorm, double R, double d, int split = 0, double dp = 0.0,
+                                        int centred = 0) {
     const double dl = d * 0x1p-140;
     if (split) {
         const double ed = (2.0001 * 0x1p-16 + 4.0 * dp * 0x1p-22) * 1.02 * qnorm * R +
                           4.0 * dp * 0x1p-96 * (qnorm + R + 1.0);
         if (METRIC == LIRA_METRIC_L2) {
             const double s = qnorm + R;
-            return 2.0 * ed + 1.05 * 8.0 * kU * s * s + dl;
+            return 2.0 * ed + (1.05 * 8.0 + (centred ? 2.01 : 0.0)) * kU * s * s + dl;
         }
         // IP: bound_P / s_lim carry no (1 +- g) factor, so E also covers
         // search.cpp's own rounding of the exact sum, (d+2) u |q| R (L2 needs
@@ -157,11 +165,15 @@ __device__ __forceinline__ float row_h(double lim, double qn, double qnorm, doub
 // SPLIT: QT per query block and 16-dim chunk c is [g 4][QR rows][8 bf16]
 // (64 QR bytes, the fp32 chunk's size), g = 2 hl + h holding the hi/lo part
 // of dims 16c + 8h .. +7 of the row: the A fragments of k_screen_m<SPLIT>.
+//
+// cpivot (L2, split): centre the rows on their partition's pivot, fl(q - c),
+// before splitting; QN.x / QN.y are then the centred norms, and pqn[pair] =
+// QN.y (the merge's copy of the row's norm).
 template <int QR, bool SPLIT>
 __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64_t dpad, int nprobe,
                                                 int n_virt, int n_lists, const int32_t *cnt, const int32_t *qoff,
                                                 const int32_t *qlist, const int32_t *qblk_off, const float *pivot,
-                                                float *QT, float4 *QN) {
+                                                const float *cpivot, float *QT, float4 *QN, float *pqn) {
     __shared__ int pairs[QR];
     __shared__ int s_v;
     __shared__ float tr[64][65];
@@ -178,6 +190,7 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
     __syncthreads();
     const int v = s_v, qb = b - qblk_off[v];
     const int nval = min(QR, cnt[v] - qb * QR);
+    const float *cpv = cpivot ? cpivot + (int64_t)(v >= n_lists ? v - n_lists : v) * d : nullptr;
     if (threadIdx.x < QR) pairs[threadIdx.x] = (int)threadIdx.x < nval ? qlist[qoff[v] + qb * QR + threadIdx.x] : -1;
     __syncthreads();
     // transpose through LDS, 64 rows x 64 dims at a time: reads along the
@@ -189,7 +202,8 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
             const int64_t j = j0 + lane;
             for (int rr = wv; rr < RT; rr += 4) {
                 const int pr = pairs[r0 + rr];
-                tr[rr][lane] = pr >= 0 && j < d ? Q[(int64_t)(pr / nprobe) * d + j] : 0.0f;
+                const float qv = pr >= 0 && j < d ? Q[(int64_t)(pr / nprobe) * d + j] : 0.0f;
+                tr[rr][lane] = cpv && j < d ? qv - cpv[j] : qv;
             }
             __syncthreads();
             if (SPLIT) {
@@ -222,7 +236,8 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
             const float *pv = pivot ? pivot + (int64_t)(v >= n_lists ? v - n_lists : v) * d : nullptr;
             for (int64_t j = lane; j < d; j += 64) {
                 const double x = (double)qr[j];
-                s = __builtin_fma(x, x, s);
+                const double xc = cpv ? (double)(qr[j] - cpv[j]) : x;  // the staged value
+                s = __builtin_fma(xc, xc, s);
                 if (pv) {
                     const double df = x - (double)pv[j];
                     t = __builtin_fma(df, df, t);
@@ -234,9 +249,11 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
             s += __shfl_xor(s, m, 64);
             t += __shfl_xor(t, m, 64);
         }
-        if (lane == 0)
-            QN[(int64_t)b * QR + r] = make_float4((float)s, __double2float_ru(__builtin_sqrt(s) * (1.0 + 0x1p-40)),
-                                                  __int_as_float(pr), (float)__builtin_sqrt(t));
+        if (lane == 0) {
+            const float qnu = __double2float_ru(__builtin_sqrt(s) * (1.0 + 0x1p-40));
+            QN[(int64_t)b * QR + r] = make_float4((float)s, qnu, __int_as_float(pr), (float)__builtin_sqrt(t));
+            if (pqn && pr >= 0) pqn[pr] = qnu;
+        }
     }
 }
 
@@ -653,6 +670,8 @@ struct SMergeArgs {
     int n_lists, nprobe, k, K2, nch_max, bpc, dedup, per_partition;
     int groups, bpc_near;  // groups == 2: slot 0 pairs are virtual partition p, chunked by bpc_near
     int split;             // the lists came from the split-bf16 screen (its error model)
+    int centred;           // ... on centred vectors: pqn[pair] = the row's norm, rmax the centred one
+    const float *pqn;
     unsigned long long *stats;
 };
 
@@ -770,7 +789,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
         const int my_pair = __float_as_int(qrec.z);
         const int my_q = my_pair >= 0 ? my_pair / a.nprobe : -1;
         const double my_qn = (double)qrec.x, my_qnorm = (double)qrec.y;
-        const double my_E = err_E<METRIC>(my_qnorm, R, dd, SPLIT, (double)a.dpad);
+        const double my_E = err_E<METRIC>(my_qnorm, R, dd, SPLIT, (double)a.dpad, a.centred);
         u64 *my_list = lists + my_row * K2;
         // this lane's 4 output rows 4g + reg: qn for the screened scores
         float qn_r[4];
@@ -1066,7 +1085,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                     const float B = ord2f((uint32_t)__shfl((int)key16, 16 * g + j - 1, 64));
                     if (h == -__builtin_inff() && B < __builtin_inff()) {
                         const double qnorm_r = (double)__shfl((float)my_qnorm, 4 * g + reg, 64);
-                        const double E_r = err_E<METRIC>(qnorm_r, R, dd, SPLIT, (double)a.dpad);
+                        const double E_r = err_E<METRIC>(qnorm_r, R, dd, SPLIT, (double)a.dpad, a.centred);
                         h = row_h<METRIC>(s_lim<METRIC>(bound_P<METRIC>((double)B, E_r, dd), E_r, dd),
                                           (double)qn_r[reg], qnorm_r, R);
                         int pm2 = 0;
@@ -1168,41 +1187,37 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
 // before k_screen, so no item starts unbounded (which would push a whole
 // first block per row through the selection).
 static constexpr int kSeedTiles = 4;
-// One wave per query; the (up to 4) tiles' rows are read from the row-major
-// copy 16 dims at a time, coalesced (a tile's 64 rows are contiguous: lane l
-// loads 16-B pieces of rows l/4 + 16 i), transposed through a per-wave LDS
-// slab [tile][row][17] (odd stride: conflict-free column reads), and lane r
-// accumulates row r of every tile in search.cpp's order.
-static constexpr int kSeedSlab = kSeedTiles * 64 * 17;  // floats per wave
+// One workgroup per query, wave w = tile w of its first probed partition.  The
+// tile's 64 rows (contiguous in the row-major copy) are read 32 dims at a time,
+// coalesced (lane l loads 16-B pieces of rows l/8 + 8 i), transposed through a
+// per-wave LDS slab [row][33] (odd stride: conflict-free row reads), and lane r
+// accumulates row r in search.cpp's order.  The 4 x 64 exact scores then meet
+// in LDS, where wave 0 forms the bound.
 template <int METRIC>
 __global__ __launch_bounds__(256) void k_seed(const float *Q, const int32_t *probe, int nprobe, int n_lists,
                                               const int32_t *tile_off, const int32_t *ids, const float *Xr,
                                               int64_t d, int64_t nq, int k, uint32_t *qbound) {
-    __shared__ float slab_all[4][kSeedSlab];
+    __shared__ float slab_all[kSeedTiles][64 * 33];
+    __shared__ float score_s[kSeedTiles][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int64_t q = (int64_t)blockIdx.x * 4 + w;
+    const int64_t q = blockIdx.x;
     if (q >= nq) return;
     const int p = probe[q * nprobe];
-    if (p < 0 || p >= n_lists) return;
+    if (p < 0 || p >= n_lists) return;  // workgroup-uniform
     const int tile0 = tile_off[p], nt = min(kSeedTiles, tile_off[p + 1] - tile0);
     if (nt <= 0) return;
-    float *slab = slab_all[w];
-    const float *qrow = Q + q * d;
-    const float *rows = Xr + (int64_t)tile0 * kTile * d;  // the nt tiles' rows, contiguous
-    const bool v4 = (d & 3) == 0;
-    float acc[kSeedTiles];
+    float acc = 0.0f;
+    if (w < nt) {
+        float *slab = slab_all[w];
+        const float *qrow = Q + q * d;
+        const float *rows = Xr + (int64_t)(tile0 + w) * kTile * d;
+        const bool v4 = (d & 3) == 0;
+        for (int64_t j0 = 0; j0 < d; j0 += 32) {
+            const int nj = (int)min<int64_t>(32, d - j0);
 #pragma unroll
-    for (int t = 0; t < kSeedTiles; ++t) acc[t] = 0.0f;
-    for (int64_t j0 = 0; j0 < d; j0 += 16) {
-        const int nj = (int)min<int64_t>(16, d - j0);
-        // stage dims j0 .. j0+nj-1 of the nt x 64 rows
-#pragma unroll
-        for (int t = 0; t < kSeedTiles; ++t) {
-            if (t >= nt) break;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int r = (lane >> 2) + 16 * i, c = 4 * (lane & 3);
-                const float *src = rows + ((int64_t)t * kTile + r) * d + j0 + c;
+            for (int i = 0; i < 8; ++i) {
+                const int r = (lane >> 3) + 8 * i, c = 4 * (lane & 7);
+                const float *src = rows + (int64_t)r * d + j0 + c;
                 float v[4];
                 if (v4 && c + 4 <= nj) {
                     const float4 f = *(const float4 *)src;
@@ -1212,38 +1227,36 @@ __global__ __launch_bounds__(256) void k_seed(const float *Q, const int32_t *pro
                     for (int u = 0; u < 4; ++u) v[u] = c + u < nj ? src[u] : 0.0f;
                 }
 #pragma unroll
-                for (int u = 0; u < 4; ++u) slab[(t * 64 + r) * 17 + c + u] = v[u];
+                for (int u = 0; u < 4; ++u) slab[r * 33 + c + u] = v[u];
             }
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        const float qv = lane < nj ? qrow[j0 + lane] : 0.0f;
-        for (int jj = 0; jj < nj; ++jj) {
-            const float qj = __shfl(qv, jj, 64);
-#pragma unroll
-            for (int t = 0; t < kSeedTiles; ++t) {
-                const float xv = slab[(t * 64 + lane) * 17 + jj];
+            const float qv = (lane & 31) < nj ? qrow[j0 + (lane & 31)] : 0.0f;
+            __builtin_amdgcn_wave_barrier();
+            for (int jj = 0; jj < nj; ++jj) {
+                const float qj = __shfl(qv, jj, 64);
+                const float xv = slab[lane * 33 + jj];
                 if (METRIC == LIRA_METRIC_L2) {
                     const float df = qj - xv;
-                    acc[t] = acc[t] + df * df;
+                    acc = acc + df * df;
                 } else {
-                    acc[t] = acc[t] + qj * xv;
+                    acc = acc + qj * xv;
                 }
             }
+            __builtin_amdgcn_wave_barrier();
         }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
+    const float sc = METRIC == LIRA_METRIC_L2 ? acc : -acc;
+    score_s[w][lane] = w < nt && ids[(tile0 + w) * kTile + lane] >= 0 && sc == sc ? sc : __builtin_inff();
+    __syncthreads();
+    if (w != 0) return;
     float m[4] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};  // 4 smallest
 #pragma unroll
     for (int u = 0; u < kSeedTiles; ++u) {
-        float sc = METRIC == LIRA_METRIC_L2 ? acc[u] : -acc[u];
-        if (u >= nt || ids[(tile0 + u) * kTile + lane] < 0 || !(sc == sc)) continue;
+        float v = score_s[u][lane];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const float lo = fminf(m[i], sc), hi = fmaxf(m[i], sc);
+            const float lo = fminf(m[i], v), hi = fmaxf(m[i], v);
             m[i] = lo;
-            sc = hi;
+            v = hi;
         }
     }
     const int t = (k + 63) / 64;
@@ -1354,7 +1367,9 @@ __global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
             double lim = 0.0;
             bool over = false;
             if (p >= 0) {
-                lim = s_lim<METRIC>((double)T, err_E<METRIC>(qnorm, (double)a.rmax[p], dd, a.split, (double)a.dpad), dd);
+                const double qn_s = a.centred ? (double)a.pqn[q * a.nprobe + s] : qnorm;
+                lim = s_lim<METRIC>((double)T, err_E<METRIC>(qn_s, (double)a.rmax[p], dd, a.split, (double)a.dpad,
+                                                             a.centred), dd);
                 const u64 last = src[K2 - 1];
                 over = last != kEmptyKey && (double)key_score(last) <= lim;
             }
@@ -1383,7 +1398,8 @@ __global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
             reset();
             if (p >= 0 && p < a.n_lists) {
                 ncand += a.list_size[p];
-                const double E = err_E<METRIC>(qnorm, (double)a.rmax[p], dd, a.split, (double)a.dpad);
+                const double qn_s = a.centred ? (double)a.pqn[q * a.nprobe + s] : qnorm;
+                const double E = err_E<METRIC>(qn_s, (double)a.rmax[p], dd, a.split, (double)a.dpad, a.centred);
                 const u64 *base = a.partial + (q * a.nprobe + s) * (int64_t)a.nch_max * K2;
                 float T = __builtin_inff();  // the pair's own bound: min over its chunk lists
                 const int nc = a.nch[vnch(s, p)];
@@ -1404,7 +1420,8 @@ __global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
             for (int s = 0; s < a.nprobe; ++s) {
                 const int p = prow[s];
                 if (p < 0 || p >= a.n_lists) continue;
-                const double E = err_E<METRIC>(qnorm, (double)a.rmax[p], dd, a.split, (double)a.dpad);
+                const double qn_s = a.centred ? (double)a.pqn[q * a.nprobe + s] : qnorm;
+                const double E = err_E<METRIC>(qn_s, (double)a.rmax[p], dd, a.split, (double)a.dpad, a.centred);
                 const u64 *base = a.partial + (q * a.nprobe + s) * (int64_t)a.nch_max * K2;
                 for (int c = 0; c < a.nch[vnch(s, p)]; ++c) T = fminf(T, list_bound(base + (int64_t)c * K2, E));
             }
@@ -1452,7 +1469,7 @@ struct SPlan {
     int rl = 1, qr = 64, K2 = 32, bpc = 1, bpc_near = 1, nch_max = 1, grid = 1, smem = 0, mfma = 1, split = 0;
     int64_t max_qblk = 0;
     size_t off_cnt, off_cursor, off_head, off_qoff, off_item, off_nch, off_qblk, off_itab, off_qlist, off_qt, off_qn,
-        off_partial, off_qbound, total;
+        off_partial, off_qbound, off_pqn, total;
 };
 
 static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k) {
@@ -1471,7 +1488,7 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     pl.qr = pl.mfma ? (pl.rl <= 2 ? qr_opt : 64) : screen_qr(pl.rl);
     // split-bf16 MFMA screen (k_screen_m<..., SPLIT>) where the index holds Xb;
     // LIRA_OPT_SPLIT = 0 keeps the fp32 MFMA screen (which reads the fp32 tiles)
-    pl.split = (op.split || !idx->X) && pl.mfma && pl.qr == 64 && idx->Xb != nullptr;
+    pl.split = (op.split || !idx->X) && pl.mfma && idx->Xb != nullptr;
     pl.K2 = 32 * pl.rl;
     pl.smem = !pl.mfma       ? screen_smem(pl.qr, pl.rl)
               : pl.qr == 128 ? (pl.rl == 1 ? SSmem<128, 1, true>::total : SSmem<128, 2, true>::total)
@@ -1526,6 +1543,7 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     pl.off_qn = take((size_t)pl.max_qblk * pl.qr * 16);
     pl.off_partial = take((size_t)npairs * pl.nch_max * pl.K2 * 8);
     pl.off_qbound = take((size_t)nq * 4);
+    pl.off_pqn = take((size_t)npairs * 4);
     pl.total = o;
     return pl;
 }
@@ -1578,6 +1596,8 @@ static hipError_t launch_screen_m(const ScreenArgs &a, const SPlan &pl, hipStrea
 template <int M>
 static hipError_t launch_screen_rl(const ScreenArgs &a, const SPlan &pl, hipStream_t st) {
     if (pl.mfma) {
+        if (pl.qr == 128 && pl.split)
+            return pl.rl == 1 ? launch_screen_m<M, 1, 128, true>(a, pl, st) : launch_screen_m<M, 2, 128, true>(a, pl, st);
         if (pl.qr == 128) return pl.rl == 1 ? launch_screen_m<M, 1, 128>(a, pl, st) : launch_screen_m<M, 2, 128>(a, pl, st);
         if (pl.split) switch (pl.rl) {
             case 1: return launch_screen_m<M, 1, 64, true>(a, pl, st);
@@ -1668,27 +1688,34 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
                              nch, head, qlist, qblk, itab, st));
     const bool tri = o.prune && !(flags & LIRA_SCAN_NO_PRUNE) && pl.mfma && idx->pivot;
     const float *tri_pivot = tri ? idx->pivot : nullptr;
-    if (pl.qr == 128)
+    // the split screen works on centred vectors where the index has them (L2)
+    const bool centred = pl.split && idx->xadjc != nullptr && idx->pivot != nullptr;
+    const float *cpivot = centred ? idx->pivot : nullptr;
+    float *pqn = centred ? (float *)(w + pl.off_pqn) : nullptr;
+    if (pl.qr == 128 && pl.split)
+        hipLaunchKernelGGL((k_qstage<128, true>), dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
+                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn);
+    else if (pl.qr == 128)
         hipLaunchKernelGGL((k_qstage<128, false>), dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
-                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, QT, QN);
+                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn);
     else if (pl.qr == 64 && pl.split)
         hipLaunchKernelGGL((k_qstage<64, true>), dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
-                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, QT, QN);
+                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn);
     else if (pl.qr == 64)
         hipLaunchKernelGGL((k_qstage<64, false>), dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
-                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, QT, QN);
+                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn);
     else
         hipLaunchKernelGGL((k_qstage<32, false>), dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
-                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, QT, QN);
+                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn);
     LIRA_HIP_TRY(hipGetLastError());
     // (measured: SIFT1M mixture 1.70 -> 1.44 ms, latent +1 %)
     if (qbound && o.seed) {
         if (idx->metric == LIRA_METRIC_L2)
-            hipLaunchKernelGGL(k_seed<LIRA_METRIC_L2>, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, q, probe,
+            hipLaunchKernelGGL(k_seed<LIRA_METRIC_L2>, dim3((unsigned)nq), dim3(256), 0, st, q, probe,
                                (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->Xr, idx->d, nq,
                                (int)k, qbound);
         else
-            hipLaunchKernelGGL(k_seed<LIRA_METRIC_IP>, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, q, probe,
+            hipLaunchKernelGGL(k_seed<LIRA_METRIC_IP>, dim3((unsigned)nq), dim3(256), 0, st, q, probe,
                                (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->Xr, idx->d, nq,
                                (int)k, qbound);
         LIRA_HIP_TRY(hipGetLastError());
@@ -1702,9 +1729,10 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     a.dbg = o.debug;
     a.share = o.share;
     a.split = pl.split;
+    a.centred = centred;
     a.X = pl.split ? (const float *)idx->Xb : idx->X;
-    a.xadj = idx->xadj;
-    a.rmax = idx->rmax;
+    a.xadj = centred ? idx->xadjc : idx->xadj;
+    a.rmax = centred ? idx->rmaxc : idx->rmax;
     a.tile_off = idx->tile_off;
     a.cnt = cnt;
     a.item_off = item_off;
@@ -1739,7 +1767,9 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     m.ids = idx->ids;
     m.Q = q;
     m.Xr = idx->Xr;
-    m.rmax = idx->rmax;
+    m.rmax = centred ? idx->rmaxc : idx->rmax;
+    m.centred = centred;
+    m.pqn = pqn;
     m.qbound = qbound;
     m.D = out_D;
     m.I = out_I;
