@@ -139,6 +139,8 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *   LIRA_OPT_NEAR_ROUNDS the same for the nearest-probe group (default 2)
  *   LIRA_OPT_MFMA        screen engine: 1 auto (default), 0 VALU, 2 MFMA wherever it fits
  *   LIRA_OPT_DEBUG       timing experiments only (results invalid): bit mask, see lira_screen.hip
+ *   LIRA_OPT_PIPELINE    1: the pipelined split screen k_screen_s (default); 0: k_screen_m
+ *   LIRA_OPT_RING        k_screen_s ring slots: 0 auto, 2..4
  */
 #define LIRA_OPT_KEEP_TILES 1
 #define LIRA_OPT_SCREEN 2
@@ -152,6 +154,8 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
 #define LIRA_OPT_NEAR_ROUNDS 10
 #define LIRA_OPT_MFMA 11
 #define LIRA_OPT_DEBUG 12
+#define LIRA_OPT_PIPELINE 13
+#define LIRA_OPT_RING 14
 int lira_index_set_option(lira_index *idx, int option, int64_t value);
 int lira_index_get_option(const lira_index *idx, int option, int64_t *value);
 /* 1 if the index holds the fp32 tile copy (LIRA_OPT_KEEP_TILES at build time) */

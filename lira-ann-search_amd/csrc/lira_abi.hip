@@ -36,7 +36,7 @@ hipError_t set_smem_attr_once(std::atomic<uint64_t> &mask, const void *fn, int b
 }
 
 // scan entry points (lira_scan.hip)
-int scan_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, size_t *bytes);
+int scan_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, unsigned flags, size_t *bytes);
 std::string scan_describe(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, unsigned flags);
 int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe, int64_t nprobe,
               int64_t k, unsigned flags, float *out_D, int64_t *out_I, int64_t *out_ncand,
@@ -587,6 +587,8 @@ int lira_index_set_option(lira_index *idx, int option, int64_t value) {
         case LIRA_OPT_NEAR_ROUNDS: if (!in(1, 1024)) break; o.near_rounds = v; return LIRA_OK;
         case LIRA_OPT_MFMA: if (!in(0, 2)) break; o.mfma = v; return LIRA_OK;
         case LIRA_OPT_DEBUG: if (!in(0, 255)) break; o.debug = v; return LIRA_OK;
+        case LIRA_OPT_PIPELINE: if (!in(0, 1)) break; o.pipeline = v; return LIRA_OK;
+        case LIRA_OPT_RING: if (!in(0, 4)) break; o.ring = v; return LIRA_OK;
         default: return fail(LIRA_EINVAL, "unknown option " + std::to_string(option));
     }
     return fail(LIRA_EINVAL, "value " + std::to_string(value) + " out of range for option " + std::to_string(option));
@@ -608,6 +610,8 @@ int lira_index_get_option(const lira_index *idx, int option, int64_t *value) {
         case LIRA_OPT_NEAR_ROUNDS: *value = o.near_rounds; break;
         case LIRA_OPT_MFMA: *value = o.mfma; break;
         case LIRA_OPT_DEBUG: *value = o.debug; break;
+        case LIRA_OPT_PIPELINE: *value = o.pipeline; break;
+        case LIRA_OPT_RING: *value = o.ring; break;
         default: return fail(LIRA_EINVAL, "unknown option " + std::to_string(option));
     }
     return LIRA_OK;
@@ -621,11 +625,10 @@ int lira_index_has_tiles(const lira_index *idx, int *out) {
 
 int lira_scan_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe_max, int64_t k,
                              unsigned flags, size_t *bytes) {
-    (void)flags;
     if (!idx || !bytes) return fail(LIRA_EINVAL, "NULL argument");
     if (nq < 0 || nprobe_max <= 0 || k <= 0 || k > 256)
         return fail(LIRA_EINVAL, "need nq >= 0, nprobe_max > 0, 1 <= k <= 256");
-    return scan_workspace_size(idx, nq, nprobe_max, k, bytes);
+    return scan_workspace_size(idx, nq, nprobe_max, k, flags, bytes);
 }
 
 int lira_scan_describe(const lira_index *idx, int64_t nq, int64_t nprobe_max, int64_t k, unsigned flags,

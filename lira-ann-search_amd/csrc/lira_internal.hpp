@@ -45,6 +45,8 @@ struct lira_opts {
     int near_rounds = 2;
     int mfma = 1;
     int debug = 0;
+    int pipeline = 1;
+    int ring = 0;
 };
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device):

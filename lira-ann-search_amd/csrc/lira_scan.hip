@@ -932,7 +932,7 @@ static void launch_merge(const MergeArgs &a, hipStream_t st) {
 }
 
 bool screen_supported(const lira_index *idx, int64_t k);
-size_t screen_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k);
+size_t screen_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, unsigned flags);
 int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe, int64_t nprobe, int64_t k,
                 unsigned flags, int Rm, float *out_D, int64_t *out_I, int64_t *out_ncand, void *ws,
                 size_t ws_bytes, hipStream_t st, hipEvent_t *ev);
@@ -944,10 +944,10 @@ static bool use_screen(const lira_index *idx, int64_t k, unsigned flags) {
     return (idx->opt.screen || !idx->X) && !(flags & (LIRA_SCAN_FMA | LIRA_SCAN_EXACT)) && screen_supported(idx, k);
 }
 
-int scan_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k,
+int scan_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, unsigned flags,
                         size_t *bytes) {
     ScanPlan pl = make_plan(idx, nq, nprobe, k);
-    *bytes = std::max(pl.total, screen_supported(idx, k) ? screen_workspace_size(idx, nq, nprobe, k) : 0);
+    *bytes = std::max(pl.total, screen_supported(idx, k) ? screen_workspace_size(idx, nq, nprobe, k, flags) : 0);
     return LIRA_OK;
 }
 

@@ -1179,6 +1179,475 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
     }
 }
 
+// ---- the pipelined split-bf16 screen (default) -------------------------------
+// k_screen_s: k_screen_m<..., SPLIT>'s work (same items, error model, row
+// lists and outputs) around an NS-slot LDS-DMA ring:
+//  * a wave waits only for its OWN DMA of the chunk it consumes, by a counted
+//    s_waitcnt vmcnt(Y) (Y = the DMA instructions it issued since that chunk's),
+//    then one barrier; NS - 1 chunks stay in flight across block boundaries,
+//    so the streaming overlaps the MFMAs and the selection;
+//  * nothing the compiler sees as a global load is consumed inside the ring
+//    (its own waitcnts would drain it): the block's xadj rides with the
+//    block's first chunk, and the query bounds published by other items come
+//    back by DMA into LDS (pub_s) at a block's end, to be read at the next;
+//  * thresholds are refreshed at a block's end (the selection's h and the
+//    triangle-skip interval the issuer uses for the blocks after it).
+template <int QR, int RL, int NS, int BC>
+struct SSmem2 {
+    static constexpr int NW = QR / 16, K2 = 32 * RL;
+    static constexpr int kX = kSBT * kSDK * kTile * 4;  // X chunk: 16 KiB (split-bf16 = fp32 bytes)
+    static constexpr int kQ = kSDK * QR * 4;            // Q chunk
+    static constexpr int kXA = kSBT * kTile * 4;        // the block's xadj (rides with chunk 0)
+    static constexpr int kSlot = kX + kQ + kXA;
+    static constexpr int kRing = NS * kSlot;
+    static constexpr int kLists = QR * K2 * 8;
+    static constexpr int kBufs = QR * BC * 8;
+    static constexpr int kBR = 256;  // block radius ranges staged per item (the planner keeps items <= kBR blocks)
+    // dq_s [QR] double2, tri_s [2][QR] float2, br_s [kBR] float2, then ints:
+    // item [16], slot tb/jc [4 + 4], marks [NW][8], pair/bufc/pub [QR] each
+    static constexpr int kMeta = QR * 16 + 2 * QR * 8 + kBR * 8 + (24 + NW * 8 + 3 * QR) * 4;
+    static constexpr int total = kRing + kLists + kBufs + kMeta;
+};
+
+__device__ __forceinline__ void sglds4(const void *gsrc, uint32_t lds_addr) {
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds_addr)
+        : "memory");
+}
+
+// s_waitcnt vmcnt(n), n wave-uniform; n > 15 waits for 15 (more than needed: safe)
+__device__ __forceinline__ void wait_vmcnt(int n) {
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+        case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+        case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+        case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+        case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+        case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    }
+}
+
+template <int METRIC, int RL, int QR, int NS, int BC, int OCC>
+__global__ __launch_bounds__(QR * 4, OCC) void k_screen_s(ScreenArgs a) {
+    constexpr int NW = QR / 16, NT = QR * 4;
+    typedef SSmem2<QR, RL, NS, BC> S;
+    constexpr int K2 = S::K2;
+    constexpr int XPW = 16 / NW;  // 1-KiB X pieces per wave per chunk
+    static_assert(NS >= 2 && NS <= 4 && BC <= 32 && 16 % NW == 0, "ring / buffer shape");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char *ring = smem;
+    u64 *lists = (u64 *)(smem + S::kRing);
+    u64 *bufs = (u64 *)(smem + S::kRing + S::kLists);
+    double *dq_s = (double *)(smem + S::kRing + S::kLists + S::kBufs);  // [QR][2]
+    float2 *tri_s = (float2 *)(dq_s + 2 * QR);                          // [2][QR]
+    float2 *br_s = tri_s + 2 * QR;                                       // [kBR]
+    int *meta = (int *)(br_s + S::kBR);                                  // [16]
+    int *slot_tb = meta + 16, *slot_jc = slot_tb + 4;                    // [NS] each
+    int *marks = slot_jc + 4;                                            // [NW][8]
+    int *m_pair = marks + NW * 8, *m_bufc = m_pair + QR;
+    uint32_t *pub_s = (uint32_t *)(m_bufc + QR);
+    const bool TRI = METRIC == LIRA_METRIC_L2 && a.tstat != nullptr;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, cj = lane & 15;
+    const int k = a.k;
+    const double dd = (double)a.d;
+    const float4 *Xg = (const float4 *)a.X;
+    const uint32_t ring_lds = (uint32_t)(uintptr_t)(lds_void_t *)ring;
+    const uint32_t pub_lds = (uint32_t)(uintptr_t)(lds_void_t *)pub_s;
+    const int tstride = (int)a.dpad * (kTile / 4);
+    const int dpad = (int)a.dpad;
+
+    int nxt = tid == 0 ? atomicAdd(&a.head[0], 1) : 0;  // thread 0: the claimed next item
+    for (;;) {
+        if (tid == 0) {
+            const int item = nxt;
+            const int ok = item < a.head[1];
+            int4 e = make_int4(0, 0, 0, 0);
+            if (ok) {
+                e = a.itab[item];
+                nxt = atomicAdd(&a.head[0], 1);
+            }
+            meta[0] = ok;
+            meta[1] = e.x;
+            meta[2] = e.y;
+            meta[3] = e.z;
+            meta[4] = e.w;
+        }
+        __syncthreads();
+        if (!meta[0]) break;
+        const int vp = __builtin_amdgcn_readfirstlane(meta[1]);  // virtual partition
+        const int p = vp >= a.n_lists ? vp - a.n_lists : vp;
+        const int ch = __builtin_amdgcn_readfirstlane(meta[3]);
+        const int gqb = __builtin_amdgcn_readfirstlane(meta[4]);
+        if (tid < QR) {
+            m_pair[tid] = __float_as_int(a.QN[(int64_t)gqb * QR + tid].z);
+            m_bufc[tid] = 0;
+        }
+        for (int i = tid; i < QR * K2; i += NT) lists[i] = kEmptyKey;
+
+        const int tile0 = __builtin_amdgcn_readfirstlane(a.tile_off[p]);
+        const int ntl = __builtin_amdgcn_readfirstlane(a.tile_off[p + 1]) - tile0;
+        const int bpc = vp < a.n_lists && a.n_virt > a.n_lists ? a.bpc_near : a.bpc;
+        const int tb_begin = ch * bpc * kSBT;
+        const int tb_end = min(ntl, tb_begin + bpc * kSBT);
+        const double R = (double)a.rmax[p];
+
+        // lanes 0..15 of wave w hold row 16w + lane's threshold state
+        const int my_row = wave * 16 + cj;
+        const float4 qrec = a.QN[(int64_t)gqb * QR + my_row];
+        const int my_pair = __float_as_int(qrec.z);
+        const int my_q = my_pair >= 0 ? my_pair / a.nprobe : -1;
+        // (kept as floats: the doubles of the bound arithmetic are formed where used)
+        const float my_qnf = qrec.x, my_qnormf = qrec.y;
+        u64 *my_list = lists + my_row * K2;
+        float qn_r[4];
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) qn_r[reg] = __shfl(my_qnf, 4 * g + reg, 64);
+        const float4 *qtg = (const float4 *)(a.QT + (int64_t)gqb * a.dpad * QR);
+        // the published bound of my row's query (plain load: nothing is in flight yet)
+        uint32_t pub = a.qbound && my_q >= 0
+            ? __hip_atomic_load(a.qbound + my_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
+        uint32_t own_pub = ~0u;
+
+        if (TRI && g == 0) {  // ||q_r - c_p|| from k_qstage (QN.w, within 1 ulp), widened by 2^-22
+            const double dq = (double)qrec.w;
+            dq_s[my_row * 2] = dq * (1.0 - 0x1p-22);
+            dq_s[my_row * 2 + 1] = dq * (1.0 + 0x1p-22);
+        }
+        if (TRI) __builtin_amdgcn_wave_barrier();
+        // the row's threshold h and (TRI) skip interval into tri_s[pr], from its
+        // list and the published bound `pub`
+        auto refresh = [&](int pr) {
+            const double my_E = err_E<METRIC>((double)my_qnormf, R, dd, 1, (double)a.dpad, a.centred);
+            const u64 kk = my_list[k - 1];
+            double T = kk == kEmptyKey ? __builtin_inf() : bound_P<METRIC>((double)key_score(kk), my_E, dd);
+            if (pub != ~0u) T = fmin(T, (double)ord2f(pub));
+            const float h = my_pair < 0 ? __builtin_inff()
+                                        : row_h<METRIC>(s_lim<METRIC>(T, my_E, dd), (double)my_qnf,
+                                                        (double)my_qnormf, R);
+            if (TRI && lane < 16) {
+                float2 ab = make_float2(-__builtin_inff(), __builtin_inff());  // never skip
+                const double F = 1.0 - (dd + 4.0) * kU;
+                if (my_pair < 0) {
+                    ab = make_float2(__builtin_inff(), -__builtin_inff());     // no query: always
+                } else if (T < 1e300 && F > 0.5) {
+                    const double rad = __builtin_sqrt((fmax(T, 0.0) + dd * 0x1p-140) / F) * (1.0 + 0x1p-40);
+                    double A = dq_s[my_row * 2] - rad, B = dq_s[my_row * 2 + 1] + rad;
+                    A -= __builtin_fabs(A) * 0x1p-50;
+                    B += __builtin_fabs(B) * 0x1p-50;
+                    ab = make_float2(__double2float_rd(A), __double2float_ru(B));
+                }
+                tri_s[pr * QR + my_row] = ab;
+            }
+            __builtin_amdgcn_wave_barrier();
+            return h;
+        };
+        const int nblk = (tb_end - tb_begin + kSBT - 1) / kSBT;  // <= kBR (planner)
+        if (TRI) {
+            for (int i = tid; i < nblk; i += NT) {
+                const int tb = tb_begin + i * kSBT, ntv = min(kSBT, tb_end - tb);
+                float lo = __builtin_inff(), hi = -__builtin_inff();
+                for (int u = 0; u < ntv; ++u) {
+                    const float2 st = a.tstat[tile0 + tb + u];
+                    lo = fminf(lo, st.x);
+                    hi = fmaxf(hi, st.y);
+                }
+                br_s[i] = make_float2(lo, hi);
+            }
+        }
+        int par = 0;
+        float h_l = refresh(par);
+        __syncthreads();  // lists, pair/bufc, br_s, tri_s[0] visible to every wave
+        // first block at or after t that some row may need (uniform across the
+        // workgroup: every wave tests all QR rows against the same LDS values)
+        auto skip_from = [&](int t, int pr) {
+            if (TRI) {
+                const float2 ab = tri_s[pr * QR + lane];
+                const float2 ab2 = QR > 64 ? tri_s[pr * QR + (QR > 64 ? 64 : 0) + lane]
+                                           : make_float2(__builtin_inff(), -__builtin_inff());
+                while (t < tb_end) {
+                    const float2 r = br_s[(t - tb_begin) / kSBT];
+                    if (!__all((r.y < ab.x || r.x > ab.y) && (r.y < ab2.x || r.x > ab2.y))) break;
+                    if (a.stats && tid == 0) atomicAdd(a.stats + 4, 1ull);
+                    t += kSBT;
+                }
+            }
+            return t;
+        };
+
+        // ---- the ring: issuer state (identical in every wave) -----------------
+        int i_tb = skip_from(tb_begin, par), i_jc = 0, n_iss = 0;
+        int vcount = 0;  // this wave's DMA instructions so far in this item
+        auto issue = [&]() {
+            if (i_tb >= tb_end) return;
+            const int slot = n_iss % NS;
+            const uint32_t base = ring_lds + (uint32_t)(slot * S::kSlot);
+            const int ntv = min(kSBT, tb_end - i_tb);
+#pragma unroll
+            for (int m = 0; m < XPW; ++m) {  // X: 16 pieces of 1 KiB (tile pc >> 2, quarter pc & 3)
+                const int pc = wave + NW * m, t = pc >> 2, qq = pc & 3;
+                sglds16(Xg + (int64_t)(tile0 + i_tb + min(t, ntv - 1)) * tstride + i_jc * (kTile / 4) + qq * 64 + lane,
+                        __builtin_amdgcn_readfirstlane(base + (uint32_t)(t * (kSDK * kTile * 4) + qq * 1024)));
+            }
+            sglds16(qtg + (int64_t)i_jc * (QR / 4) + wave * 64 + lane,  // Q: one 1-KiB piece per wave
+                    __builtin_amdgcn_readfirstlane(base + (uint32_t)S::kX + (uint32_t)wave * 1024u));
+            vcount += XPW + 1;
+            if (i_jc == 0 && wave == 0) {  // the block's xadj (tiles past its end: masked on read)
+                sglds16(a.xadj + (int64_t)(tile0 + i_tb + min(lane >> 4, ntv - 1)) * kTile + (lane & 15) * 4,
+                        __builtin_amdgcn_readfirstlane(base + (uint32_t)(S::kX + S::kQ)));
+                vcount += 1;
+            }
+            if (lane == 0) marks[wave * 8 + slot] = vcount;
+            if (tid == 0) {
+                slot_tb[slot] = i_tb;
+                slot_jc[slot] = i_jc;
+            }
+            ++n_iss;
+            i_jc += kSDK;
+            if (i_jc == dpad) {
+                i_jc = 0;
+                i_tb = skip_from(i_tb + kSBT, par);
+            }
+        };
+        for (int i = 0; i < NS - 1; ++i) issue();
+
+        f4v acc[16];
+        f4 xa[4];
+        bool wdead = true;
+        int c_tb = 0, pubmark = -1;
+#pragma unroll 1
+        for (int seq = 0; seq < n_iss; ++seq) {
+            const int slot = seq % NS;
+            // my DMA of this chunk has landed (uniform count: scalar branches only)
+            wait_vmcnt(__builtin_amdgcn_readfirstlane(vcount - marks[wave * 8 + slot]));
+            __syncthreads();  // everyone's has; the previous slot is free
+            const int tb = __builtin_amdgcn_readfirstlane(slot_tb[slot]);
+            const int jc = __builtin_amdgcn_readfirstlane(slot_jc[slot]);
+            issue();
+            const char *sb = ring + slot * S::kSlot;
+            if (jc == 0) {
+                c_tb = tb;
+                const int ntv = min(kSBT, tb_end - tb);
+                const float *xs = (const float *)(sb + S::kX + S::kQ);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) xa[t] = t < ntv ? *(const f4 *)(xs + t * kTile + 4 * cj) : (f4)(__builtin_inff());
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[i] = (f4v)(0.0f);
+                // a wave whose 16 rows all skip the block (or hold no query) computes nothing for it
+                wdead = !__any(lane < 16 && my_pair >= 0);
+                if (TRI && !wdead) {
+                    const float2 r = br_s[(tb - tb_begin) / kSBT];
+                    const float2 ab = tri_s[par * QR + wave * 16 + cj];
+                    wdead = __all(r.y < ab.x || r.x > ab.y);
+                }
+            }
+            if (!wdead && !(a.dbg & 1)) {
+                const bf16x8 a_hi = *(const bf16x8 *)(sb + S::kX + (((g & 1) * QR + wave * 16 + cj) << 4));
+                const bf16x8 a_lo = *(const bf16x8 *)(sb + S::kX + (((2 + (g & 1)) * QR + wave * 16 + cj) << 4));
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    bf16x8 bv[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        bv[i] = *(const bf16x8 *)(sb + t * (kSDK * kTile * 4) + ((g * 64 + i * 16 + cj) << 4));
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        acc[t * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_hi, bv[i], acc[t * 4 + i], 0, 0, 0);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        acc[t * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_lo, bv[i], acc[t * 4 + i], 0, 0, 0);
+                }
+            }
+            if (jc + kSDK < dpad) continue;
+
+            // ---- the block's last chunk: thresholds, selection, bound exchange
+            if (a.stats && lane == 0) {
+                if (wave == 0) atomicAdd(a.stats + 2, 1ull);
+                if (!wdead) atomicAdd(a.stats + 0, 16ull * kSBT * kTile);
+            }
+            if (pubmark >= 0) {  // the bounds fetched at the previous block's end
+                wait_vmcnt(__builtin_amdgcn_readfirstlane(vcount - pubmark));
+                if (my_q >= 0) pub = min(pub, pub_s[wave * 16 + cj]);
+                pubmark = -1;
+            }
+            h_l = refresh(par ^ 1);  // also the skip interval for the blocks the issuer picks next
+            par ^= 1;
+            if (!wdead && !(a.dbg & 2)) {
+                const int tb = c_tb;
+                float h_r[4];
+#pragma unroll
+                for (int reg = 0; reg < 4; ++reg) h_r[reg] = __shfl(h_l, 4 * g + reg, 64);
+#pragma unroll
+                for (int reg = 0; reg < 4; ++reg) {
+                    float h = h_r[reg];
+                    float wv[16];  // fl(dot - xadj) of my 16 candidates
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const f2 w0 = (f2){acc[t * 4 + 0][reg], acc[t * 4 + 1][reg]} - xa[t].xy;
+                        const f2 w1 = (f2){acc[t * 4 + 2][reg], acc[t * 4 + 3][reg]} - xa[t].zw;
+                        wv[4 * t + 0] = w0.x;
+                        wv[4 * t + 1] = w0.y;
+                        wv[4 * t + 2] = w1.x;
+                        wv[4 * t + 3] = w1.y;
+                    }
+                    const float m01 = fmaxf(fmaxf(wv[0], wv[1]), wv[2]), m02 = fmaxf(fmaxf(wv[3], wv[4]), wv[5]);
+                    const float m03 = fmaxf(fmaxf(wv[6], wv[7]), wv[8]), m04 = fmaxf(fmaxf(wv[9], wv[10]), wv[11]);
+                    const float m05 = fmaxf(fmaxf(wv[12], wv[13]), wv[14]);
+                    const float mx = fmaxf(fmaxf(fmaxf(m01, m02), m03), fmaxf(fmaxf(m04, m05), wv[15]));
+                    if (!__any(mx >= h)) continue;  // wave-uniform: none of the four rows has a candidate
+                    int pm = 0;
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) pm |= (wv[i] >= h && xa[i >> 2][i & 3] != __builtin_inff()) << i;
+                    auto score = [&](int i) {
+                        const float av = xa[i >> 2][i & 3], dv = acc[i][reg];
+                        return METRIC == LIRA_METRIC_L2 ? __builtin_fmaf(-2.0f, dv, qn_r[reg] + 2.0f * av) : -dv;
+                    };
+                    if (__any(h == -__builtin_inff()) && k <= 64) {
+                        // a row without a bound yet: t = ceil(k/16) smallest of each
+                        // of its 16 lanes, j = ceil(k/t) <= 16 over those lanes
+                        float m4[4] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};
+#pragma unroll
+                        for (int i = 0; i < 16; ++i) {
+                            const float sv = score(i);
+                            float v = xa[i >> 2][i & 3] != __builtin_inff() && sv == sv ? sv : __builtin_inff();
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                const float lo = fminf(m4[u], v), hi = fmaxf(m4[u], v);
+                                m4[u] = lo;
+                                v = hi;
+                            }
+                        }
+                        const int t = (k + 15) / 16;
+                        uint32_t key16 = f2ord(t <= 1 ? m4[0] : t == 2 ? m4[1] : t == 3 ? m4[2] : m4[3]);
+#pragma unroll
+                        for (int size = 2; size <= 16; size <<= 1)
+#pragma unroll
+                            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                                const uint32_t o = (uint32_t)__shfl_xor((int)key16, stride, 64);
+                                const bool lower = (cj & stride) == 0, asc = (cj & size) == 0;
+                                key16 = (lower == asc) ? min(key16, o) : max(key16, o);
+                            }
+                        const int j = (k + t - 1) / t;
+                        const float B = ord2f((uint32_t)__shfl((int)key16, 16 * g + j - 1, 64));
+                        if (h == -__builtin_inff() && B < __builtin_inff()) {
+                            const double qnorm_r = (double)__shfl(my_qnormf, 4 * g + reg, 64);
+                            const double E_r = err_E<METRIC>(qnorm_r, R, dd, 1, (double)a.dpad, a.centred);
+                            h = row_h<METRIC>(s_lim<METRIC>(bound_P<METRIC>((double)B, E_r, dd), E_r, dd),
+                                              (double)qn_r[reg], qnorm_r, R);
+                            int pm2 = 0;
+#pragma unroll
+                            for (int i = 0; i < 16; ++i) pm2 |= (acc[i][reg] - xa[i >> 2][i & 3] >= h) << i;
+                            pm &= pm2;
+                        }
+                    }
+                    {
+                        const int row = wave * 16 + 4 * g + reg;
+                        const int bc0 = m_bufc[row];
+                        const int n_l = __builtin_popcount(pm);
+                        int inc = n_l;  // inclusive prefix over the group's 16 lanes
+#pragma unroll
+                        for (int dl = 1; dl < 16; dl <<= 1) {
+                            const int o = __shfl_up(inc, dl, 16);
+                            if (cj >= dl) inc += o;
+                        }
+                        const int rowtot = __shfl(inc, 16 * g + 15, 64);
+                        const bool pre = bc0 > 0 && bc0 + rowtot > BC;
+                        const int total = (pre ? 0 : bc0) + rowtot;
+                        const int base = (pre ? 0 : bc0) + inc - n_l;
+                        for (int r0 = 0;; r0 += BC) {
+                            u64 fl = __ballot((r0 == 0 ? pre : total > r0) && cj == 0);
+                            while (fl) {
+                                const int gg = __builtin_ctzll(fl) >> 4;
+                                fl &= fl - 1;
+                                const int r = wave * 16 + 4 * gg + reg;
+                                s_flush<RL>(lists + r * K2, bufs + r * BC, r0 == 0 ? __shfl(bc0, 16 * gg, 64) : BC);
+                            }
+                            int rank = base;
+#pragma unroll
+                            for (int v = 0; v < 16; ++v) {
+                                if ((pm >> v) & 1) {
+                                    if (rank >= r0 && rank < r0 + BC)
+                                        bufs[row * BC + rank - r0] =
+                                            ((u64)f2ord(score(v)) << 32) |
+                                            (uint32_t)((tile0 + tb + (v >> 2)) * kTile + 4 * cj + (v & 3));
+                                    ++rank;
+                                }
+                            }
+                            __builtin_amdgcn_wave_barrier();
+                            if (!__any(total - r0 > BC)) break;
+                        }
+                        if (cj == 0) {
+                            m_bufc[row] = total <= BC ? total : total - BC * ((total - 1) / BC);
+                            if (a.stats && rowtot) atomicAdd(a.stats + 7, (unsigned long long)rowtot);
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                    }
+                }
+            }
+            // publish my rows' bounds when they improved, and fetch the query's
+            // bounds by DMA for the next block's thresholds
+            if (a.share && a.qbound) {
+                if (lane < 16 && my_q >= 0) {
+                    const u64 kk = my_list[k - 1];
+                    if (kk != kEmptyKey) {
+                        const double my_E = err_E<METRIC>((double)my_qnormf, R, dd, 1, (double)a.dpad, a.centred);
+                        const uint32_t b = f2ord(__double2float_ru(bound_P<METRIC>((double)key_score(kk), my_E, dd)));
+                        if (b < own_pub) {
+                            atomicMin(a.qbound + my_q, b);
+                            own_pub = b;
+                        }
+                    }
+                }
+                if (lane < 16)
+                    sglds4(a.qbound + (my_q >= 0 ? my_q : 0),
+                           __builtin_amdgcn_readfirstlane(pub_lds + (uint32_t)(wave * 64)));
+                vcount += 1;
+                pubmark = vcount;
+            }
+        }
+
+        // ---- flush buffers, emit lists, publish bounds (wave-owned rows)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (a pending bound fetch into pub_s)
+#pragma unroll 1
+        for (int r = 0; r < 16; ++r) {
+            const int row = wave * 16 + r;
+            const int bc = m_bufc[row];
+            if (bc > 0) s_flush<RL>(lists + row * K2, bufs + row * BC, bc);
+            const int pr = m_pair[row];
+            if (pr >= 0) {
+                u64 *dst = a.partial + ((int64_t)pr * a.nch_max + ch) * K2;
+                for (int e = lane; e < K2; e += 64) dst[e] = lists[row * K2 + e];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (lane < 16 && a.qbound && my_q >= 0) {
+            const u64 kk = my_list[k - 1];
+            if (kk != kEmptyKey) {
+                const double my_E = err_E<METRIC>((double)my_qnormf, R, dd, 1, (double)a.dpad, a.centred);
+                const double P = bound_P<METRIC>((double)key_score(kk), my_E, dd);
+                atomicMin(a.qbound + my_q, f2ord(__double2float_ru(P)));
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // ---- seed: a finite starting bound for every query ----------------------
 // One wave per query: exact scores of the first kSeedTiles tiles (256 rows) of its first
 // probed partition; with t = ceil(k/64) smallest per lane and j = ceil(k/t),
@@ -1187,6 +1656,81 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
 // before k_screen, so no item starts unbounded (which would push a whole
 // first block per row through the selection).
 static constexpr int kSeedTiles = 4;
+// The same bound from the fp32 tiles where the index keeps them (one wave per
+// query, lane = candidate: each dim of a tile is one coalesced 256-B row).
+template <int METRIC>
+__global__ __launch_bounds__(256) void k_seed_t(const float *Q, const int32_t *probe, int nprobe, int n_lists,
+                                                const int32_t *tile_off, const int32_t *ids, const float *X,
+                                                int64_t d, int64_t dpad, int64_t nq, int k, uint32_t *qbound) {
+    const int lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    const int p = probe[q * nprobe];
+    if (p < 0 || p >= n_lists) return;
+    const int tile0 = tile_off[p], nt = min(kSeedTiles, tile_off[p + 1] - tile0);
+    if (nt <= 0) return;
+    const float *qrow = Q + q * d;
+    const float *xt[kSeedTiles];
+#pragma unroll
+    for (int t = 0; t < kSeedTiles; ++t) xt[t] = X + (int64_t)(tile0 + min(t, nt - 1)) * dpad * kTile + lane;
+    float acc[kSeedTiles];
+#pragma unroll
+    for (int t = 0; t < kSeedTiles; ++t) acc[t] = 0.0f;
+    for (int64_t j0 = 0; j0 < d; j0 += 64) {
+        const float qv = j0 + lane < d ? qrow[j0 + lane] : 0.0f;
+        const int nj = (int)min<int64_t>(64, d - j0);
+        if (nj == 64) {
+#pragma unroll 16
+            for (int jj = 0; jj < 64; ++jj) {
+                const float qj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qv), jj));
+#pragma unroll
+                for (int t = 0; t < kSeedTiles; ++t) {
+                    const float xv = xt[t][(j0 + jj) * kTile];
+                    if (METRIC == LIRA_METRIC_L2) {
+                        const float df = qj - xv;
+                        acc[t] = acc[t] + df * df;
+                    } else {
+                        acc[t] = acc[t] + qj * xv;
+                    }
+                }
+            }
+        } else {
+            for (int jj = 0; jj < nj; ++jj) {
+                const float qj = __shfl(qv, jj, 64);
+#pragma unroll
+                for (int t = 0; t < kSeedTiles; ++t) {
+                    const float xv = xt[t][(j0 + jj) * kTile];
+                    if (METRIC == LIRA_METRIC_L2) {
+                        const float df = qj - xv;
+                        acc[t] = acc[t] + df * df;
+                    } else {
+                        acc[t] = acc[t] + qj * xv;
+                    }
+                }
+            }
+        }
+    }
+    float m[4] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};  // 4 smallest
+#pragma unroll
+    for (int u = 0; u < kSeedTiles; ++u) {
+        float sc = METRIC == LIRA_METRIC_L2 ? acc[u] : -acc[u];
+        if (u >= nt || ids[(tile0 + u) * kTile + lane] < 0 || !(sc == sc)) continue;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float lo = fminf(m[i], sc), hi = fmaxf(m[i], sc);
+            m[i] = lo;
+            sc = hi;
+        }
+    }
+    const int t = (k + 63) / 64;
+    if (t > 4) return;
+    const float mine = t == 1 ? m[0] : t == 2 ? m[1] : t == 3 ? m[2] : m[3];
+    const uint32_t sorted = wave_sort64_u32(f2ord(mine));
+    const int j = (k + t - 1) / t;
+    const float B = ord2f((uint32_t)__shfl((int)sorted, j - 1, 64));
+    if (lane == 0 && B < __builtin_inff()) qbound[q] = f2ord(B);
+}
+
 // One workgroup per query, wave w = tile w of its first probed partition.  The
 // tile's 64 rows (contiguous in the row-major copy) are read 32 dims at a time,
 // coalesced (lane l loads 16-B pieces of rows l/8 + 8 i), transposed through a
@@ -1467,20 +2011,23 @@ static int screen_smem(int qr, int rl) {
 
 struct SPlan {
     int rl = 1, qr = 64, K2 = 32, bpc = 1, bpc_near = 1, nch_max = 1, grid = 1, smem = 0, mfma = 1, split = 0;
+    int v2 = 0, ns = 2, bc = 32;  // the pipelined split screen (k_screen_s): ring slots, buffer keys per row
     int64_t max_qblk = 0;
     size_t off_cnt, off_cursor, off_head, off_qoff, off_item, off_nch, off_qblk, off_itab, off_qlist, off_qt, off_qn,
         off_partial, off_qbound, off_pqn, total;
 };
 
-static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k) {
+static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, unsigned flags) {
     SPlan pl;
     const lira_opts &op = idx->opt;
     pl.rl = screen_rl(k);
+    // the split-bf16 screen unless asked off (it is the only one without the fp32 tiles)
+    const bool split_wanted = (op.split && !(flags & LIRA_SCAN_NO_SPLIT)) || !idx->X;
     // MFMA screen where its LDS (64-query lists) still fits 2 workgroups per
     // CU; larger k (RL 4: DEEP10M's k = 100) measured faster on the VALU one,
     // which needs the fp32 tiles (without them: MFMA up to RL 4)
     const int mfma_opt = idx->X ? op.mfma : 2;
-    pl.mfma = mfma_opt == 2 ? pl.rl <= 4 : mfma_opt && pl.rl <= 2;
+    pl.mfma = mfma_opt == 2 ? pl.rl <= 4 : mfma_opt && pl.rl <= (op.pipeline && idx->Xb && split_wanted ? 4 : 2);
     // queries per item of the MFMA screen: 64 (4 waves); 128 (8 waves, k <= 56)
     // halves the L2 -> LDS bytes per FMA but measured slower on every config
     // (SIFT1M 1.10 -> 1.25 ms mixture, 4.45 -> 4.66 ms latent; GIST, BIGANN too)
@@ -1488,9 +2035,27 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     pl.qr = pl.mfma ? (pl.rl <= 2 ? qr_opt : 64) : screen_qr(pl.rl);
     // split-bf16 MFMA screen (k_screen_m<..., SPLIT>) where the index holds Xb;
     // LIRA_OPT_SPLIT = 0 keeps the fp32 MFMA screen (which reads the fp32 tiles)
-    pl.split = (op.split || !idx->X) && pl.mfma && idx->Xb != nullptr;
+    pl.split = split_wanted && pl.mfma && idx->Xb != nullptr;
+    // the pipelined split screen (LIRA_OPT_PIPELINE): RL 1 at 128 queries per item
+    // (8 waves, 4 ring slots, 16-key buffers), RL 2 at 64 (4 slots), RL 4 at 64 (3 slots)
+    // (measured, SIFT1M / GIST1M, k = 10: every ring / QR variant of k_screen_s
+    // slower than k_screen_m's 2-slot ring at 2 workgroups per CU -- its LDS
+    // leaves 1 workgroup per CU; DEEP10M k = 100: 28.1 ms vs 33.4 ms on the VALU
+    // screen), so RL 4 only, unless LIRA_OPT_RING asks for it
+    pl.v2 = pl.split && op.pipeline && (pl.rl == 4 || op.ring > 0);
+    if (pl.v2) {
+        pl.qr = pl.rl == 1 && op.qr != 64 ? 128 : 64;
+        pl.ns = pl.rl == 4 ? 3 : 4;
+        if (op.ring >= 2 && op.ring <= 4 && pl.rl == 1) pl.ns = op.ring;  // (A/B: 64 x 2/4 and 128 x 3/4 built)
+        if (pl.qr == 64 && pl.rl == 1 && pl.ns == 3) pl.ns = 4;
+        if (pl.qr == 128 && pl.ns == 2) pl.ns = 3;
+        pl.bc = pl.qr == 128 && pl.ns == 4 ? 16 : 32;
+    }
     pl.K2 = 32 * pl.rl;
-    pl.smem = !pl.mfma       ? screen_smem(pl.qr, pl.rl)
+    pl.smem = pl.v2 ? (pl.qr == 128 ? (pl.ns == 4 ? SSmem2<128, 1, 4, 16>::total : SSmem2<128, 1, 3, 32>::total)
+                                     : pl.rl == 1 ? (pl.ns == 4 ? SSmem2<64, 1, 4, 32>::total : SSmem2<64, 1, 2, 32>::total)
+                                     : pl.rl == 2 ? SSmem2<64, 2, 4, 32>::total : SSmem2<64, 4, 3, 32>::total)
+              : !pl.mfma       ? screen_smem(pl.qr, pl.rl)
               : pl.qr == 128 ? (pl.rl == 1 ? SSmem<128, 1, true>::total : SSmem<128, 2, true>::total)
               : pl.rl == 1   ? SSmem<64, 1, true>::total
               : pl.rl == 2   ? SSmem<64, 2, true>::total
@@ -1520,6 +2085,10 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
         const int64_t est0 = std::min<int64_t>(nq, (nq + pl.qr - 1) / pl.qr + idx->n_lists);
         const int64_t split0 = std::max<int64_t>(1, ((int64_t)near_rounds * pl.grid + est0 - 1) / std::max<int64_t>(1, est0));
         pl.bpc_near = (int)std::min<int64_t>(pl.bpc, std::max<int64_t>(1, (max_blocks + split0 - 1) / split0));
+    }
+    if (pl.v2 && idx->metric == LIRA_METRIC_L2 && idx->pivot) {  // k_screen_s stages <= kBR block ranges per item
+        pl.bpc = std::min(pl.bpc, SSmem2<64, 1, 4, 32>::kBR);
+        pl.bpc_near = std::min(pl.bpc_near, pl.bpc);
     }
     pl.nch_max = (int)((max_blocks + pl.bpc_near - 1) / pl.bpc_near);
     pl.max_qblk = npairs / pl.qr + std::min<int64_t>(2 * idx->n_lists, npairs) + 1;
@@ -1555,15 +2124,16 @@ bool screen_supported(const lira_index *idx, int64_t k) {
     return idx->X != nullptr || (idx->Xb != nullptr && screen_rl(k) <= 4);
 }
 
-size_t screen_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k) {
-    return make_splan(idx, nq, nprobe, k).total;
+size_t screen_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, unsigned flags) {
+    return make_splan(idx, nq, nprobe, k, flags).total;
 }
 
 // the kernel a screened scan of this shape runs (lira_scan_describe)
 std::string screen_describe(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, unsigned flags) {
-    SPlan pl = make_splan(idx, nq, nprobe, k);
-    if ((flags & LIRA_SCAN_NO_SPLIT) && idx->X) pl.split = 0;
-    std::string s = pl.mfma ? (pl.split ? "k_screen_m split-bf16 v_mfma_f32_16x16x32_bf16"
+    SPlan pl = make_splan(idx, nq, nprobe, k, flags);
+    std::string s = pl.v2 ? "k_screen_s split-bf16 v_mfma_f32_16x16x32_bf16 NS=" + std::to_string(pl.ns) +
+                                " BC=" + std::to_string(pl.bc)
+                    : pl.mfma ? (pl.split ? "k_screen_m split-bf16 v_mfma_f32_16x16x32_bf16"
                                         : "k_screen_m fp32 v_mfma_f32_16x16x4_f32")
                             : "k_screen VALU v_pk_fma_f32";
     s += " RL=" + std::to_string(pl.rl) + " QR=" + std::to_string(pl.qr) + " K2=" + std::to_string(pl.K2) +
@@ -1593,8 +2163,29 @@ static hipError_t launch_screen_m(const ScreenArgs &a, const SPlan &pl, hipStrea
     return hipGetLastError();
 }
 
+template <int M, int RL, int QR, int NS, int BC>
+static hipError_t launch_screen_s(const ScreenArgs &a, const SPlan &pl, hipStream_t st) {
+    constexpr int smem = SSmem2<QR, RL, NS, BC>::total;
+    static_assert(smem <= 160 * 1024, "k_screen_s LDS");
+    constexpr int OCC = (160 * 1024) / smem >= 2 ? 2 : 1;
+    static std::atomic<uint64_t> attr{0};
+    hipError_t e = set_smem_attr_once(attr, (const void *)k_screen_s<M, RL, QR, NS, BC, OCC>, 160 * 1024);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_screen_s<M, RL, QR, NS, BC, OCC>), dim3(pl.grid), dim3(QR * 4), smem, st, a);
+    return hipGetLastError();
+}
+
 template <int M>
 static hipError_t launch_screen_rl(const ScreenArgs &a, const SPlan &pl, hipStream_t st) {
+    if (pl.v2) {
+        if (pl.qr == 128)
+            return pl.ns == 4 ? launch_screen_s<M, 1, 128, 4, 16>(a, pl, st) : launch_screen_s<M, 1, 128, 3, 32>(a, pl, st);
+        switch (pl.rl) {
+            case 1: return pl.ns == 4 ? launch_screen_s<M, 1, 64, 4, 32>(a, pl, st) : launch_screen_s<M, 1, 64, 2, 32>(a, pl, st);
+            case 2: return launch_screen_s<M, 2, 64, 4, 32>(a, pl, st);
+            default: return launch_screen_s<M, 4, 64, 3, 32>(a, pl, st);
+        }
+    }
     if (pl.mfma) {
         if (pl.qr == 128 && pl.split)
             return pl.rl == 1 ? launch_screen_m<M, 1, 128, true>(a, pl, st) : launch_screen_m<M, 2, 128, true>(a, pl, st);
@@ -1636,8 +2227,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
                 size_t ws_bytes, hipStream_t st, hipEvent_t *ev) {
     const bool dedup = (flags & LIRA_SCAN_DEDUP) != 0;
     const bool per_part = (flags & LIRA_SCAN_PER_PARTITION) != 0;
-    SPlan pl = make_splan(idx, nq, nprobe, k);
-    if ((flags & LIRA_SCAN_NO_SPLIT) && idx->X) pl.split = 0;  // (no tiles: the split copy is the only one)
+    SPlan pl = make_splan(idx, nq, nprobe, k, flags);
     if (!ws) {
         if (idx->ws_bytes < pl.total) {
             if (idx->ws) hipFree(idx->ws);
@@ -1709,7 +2299,17 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
                            (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn);
     LIRA_HIP_TRY(hipGetLastError());
     // (measured: SIFT1M mixture 1.70 -> 1.44 ms, latent +1 %)
-    if (qbound && o.seed) {
+    if (qbound && o.seed && idx->X) {  // from the fp32 tiles (coalesced)
+        if (idx->metric == LIRA_METRIC_L2)
+            hipLaunchKernelGGL(k_seed_t<LIRA_METRIC_L2>, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, q, probe,
+                               (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad,
+                               nq, (int)k, qbound);
+        else
+            hipLaunchKernelGGL(k_seed_t<LIRA_METRIC_IP>, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, q, probe,
+                               (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad,
+                               nq, (int)k, qbound);
+        LIRA_HIP_TRY(hipGetLastError());
+    } else if (qbound && o.seed) {  // compact index: from the row-major copy
         if (idx->metric == LIRA_METRIC_L2)
             hipLaunchKernelGGL(k_seed<LIRA_METRIC_L2>, dim3((unsigned)nq), dim3(256), 0, st, q, probe,
                                (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->Xr, idx->d, nq,

@@ -351,13 +351,21 @@ def test_options_do_not_change_results(metric):
     ref = run(idx, q, probe, 10)
     for name, vals in (("qr", (128,)), ("two_phase", (0, 2)), ("seed", (0,)), ("share", (0,)),
                        ("prune", (0,)), ("split", (0,)), ("mfma", (0, 2)), ("rounds", (1, 64)),
-                       ("near_rounds", (8,)), ("screen", (0,))):
+                       ("near_rounds", (8,)), ("screen", (0,)), ("ring", (2, 3, 4))):
         old = idx.get_option(name)
         for v in vals:
             idx.set_option(name, v)
             D, I, nc = run(idx, q, probe, 10)
             assert np.array_equal(I, ref[1]) and np.array_equal(bits(D), bits(ref[0])), (name, v)
         idx.set_option(name, old)
+    # the pipelined screen's ring variants at both query-block sizes
+    for qr, ring in ((64, 2), (64, 4), (128, 3), (128, 4)):
+        idx.set_option("qr", qr)
+        idx.set_option("ring", ring)
+        D, I, nc = run(idx, q, probe, 10)
+        assert np.array_equal(I, ref[1]) and np.array_equal(bits(D), bits(ref[0])), (qr, ring)
+    idx.set_option("qr", 0)
+    idx.set_option("ring", 0)
 
 
 @pytest.mark.parametrize("metric", ["L2", "inner_product"])

@@ -1,0 +1,39 @@
+"""Per-phase cycle split of the screen kernel (LIRA_OPT_DEBUG bit 8: thread 0 of
+every workgroup adds clock64() deltas: item prologue -> stats[1], block loop ->
+stats[3], epilogue -> stats[6]).  Timing experiment only (debug bits 1/2/4 also
+switch off MFMA / selection / staging; results invalid).
+
+usage: python tools/phase_clocks.py <config> <data> <debug bits> [option=value ...]
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lira-ann-search_amd"))
+import torch  # noqa: E402
+
+from lira_amd import PartitionedIndex, rank_nearest  # noqa: E402
+from lira_amd.synthetic import CONFIGS, workload  # noqa: E402
+
+cfg, data, dbg = sys.argv[1], sys.argv[2], int(sys.argv[3])
+opts = dict((a.split("=")[0], int(a.split("=")[1])) for a in sys.argv[4:])
+N, d, B, nprobe, k, metric, nq = CONFIGS[cfg]
+dev = torch.device("cuda", 0)
+x, c, assign, mq = workload(cfg, 1234, dev, data)
+idx = PartitionedIndex(d, metric, 0, **opts).build(assign[:, None] if assign.dim() == 1 else assign, x, B)
+q = mq(nq, 1335)
+probe = rank_nearest(q, c, nprobe)
+for _ in range(3):
+    idx.search(q, probe, k)
+idx.set_option("debug", dbg | 8)
+idx.set_stats(True)
+idx.set_profiling(True)
+idx.search(q, probe, k)
+torch.cuda.synchronize()
+st = idx.stats_read()
+pr = idx.profile_read()
+print(cfg, data, "debug", dbg, opts, "kernel", idx.describe(nq, nprobe, k))
+tot = st["chunks_nominal"] + st["blocks_dropped"] + st["rescans"]
+print("scan_ms %.3f  cycles: prologue %.3g  blocks %.3g  epilogue %.3g  (fractions %.2f / %.2f / %.2f)" % (
+    pr["scan_ms"], st["chunks_nominal"], st["blocks_dropped"], st["rescans"],
+    st["chunks_nominal"] / tot, st["blocks_dropped"] / tot, st["rescans"] / tot))
+print("blocks", st["blocks"], "skipped", st["blocks_skipped"])
