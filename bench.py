@@ -64,6 +64,7 @@ def parse():
     ap.add_argument("--opt", action="append", default=[],
                     help="index option name=value (include/lira_hip.h LIRA_OPT_*), repeatable")
     ap.add_argument("--no-exact", action="store_true", help="skip the all-exact kernel comparison")
+    ap.add_argument("--no-pipeline", action="store_true", help="skip the MLP-probed pipeline timing")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo only to rehearse N>1 on one GPU")
     return ap.parse_args()
@@ -369,8 +370,101 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
             "note": "cores = threads used = the box's allotted CPU share (OMP_NUM_THREADS); nproc counts "
                     "the whole machine; nproc_linear_estimate = single-thread QPS x nproc (not measured)",
             "nproc_linear_estimate_qps": st_qps * (os.cpu_count() or 1)}
+    # ---- the MLP-probed search.cpp pipeline, N = 1 ---------------
+    if primary and world == 1 and B <= 256 and not args.no_pipeline:
+        out["pipeline"] = time_pipeline(args, oracle, index, x, centres, q, make_queries, k, nprobe, metric,
+                                        host, rows, Igt, dev)
     del index, x
     return out
+
+
+def time_pipeline(args, oracle, index, x, centres, q, make_queries, k, nprobe, metric, host, rows, Igt, dev):
+    """search.cpp:424-514 per batch: exact distances + standardise (one HIP
+    kernel) -> MLP_2_Input (PyTorch-ROCm) -> score >= 0.5 with argmax fallback
+    (lira_select_probes) -> scan + top-k, eagerly and as one replayed HIP graph.
+    The MLP is fitted (untimed) to score each query's nprobe nearest centroids,
+    standing in for LIRA's kNN-label training (out of scope)."""
+    from lira_amd import centroid_dist
+    from lira_amd.probing import MLP_2_Input, fit_probe_to_nearest, standard_scaler
+    from lira_amd.search import ProbePipeline
+    nq, d = q.shape
+    B = centres.shape[0]
+    met = oracle.IP if metric == "inner_product" else oracle.L2
+    mean, scale = standard_scaler(centroid_dist(x[:65536].contiguous(), centres))  # data-side (utils.py:120-180)
+    model = MLP_2_Input(B, d, B).to(dev)
+
+    def batch(n, it):
+        qb = make_queries(n, args.seed + 5000 + it)
+        return centroid_dist(qb, centres, mean, scale), qb
+
+    tf = time.perf_counter()
+    fit_probe_to_nearest(model, batch, nprobe, steps=300, batch=4096)
+    fit_s = time.perf_counter() - tf
+    pipe = ProbePipeline(index, centres, mean, scale, model, nq, k, 0.5, dedup=True)
+    pipe.q.copy_(q)
+    pipe.run()
+    torch.cuda.synchronize()
+
+    def timed(fn, n):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / n
+
+    for _ in range(args.warmup):
+        pipe.run()
+    eager_s = timed(pipe.run, args.steps)
+    I_e, D_e = pipe.I.clone(), pipe.D.clone()
+    pipe.capture()
+    for _ in range(args.warmup):
+        pipe.replay()
+    graph_s = timed(pipe.replay, args.steps)
+    same = bool(torch.equal(pipe.I, I_e) and torch.equal(pipe.D.view(torch.int32), D_e.view(torch.int32)))
+    # per-stage device time of one eager pass (events on the current stream)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+    parts = {"distances": 0.0, "mlp": 0.0, "select": 0.0, "scan": 0.0}
+    for _ in range(5):
+        ev[0].record()
+        centroid_dist(pipe.q, pipe.C, pipe.mean, pipe.scale, out=pipe.dist)
+        ev[1].record()
+        with torch.no_grad():
+            pipe.scores = pipe.model(pipe.dist, pipe.q)
+        ev[2].record()
+        from lira_amd import _lib
+        _lib.call("lira_select_probes", _lib.ptr(pipe.scores), nq, B, _lib.LIRA_PROBE_THRESHOLD_GE, 0.5,
+                  pipe.max_probe, _lib.ptr(pipe.probe), _lib.ptr(pipe.nprobe), _lib.stream_ptr())
+        ev[3].record()
+        index.search(pipe.q, pipe.probe, k, dedup=True, out=(pipe.D, pipe.I, pipe.ncand))
+        ev[4].record()
+        torch.cuda.synchronize()
+        for i, name in enumerate(parts):
+            parts[name] += ev[i].elapsed_time(ev[i + 1]) / 5
+    # parity on the sample: distances, probe selection on the pipeline's scores, scan
+    qs = q.cpu().numpy()[rows]
+    dist_o = oracle.centroid_dist(qs, centres.cpu().numpy(), mean.cpu().numpy(), scale.cpu().numpy())
+    dist_ok = bool(np.array_equal(pipe.dist.cpu().numpy()[rows].view(np.uint32), dist_o.view(np.uint32)))
+    sc = pipe.scores.cpu().numpy()[rows]
+    pr, cnt = oracle.probe_threshold(sc, 0.5)
+    sel_ok = bool(np.array_equal(pipe.nprobe.cpu().numpy()[rows], cnt))
+    Ig, Dg = pipe.I.cpu().numpy()[rows], pipe.D.cpu().numpy()[rows]
+    if host is not None:
+        Do, Io, _ = oracle.scan_topk(qs, *host, pr, k, met, index.max_replicas)
+        scan_ok = bool(np.array_equal(Io, Ig) and np.array_equal(Do.view(np.uint32), Dg.view(np.uint32)))
+    else:
+        scan_ok = None
+    recall = float(np.mean([len(set(Ig[i]) & set(Igt[i])) / k for i in range(len(rows))]))
+    npb = pipe.nprobe.float().mean().item()
+    return {"what": "search.cpp:424-514 on the batch: lira_centroid_dist (exact + standardise) -> MLP_2_Input "
+                    "(torch) -> lira_select_probes (>= 0.5, argmax fallback) -> lira_scan_topk",
+            "value_eager": nq / eager_s, "value_graph": nq / graph_s, "unit": "queries/s",
+            "ms_eager": eager_s * 1e3, "ms_graph": graph_s * 1e3, "graph_same_output": same,
+            "stage_ms": parts, "max_probe": pipe.max_probe,
+            "avg_nprobe": npb, "recall_at_k": recall, "parity_sample": int(len(rows)),
+            "parity": {"distances_bit_exact": dist_ok, "probe_selection_exact": sel_ok, "scan_bit_exact": scan_ok},
+            "mlp": f"MLP_2_Input({B}, {d}, {B}) fitted in {fit_s:.1f} s (300 Adam steps) to the nearest-{nprobe} "
+                   f"indicator: synthetic stand-in for LIRA's kNN labels"}
 
 
 def main():
@@ -429,7 +523,7 @@ def main():
                        "parallelism": f"query-shard x{world} (index replicated)"},
             "roofline": head.get("roofline"),
             "cpu_baseline": head.get("cpu_baseline"),
-            **{key: head[key] for key in ("kernels_ms_per_step", "kernel", "index_bytes", "index_options",
+            **{key: head[key] for key in ("kernels_ms_per_step", "kernel", "index_bytes", "index_options", "pipeline",
                                           "rank_gemm", "exact_kernel", "candidates_per_query", "parity_sample",
                                           "parity_bit_exact", "recall_at_k", "recall_gate", "recall_note")
                if key in head},

@@ -52,3 +52,42 @@ def probe_scores(model, dist_scaled: torch.Tensor, q: torch.Tensor, batch: int =
     """Model scores (n, n_bkt) for a whole query batch (model_infer, model_probing.py:135-156)."""
     outs = [model(dist_scaled[s:s + batch], q[s:s + batch]) for s in range(0, q.shape[0], batch)]
     return torch.cat(outs).float() if outs else torch.zeros((0, dist_scaled.shape[1]), device=q.device)
+
+
+def standard_scaler(dist: torch.Tensor):
+    """sklearn StandardScaler.fit over (n, B) distances, as utils.py:139-142 /
+    166-178 save it for search.cpp: per-bucket mean and population std, a zero
+    std replaced by 1 (search.cpp:247 does the same at use)."""
+    d = dist.double()
+    mean = d.mean(0)
+    std = d.std(0, unbiased=False)
+    std = torch.where(std == 0, torch.ones_like(std), std)
+    return mean.float(), std.float()
+
+
+def fit_probe_to_nearest(model: nn.Module, dist_scaled_fn, nprobe: int, steps: int = 300, batch: int = 4096,
+                         lr: float = 2e-3, seed: int = 0) -> nn.Module:
+    """Train MLP_2_Input to score each query's nprobe nearest centroids 1 and
+    the rest 0 (BCE, Adam), from batches dist_scaled_fn(batch, step) ->
+    (standardised distances (n, B), queries (n, d)).
+
+    A synthetic stand-in for LIRA's training on kNN partition labels
+    (model_probing.py:41-54, LIRA_smallscale.py:308-329; training is outside
+    the query-time hot path), so that the MLP-probed pipeline selects a
+    realistic number of partitions at threshold 0.5 instead of a random-init
+    model's arbitrary ones.
+    """
+    torch.manual_seed(seed)
+    opt = torch.optim.Adam(model.parameters(), lr=lr)
+    lossf = nn.BCELoss()
+    model.train()
+    for it in range(steps):
+        xd, xq = dist_scaled_fn(batch, it)
+        kth = torch.topk(xd, nprobe, dim=1, largest=False).values[:, -1:]
+        target = (xd <= kth).float()
+        opt.zero_grad(set_to_none=True)
+        loss = lossf(model(xd, xq), target)
+        loss.backward()
+        opt.step()
+    model.eval()
+    return model

@@ -78,17 +78,31 @@ class SearchEngine:
         self.index.add_lists(offsets, ids, x, rep)
         del x
         self.dedup = dedup  # search.cpp keeps replicated gids twice (Appendix A)
+        self._pipe, self._pipe_key = None, None
 
     def scores(self, q: torch.Tensor) -> torch.Tensor:
         dist = centroid_dist(q, self.centroids, self.mean, self.scale)
         return probe_scores(self.model, dist, q)
 
     def search(self, q, threshold: float, k: int, scores: torch.Tensor | None = None):
-        """One threshold: returns (D, I, nprobe, ncand) device tensors."""
+        """One threshold: returns (D, I, nprobe, ncand) device tensors.
+
+        Without precomputed ``scores`` this runs the ProbePipeline of the
+        batch shape (distances + standardise in one kernel, MLP, select, scan
+        on preallocated buffers; the tensors returned are that pipeline's
+        buffers, valid until the next search of the same shape)."""
         q = q if isinstance(q, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(q))
         q = q.to(self.device, torch.float32).contiguous()
         if scores is None:
-            scores = self.scores(q)
+            key = (q.shape[0], int(k), float(threshold))
+            if self._pipe is None or self._pipe_key != key:
+                self._pipe = ProbePipeline(self.index, self.centroids, self.mean, self.scale, self.model,
+                                           q.shape[0], k, threshold, max_probe=self.n_bkt, dedup=self.dedup)
+                self._pipe_key = key
+            self._pipe.q.copy_(q)
+            self._pipe.run()
+            p = self._pipe
+            return p.D, p.I, p.nprobe, p.ncand
         probe, nprobe = select_probes(scores, "ge", self.n_bkt, threshold)
         D, I, ncand = self.index.search(q, probe, k, dedup=self.dedup)
         return D, I, nprobe, ncand
@@ -115,6 +129,72 @@ class SearchEngine:
                       f"avg_cmp      : {row['avg_cmp']:g}\navg_time(q)  : {row['avg_time']:g} s\n"
                       f"QPS          : {row['qps']:g} q/s\n----------------------------------------")
         return rows
+
+
+class ProbePipeline:
+    """search.cpp's per-query pipeline (search.cpp:424-514) for a fixed batch
+    shape, on preallocated device buffers so the whole chain can be captured in
+    one HIP graph (no allocation, no host synchronisation inside):
+
+        exact query->centroid distances + standardise   lira_centroid_dist (one kernel)
+        probing MLP                                      PyTorch-ROCm (hipBLASLt)
+        score >= thr, argmax fallback                    lira_select_probes
+        scan + exact top-k                               lira_scan_topk
+
+    ``max_probe`` caps the probe list per query (search.cpp has no cap: pass
+    n_bkt for its exact semantics).
+    """
+
+    def __init__(self, index: PartitionedIndex, centroids, scaler_mean, scaler_scale, model, nq: int, k: int,
+                 threshold: float, max_probe: int | None = None, dedup: bool = True):
+        dev = index.device
+        self.index, self.model, self.k, self.thr, self.dedup = index, model, int(k), float(threshold), dedup
+        self.C = torch.as_tensor(centroids, dtype=torch.float32).to(dev).contiguous()
+        self.mean = torch.as_tensor(scaler_mean, dtype=torch.float32).to(dev).contiguous()
+        self.scale = torch.as_tensor(scaler_scale, dtype=torch.float32).to(dev).contiguous()
+        nb = self.C.shape[0]
+        self.max_probe = int(max_probe or nb)
+        self.q = torch.zeros((nq, index.d), dtype=torch.float32, device=dev)
+        self.dist = torch.empty((nq, nb), dtype=torch.float32, device=dev)
+        self.probe = torch.empty((nq, self.max_probe), dtype=torch.int32, device=dev)
+        self.nprobe = torch.empty(nq, dtype=torch.int32, device=dev)
+        self.D = torch.empty((nq, k), dtype=torch.float32, device=dev)
+        self.I = torch.empty((nq, k), dtype=torch.int64, device=dev)
+        self.ncand = torch.empty(nq, dtype=torch.int64, device=dev)
+        self.scores = None
+        self.graph = None
+
+    @torch.no_grad()
+    def run(self):
+        """One pass over self.q (stream-ordered, asynchronous)."""
+        centroid_dist(self.q, self.C, self.mean, self.scale, out=self.dist)
+        self.scores = self.model(self.dist, self.q)
+        self._select_scan()
+
+    def _select_scan(self):
+        from . import _lib
+        with torch.cuda.device(self.q.device):
+            _lib.call("lira_select_probes", _lib.ptr(self.scores), self.q.shape[0], self.C.shape[0],
+                      _lib.LIRA_PROBE_THRESHOLD_GE, self.thr, self.max_probe, _lib.ptr(self.probe),
+                      _lib.ptr(self.nprobe), _lib.stream_ptr())
+        self.index.search(self.q, self.probe, self.k, dedup=self.dedup, out=(self.D, self.I, self.ncand))
+
+    def capture(self):
+        """Record run() into a HIP graph (after one eager warm-up run, so the
+        scan's cached workspace is already sized)."""
+        s = torch.cuda.Stream(device=self.q.device)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self.run()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.run()
+        return self
+
+    def replay(self):
+        self.graph.replay()
 
 
 def main(argv=None) -> int:

@@ -144,3 +144,50 @@ def test_search_engine_mlp_threshold():
     off, ids = oracle.build_csr(d2b, 12)
     Do, Io, _ = oracle.scan_topk(q, off, ids, x[ids], pr, 10, oracle.L2, 0)
     assert np.array_equal(I.cpu().numpy(), Io)
+
+
+def test_probe_pipeline_graph_matches_eager_and_oracle():
+    """The MLP-probed search.cpp pipeline (search.cpp:424-514) on preallocated
+    buffers, eagerly and replayed from one captured HIP graph: identical to
+    each other, and to the oracle given the pipeline's own scores."""
+    from lira_amd import PartitionedIndex
+    from lira_amd.probing import MLP_2_Input, fit_probe_to_nearest, standard_scaler
+    from lira_amd.search import ProbePipeline
+    from lira_amd import centroid_dist
+    x, c, rng = mixture(20000, 32, 16, 7)
+    d2b = oracle.centroid_dist(x, c).argmin(1).astype(np.int32)[:, None]
+    dev = torch.device("cuda", 0)
+    xt, ct = torch.from_numpy(x).to(dev), torch.from_numpy(c).to(dev)
+    idx = PartitionedIndex.from_assignment(xt, torch.from_numpy(d2b).to(dev), 16, "L2")
+    mean, scale = standard_scaler(centroid_dist(xt[:4096], ct))
+    model = MLP_2_Input(16, 32, 16).to(dev)
+
+    def batch(n, it):
+        g = torch.Generator(device=dev).manual_seed(100 + it)
+        qb = ct[torch.randint(0, 16, (n,), generator=g, device=dev)] + 0.35 * torch.randn(
+            (n, 32), generator=g, device=dev)
+        return centroid_dist(qb, ct, mean, scale), qb
+
+    fit_probe_to_nearest(model, batch, 3, steps=60, batch=1024)
+    q = (c[rng.integers(0, 16, 300)] + 0.35 * rng.standard_normal((300, 32), dtype=np.float32)).astype(np.float32)
+    pipe = ProbePipeline(idx, ct, mean, scale, model, 300, 10, 0.5)
+    pipe.q.copy_(torch.from_numpy(q))
+    pipe.run()
+    torch.cuda.synchronize()
+    D0, I0, np0, s0 = pipe.D.clone(), pipe.I.clone(), pipe.nprobe.clone(), pipe.scores.clone()
+    pipe.capture()
+    pipe.D.zero_()
+    pipe.I.zero_()
+    pipe.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(pipe.I, I0) and torch.equal(pipe.D.view(torch.int32), D0.view(torch.int32))
+    assert torch.equal(pipe.nprobe, np0)
+    # oracle: exact standardised distances, select on the pipeline's scores, scan
+    dist_o = oracle.centroid_dist(q, c, mean.cpu().numpy(), scale.cpu().numpy())
+    assert np.array_equal(pipe.dist.cpu().numpy().view(np.uint32), dist_o.view(np.uint32))
+    pr, cnt = oracle.probe_threshold(s0.cpu().numpy(), 0.5)
+    assert np.array_equal(np0.cpu().numpy(), cnt) and 1.0 <= cnt.mean() <= 16
+    off, ids = oracle.build_csr(d2b, 16)
+    Do, Io, _ = oracle.scan_topk(q, off, ids, x[ids], pr, 10, oracle.L2, 1)
+    assert np.array_equal(I0.cpu().numpy(), Io)
+    assert np.array_equal(D0.cpu().numpy().view(np.uint32), Do.view(np.uint32))

@@ -7,7 +7,7 @@ for r in $(seq "$rounds"); do
   for v in "$@"; do
     lib=variants/$v.so; [ "$v" = base ] && lib=lira-ann-search_amd/lira_amd/liblira_hip.so
     LIRA_HIP_LIB=$lib timeout -k 10 200 python bench.py --config "$cfg" --data "$data" --steps 20 --warmup 3 \
-        --no-cpu-baseline --no-exact --contrast none $BENCH_ARGS > gpurun_out/ab_$v.log 2>&1 || { echo "variant $v failed"; tail -5 gpurun_out/ab_$v.log; exit 1; }
+        --no-cpu-baseline --no-exact --no-pipeline --contrast none $BENCH_ARGS > gpurun_out/ab_$v.log 2>&1 || { echo "variant $v failed"; tail -5 gpurun_out/ab_$v.log; exit 1; }
     python3 -c "import json,sys; j=json.loads(open('gpurun_out/ab_$v.log').read().strip().splitlines()[-1]); k=j['kernels_ms_per_step']; \
 print('$cfg/$data', '$v', 'round', $r, 'qps %.0f scan %.3f merge %.3f plan %.3f exact %s' % (j['value'], k['scan'], k['merge'], k['plan'], j['parity_bit_exact']))" \
         | tee -a gpurun_out/ab.txt

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 for v in "$@"; do
   OUT=gpurun_out/pmcab_$v
   mkdir -p $OUT
-  B="python3 bench.py --config $cfg --data $data --no-cpu-baseline --no-exact --contrast none --recall-sample 4 --steps 3 --warmup 1"
+  B="python3 bench.py --config $cfg --data $data --no-cpu-baseline --no-exact --no-pipeline --contrast none --recall-sample 4 --steps 3 --warmup 1"
   lib=variants/$v.so; [ "$v" = base ] && lib=lira-ann-search_amd/lira_amd/liblira_hip.so
   export LIRA_HIP_LIB=$lib
   timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --kernel-trace -d $OUT/sq1 -o run --output-format csv -- $B > $OUT/sq1.log 2>&1

@@ -16,7 +16,7 @@ ARGS="$@"
 OUT=gpurun_out/prof_${TAG}_${CFG}_${DATA}
 mkdir -p $OUT
 export TMPDIR=/tmp
-B="python3 bench.py --config $CFG --data $DATA --no-cpu-baseline --no-exact --contrast none --recall-sample 4 $ARGS"
+B="python3 bench.py --config $CFG --data $DATA --no-cpu-baseline --no-exact --no-pipeline --contrast none --recall-sample 4 $ARGS"
 T=${PROF_TIMEOUT:-240}
 timeout -k 10 $T rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- $B --steps 10 --warmup 2 > $OUT/trace.log 2>&1
 timeout -s KILL $T rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/fetch -o run --output-format csv -- $B --steps 3 --warmup 1 > $OUT/fetch.log 2>&1
