@@ -144,9 +144,12 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
     gdev = dev if args.backend == "nccl" else torch.device("cpu")
     kernel = index.describe(nq, nprobe, k)
 
-    def step():
+    def local_step():
         rank_nearest(q, centres, nprobe, out=probe, workspace=ws)
         index.search(q, probe, k, dedup=True, out=(D, I, ncand), fma=args.fma)
+
+    def step():
+        local_step()
         if world > 1:  # the per-rank top-k of the batch, to every rank (RCCL all-gather)
             if args.scaling == "strong":
                 all_gather_rows(D.to(gdev), nq_job, world)
@@ -188,7 +191,7 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
 
     # ---- scan work counters (one untimed step) ---------------------------------
     index.set_stats(True)
-    step()
+    local_step()  # (rank 0 only from here on: no collectives)
     work = index.stats_read()
     index.set_stats(False)
 
@@ -400,7 +403,7 @@ def time_pipeline(args, oracle, index, x, centres, q, make_queries, k, nprobe, m
     tf = time.perf_counter()
     fit_probe_to_nearest(model, batch, nprobe, steps=300, batch=4096)
     fit_s = time.perf_counter() - tf
-    pipe = ProbePipeline(index, centres, mean, scale, model, nq, k, 0.5, dedup=True)
+    pipe = ProbePipeline(index, centres, mean, scale, model, nq, k, 0.5, dedup=True, expect_probes=nprobe)
     pipe.q.copy_(q)
     pipe.run()
     torch.cuda.synchronize()
@@ -433,7 +436,7 @@ def time_pipeline(args, oracle, index, x, centres, q, make_queries, k, nprobe, m
             pipe.scores = pipe.model(pipe.dist, pipe.q)
         ev[2].record()
         from lira_amd import _lib
-        _lib.call("lira_select_probes", _lib.ptr(pipe.scores), nq, B, _lib.LIRA_PROBE_THRESHOLD_GE, 0.5,
+        _lib.call("lira_select_probes", _lib.ptr(pipe.scores), nq, B, pipe.mode, 0.5,
                   pipe.max_probe, _lib.ptr(pipe.probe), _lib.ptr(pipe.nprobe), _lib.stream_ptr())
         ev[3].record()
         index.search(pipe.q, pipe.probe, k, dedup=True, out=(pipe.D, pipe.I, pipe.ncand))
@@ -447,7 +450,9 @@ def time_pipeline(args, oracle, index, x, centres, q, make_queries, k, nprobe, m
     dist_ok = bool(np.array_equal(pipe.dist.cpu().numpy()[rows].view(np.uint32), dist_o.view(np.uint32)))
     sc = pipe.scores.cpu().numpy()[rows]
     pr, cnt = oracle.probe_threshold(sc, 0.5)
-    sel_ok = bool(np.array_equal(pipe.nprobe.cpu().numpy()[rows], cnt))
+    got = pipe.probe.cpu().numpy()[rows]
+    sel_ok = bool(np.array_equal(pipe.nprobe.cpu().numpy()[rows], cnt) and all(
+        np.array_equal(np.sort(got[i][got[i] >= 0]), pr[i][pr[i] >= 0]) for i in range(len(rows))))
     Ig, Dg = pipe.I.cpu().numpy()[rows], pipe.D.cpu().numpy()[rows]
     if host is not None:
         Do, Io, _ = oracle.scan_topk(qs, *host, pr, k, met, index.max_replicas)
@@ -531,6 +536,7 @@ def main():
         }
         print(json.dumps(line), flush=True)
     if world > 1:
+        dist.barrier()  # (rank 0's untimed legs above run without collectives)
         dist.destroy_process_group()
 
 

@@ -59,6 +59,9 @@ extern "C" {
 #define LIRA_PROBE_NEAREST 0      /* nprobe smallest values, ties -> smaller bucket (IVF nprobe) */
 #define LIRA_PROBE_THRESHOLD_GE 1 /* score >= thr, argmax fallback (search.cpp:447-466) */
 #define LIRA_PROBE_THRESHOLD_GT 2 /* score >  thr, no fallback (LIRA_smallscale.py:206) */
+#define LIRA_PROBE_BY_SCORE 16    /* or-ed into a THRESHOLD mode: the same set, in descending score order
+                                     (ties -> smaller bucket) instead of ascending bucket; truncation at
+                                     max_probe keeps the highest scores; max_probe <= 256 */
 
 typedef struct lira_index lira_index; /* opaque; one handle per device */
 
@@ -141,6 +144,8 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *   LIRA_OPT_DEBUG       timing experiments only (results invalid): bit mask, see lira_screen.hip
  *   LIRA_OPT_PIPELINE    1: the pipelined split screen k_screen_s (default); 0: k_screen_m
  *   LIRA_OPT_RING        k_screen_s ring slots: 0 auto, 2..4
+ *   LIRA_OPT_PROBES_HINT expected valid probes per query when the probe lists are mostly -1
+ *                        padding (a threshold selection padded to B): sizes the work split (0 = nprobe_max)
  */
 #define LIRA_OPT_KEEP_TILES 1
 #define LIRA_OPT_SCREEN 2
@@ -156,6 +161,7 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
 #define LIRA_OPT_DEBUG 12
 #define LIRA_OPT_PIPELINE 13
 #define LIRA_OPT_RING 14
+#define LIRA_OPT_PROBES_HINT 15
 int lira_index_set_option(lira_index *idx, int option, int64_t value);
 int lira_index_get_option(const lira_index *idx, int option, int64_t *value);
 /* 1 if the index holds the fp32 tile copy (LIRA_OPT_KEEP_TILES at build time) */
@@ -205,6 +211,8 @@ int lira_rank_nearest(const float *q, int64_t nq, const float *centroids, int64_
  *                 when none (first max wins) -- search.cpp:447-466.
  *  THRESHOLD_GT:  score > thr, no fallback -- LIRA_smallscale.py:206.
  * Threshold modes truncate at max_probe (pass max_probe = B for no truncation).
+ * | LIRA_PROBE_BY_SCORE: threshold sets ordered by descending score (the scan
+ * then meets each query's most probable partition first; same results).
  */
 int lira_select_probes(const float *scores, int64_t n, int64_t n_centroids, int mode, float thr,
                        int64_t max_probe, int32_t *out_probe, int32_t *out_nprobe, void *stream);

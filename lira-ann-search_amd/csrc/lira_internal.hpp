@@ -47,6 +47,7 @@ struct lira_opts {
     int debug = 0;
     int pipeline = 1;
     int ring = 0;
+    int probes_hint = 0;
 };
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device):

@@ -19,32 +19,63 @@
 namespace lira {
 
 // ---------------------------------------------------------------- exact dist
-// One wave per query, lane = centroid.  Centroids are re-read from L2 (B*d*4
-// bytes, 32 KiB at SIFT/B=64); the query row is wave-uniform.
+// Tiled like a GEMM: a workgroup owns 64 queries x 64 centroids, stages 32-dim
+// slabs of both (coalesced row loads, transposed into LDS), and each thread
+// keeps 4 x 4 pairs' sums -- every one search.cpp's own sequential fp32 sum of
+// fl(q_j - c_j)^2 in j order (no contraction: -ffp-contract=off), then sqrt
+// and the optional standardisation.
 __global__ __launch_bounds__(256) void k_centroid_dist(const float *__restrict__ q, int64_t nq,
                                                        const float *__restrict__ cent, int nb,
                                                        int64_t d, const float *mean,
                                                        const float *scale, float *out) {
-    const int lane = threadIdx.x & 63;
-    const int64_t qi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (qi >= nq) return;
-    const float *qr = q + qi * d;
-    for (int b0 = 0; b0 < nb; b0 += 64) {
-        const int b = b0 + lane;
-        if (b >= nb) break;
-        const float *cr = cent + (int64_t)b * d;
-        float acc = 0.0f;
-        for (int64_t j = 0; j < d; ++j) {
-            float df = qr[j] - cr[j];
-            acc = acc + df * df;
+    __shared__ __attribute__((aligned(16))) float Qs[32][68], Cs[32][68];  // [dim][row], padded
+    const int tid = threadIdx.x;
+    const int64_t q0 = (int64_t)blockIdx.x * 64;
+    const int c0 = blockIdx.y * 64;
+    const int tq = (tid & 15) * 4, tc = (tid >> 4) * 4;
+    float acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = 0.0f;
+    for (int64_t j0 = 0; j0 < d; j0 += 32) {
+        const int nj = (int)min<int64_t>(32, d - j0);
+        for (int i = tid; i < 64 * 32; i += 256) {
+            const int r = i >> 5, jj = i & 31;
+            Qs[jj][r] = q0 + r < nq && jj < nj ? q[(q0 + r) * d + j0 + jj] : 0.0f;
+            Cs[jj][r] = c0 + r < nb && jj < nj ? cent[(int64_t)(c0 + r) * d + j0 + jj] : 0.0f;
         }
-        float r = __fsqrt_rn(acc);
-        if (mean) {
-            float s = scale[b];
-            if (s == 0.0f) s = 1.0f;
-            r = __fdiv_rn(r - mean[b], s);
+        __syncthreads();
+        for (int jj = 0; jj < nj; ++jj) {
+            const float4 qa = *(const float4 *)&Qs[jj][tq];
+            const float4 ca = *(const float4 *)&Cs[jj][tc];
+            const float qv[4] = {qa.x, qa.y, qa.z, qa.w}, cv[4] = {ca.x, ca.y, ca.z, ca.w};
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const float df = qv[a] - cv[b];
+                    acc[a][b] = acc[a][b] + df * df;
+                }
         }
-        out[qi * nb + b] = r;
+        __syncthreads();
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        const int64_t qi = q0 + tq + a;
+        if (qi >= nq) continue;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int cb = c0 + tc + b;
+            if (cb >= nb) continue;
+            float r = __fsqrt_rn(acc[a][b]);
+            if (mean) {
+                float s = scale[cb];
+                if (s == 0.0f) s = 1.0f;
+                r = __fdiv_rn(r - mean[cb], s);
+            }
+            out[qi * nb + cb] = r;
+        }
     }
 }
 
@@ -285,6 +316,63 @@ __global__ __launch_bounds__(256) void k_select_threshold(const float *__restric
     if (out_np && lane == 0) out_np[i] = mm;
 }
 
+// The same selection with the probes ordered by descending score (ties ->
+// smaller bucket) instead of ascending bucket: the set is identical, and the
+// scan -- whose results do not depend on slot order -- then meets each
+// query's most probable partition first (its seed bound and its nearest-slot
+// group; LIRA_PROBE_BY_SCORE).  Truncation at maxp keeps the highest scores.
+template <int R>
+__global__ __launch_bounds__(256) void k_select_threshold_sorted(const float *__restrict__ s, int64_t n, int nb,
+                                                                 float thr, int ge, int maxp, int32_t *out,
+                                                                 int32_t *out_np) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const float *row = s + i * nb;
+    int32_t *o = out + i * maxp;
+    u64 lst[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) lst[r] = kEmptyKey;
+    int m = 0;
+    float best = -__builtin_inff();
+    int bestb = 0x7fffffff;
+    for (int b0 = 0; b0 < nb; b0 += 64) {
+        const int b = b0 + lane;
+        const float v = b < nb ? row[b] : 0.0f;
+        const bool take = b < nb && (ge ? v >= thr : v > thr);
+        m += popc64(__ballot(take));
+        const u64 key = take ? ((u64)(~f2ord(v)) << 32) | (uint32_t)b : kEmptyKey;
+        const u64 tk = wave_list_at<R>(lst, 64 * R - 1);
+        if (__ballot(key < tk)) wave_merge_batch<R>(lst, key);
+        if (b < nb && (v > best || (v == best && b < bestb))) {
+            best = v;
+            bestb = b;
+        }
+    }
+    if (ge && m == 0) {  // argmax fallback, as k_select_threshold
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            float ov = __shfl_xor(best, off, 64);
+            int ob = __shfl_xor(bestb, off, 64);
+            if (ov > best || (ov == best && ob < bestb)) {
+                best = ov;
+                bestb = ob;
+            }
+        }
+        if (bestb == 0x7fffffff || row[0] != row[0]) bestb = 0;
+        for (int e = lane; e < maxp; e += 64) o[e] = e == 0 ? bestb : -1;
+        if (out_np && lane == 0) out_np[i] = 1;
+        return;
+    }
+    const int mm = min(m, maxp);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = r * 64 + lane;
+        if (e < maxp) o[e] = e < mm ? (int32_t)(uint32_t)lst[r] : -1;
+    }
+    if (out_np && lane == 0) out_np[i] = mm;
+}
+
 static int sel_r(int64_t np) { return np <= 64 ? 1 : np <= 128 ? 2 : np <= 256 ? 4 : -1; }
 
 }  // namespace lira
@@ -302,8 +390,10 @@ int lira_centroid_dist(const float *q, int64_t nq, const float *centroids, int64
         return fail(LIRA_EINVAL, "scaler_mean and scaler_scale must both be set or both NULL");
     if (nq == 0) return LIRA_OK;
     if (!q || !centroids || !out) return fail(LIRA_EINVAL, "NULL buffer");
-    hipLaunchKernelGGL(k_centroid_dist, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0,
-                       (hipStream_t)stream, q, nq, centroids, (int)n_centroids, d, scaler_mean,
+    if ((nq + 63) / 64 > INT32_MAX || (n_centroids + 63) / 64 > 65535)
+        return fail(LIRA_EUNSUPPORTED, "too many queries / centroids for one launch");
+    hipLaunchKernelGGL(k_centroid_dist, dim3((unsigned)((nq + 63) / 64), (unsigned)((n_centroids + 63) / 64)),
+                       dim3(256), 0, (hipStream_t)stream, q, nq, centroids, (int)n_centroids, d, scaler_mean,
                        scaler_scale, out);
     LIRA_HIP_TRY(hipGetLastError());
     return LIRA_OK;
@@ -382,6 +472,24 @@ int lira_select_probes(const float *scores, int64_t n, int64_t n_centroids, int 
     if (!scores || !out_probe) return fail(LIRA_EINVAL, "NULL buffer");
     hipStream_t st = (hipStream_t)stream;
     dim3 g((unsigned)((n + 3) / 4));
+    const bool by_score = (mode & LIRA_PROBE_BY_SCORE) != 0;
+    mode &= ~LIRA_PROBE_BY_SCORE;
+    if (by_score && (mode == LIRA_PROBE_THRESHOLD_GE || mode == LIRA_PROBE_THRESHOLD_GT)) {
+        const int R = sel_r(max_probe);
+        if (R < 0) return fail(LIRA_EUNSUPPORTED, "LIRA_PROBE_BY_SCORE supports max_probe <= 256");
+        const int ge = mode == LIRA_PROBE_THRESHOLD_GE ? 1 : 0;
+        if (R == 1)
+            hipLaunchKernelGGL(k_select_threshold_sorted<1>, g, dim3(256), 0, st, scores, n, (int)n_centroids, thr,
+                               ge, (int)max_probe, out_probe, out_nprobe);
+        else if (R == 2)
+            hipLaunchKernelGGL(k_select_threshold_sorted<2>, g, dim3(256), 0, st, scores, n, (int)n_centroids, thr,
+                               ge, (int)max_probe, out_probe, out_nprobe);
+        else
+            hipLaunchKernelGGL(k_select_threshold_sorted<4>, g, dim3(256), 0, st, scores, n, (int)n_centroids, thr,
+                               ge, (int)max_probe, out_probe, out_nprobe);
+        LIRA_HIP_TRY(hipGetLastError());
+        return LIRA_OK;
+    }
     if (mode == LIRA_PROBE_NEAREST) {
         int R = sel_r(max_probe);
         if (R < 0) return fail(LIRA_EUNSUPPORTED, "nearest mode supports max_probe <= 256");

@@ -2067,7 +2067,10 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // the mixture, 4.80 -> 4.66 ms on latent data; 4 and 32 slower overall)
     const int rounds = op.rounds > 0 ? op.rounds : 8;
     const int64_t target = (int64_t)rounds * pl.grid;
-    const int64_t est_items = (npairs + pl.qr - 1) / pl.qr + std::min<int64_t>(idx->n_lists, npairs);
+    // (LIRA_OPT_PROBES_HINT: the probe lists are mostly -1 padding, e.g. a
+    // threshold selection padded to B; size the chunking for the expected pairs)
+    const int64_t npairs_est = op.probes_hint > 0 ? std::min<int64_t>(npairs, nq * op.probes_hint) : npairs;
+    const int64_t est_items = (npairs_est + pl.qr - 1) / pl.qr + std::min<int64_t>(idx->n_lists, npairs_est);
     const int64_t max_blocks = std::max<int64_t>(1, (idx->max_list_tiles + kSBT - 1) / kSBT);
     if (est_items >= target) {
         pl.bpc = (int)max_blocks;

@@ -363,11 +363,12 @@ def rank_nearest(q: torch.Tensor, centroids: torch.Tensor, nprobe: int, out=None
 
 
 def select_probes(scores: torch.Tensor, mode: str, max_probe: int, threshold: float = 0.0,
-                  stream=None):
+                  stream=None, by_score: bool = False):
     """Probe lists from an (n, B) score matrix.
 
     mode "nearest": max_probe smallest; "ge": score >= threshold with argmax
     fallback (search.cpp:447-466); "gt": score > threshold (LIRA_smallscale.py:206).
+    by_score: the threshold set in descending score order (LIRA_PROBE_BY_SCORE).
     Returns (probe (n, max_probe) int32 -1 padded, nprobe (n,) int32).
     """
     modes = {"nearest": _lib.LIRA_PROBE_NEAREST, "ge": _lib.LIRA_PROBE_THRESHOLD_GE,
@@ -376,7 +377,8 @@ def select_probes(scores: torch.Tensor, mode: str, max_probe: int, threshold: fl
     n, nb = s.shape
     probe = torch.empty((n, max_probe), dtype=torch.int32, device=s.device)
     cnt = torch.empty(n, dtype=torch.int32, device=s.device)
+    m = modes[mode] | (_lib.LIRA_PROBE_BY_SCORE if by_score else 0)
     with torch.cuda.device(s.device):
-        _lib.call("lira_select_probes", _lib.ptr(s), n, nb, modes[mode], float(threshold),
+        _lib.call("lira_select_probes", _lib.ptr(s), n, nb, m, float(threshold),
                   int(max_probe), _lib.ptr(probe), _lib.ptr(cnt), _lib.stream_ptr(stream))
     return probe, cnt

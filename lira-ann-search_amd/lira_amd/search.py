@@ -146,7 +146,8 @@ class ProbePipeline:
     """
 
     def __init__(self, index: PartitionedIndex, centroids, scaler_mean, scaler_scale, model, nq: int, k: int,
-                 threshold: float, max_probe: int | None = None, dedup: bool = True):
+                 threshold: float, max_probe: int | None = None, dedup: bool = True,
+                 expect_probes: int | None = None):
         dev = index.device
         self.index, self.model, self.k, self.thr, self.dedup = index, model, int(k), float(threshold), dedup
         self.C = torch.as_tensor(centroids, dtype=torch.float32).to(dev).contiguous()
@@ -163,6 +164,12 @@ class ProbePipeline:
         self.ncand = torch.empty(nq, dtype=torch.int64, device=dev)
         self.scores = None
         self.graph = None
+        # search.cpp's set (>= thr, argmax fallback); ordered by descending score
+        # where the list fits (same results, faster scan: most probable partition first)
+        from . import _lib
+        self.mode = _lib.LIRA_PROBE_THRESHOLD_GE | (_lib.LIRA_PROBE_BY_SCORE if self.max_probe <= 256 else 0)
+        if expect_probes:  # a performance hint for the scan's work split (LIRA_OPT_PROBES_HINT)
+            index.set_option("probes_hint", int(expect_probes))
 
     @torch.no_grad()
     def run(self):
@@ -175,8 +182,8 @@ class ProbePipeline:
         from . import _lib
         with torch.cuda.device(self.q.device):
             _lib.call("lira_select_probes", _lib.ptr(self.scores), self.q.shape[0], self.C.shape[0],
-                      _lib.LIRA_PROBE_THRESHOLD_GE, self.thr, self.max_probe, _lib.ptr(self.probe),
-                      _lib.ptr(self.nprobe), _lib.stream_ptr())
+                      self.mode, self.thr, self.max_probe, _lib.ptr(self.probe), _lib.ptr(self.nprobe),
+                      _lib.stream_ptr())
         self.index.search(self.q, self.probe, self.k, dedup=self.dedup, out=(self.D, self.I, self.ncand))
 
     def capture(self):

@@ -86,3 +86,23 @@ def test_threshold_select(thr):
     wp, wc = oracle.probe_threshold(s, thr, False)
     assert np.array_equal(p.cpu().numpy(), wp[:, :4])
     assert np.array_equal(c.cpu().numpy(), np.minimum(wc, 4))
+
+
+@pytest.mark.parametrize("thr", [0.3, 0.8, 1.5])
+def test_threshold_select_by_score(thr):
+    # LIRA_PROBE_BY_SCORE: search.cpp's set, descending score (ties -> smaller
+    # bucket); truncation keeps the highest scores; argmax fallback as before
+    from lira_amd import select_probes
+    rng = np.random.default_rng(int(thr * 10) + 7)
+    s = np.round(rng.random((200, 150), dtype=np.float32) * 20) / 20  # many exact ties
+    s[3] = 0.1
+    for mode, strict in (("ge", False), ("gt", True)):
+        for maxp in (150, 5):
+            p, c = select_probes(torch.from_numpy(s).cuda(), mode, maxp, thr, by_score=True)
+            p, c = p.cpu().numpy(), c.cpu().numpy()
+            wp, wc = oracle.probe_threshold(s, thr, strict)
+            assert np.array_equal(c, np.minimum(wc, maxp))
+            for i in range(s.shape[0]):
+                sel = wp[i][wp[i] >= 0]
+                want = sorted(sel, key=lambda b: (-s[i, b], b))[:maxp]
+                assert list(p[i][:c[i]]) == want and (p[i][c[i]:] == -1).all()
