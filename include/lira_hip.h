@@ -146,6 +146,9 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *   LIRA_OPT_RING        k_screen_s ring slots: 0 auto, 2..4
  *   LIRA_OPT_PROBES_HINT expected valid probes per query when the probe lists are mostly -1
  *                        padding (a threshold selection padded to B): sizes the work split (0 = nprobe_max)
+ *   LIRA_OPT_XHI         1: the split screen multiplies the query's hi + lo parts by x's hi part only
+ *                        (half the staged bytes and MFMAs, a 2^-8 wider bound, more exact re-checks);
+ *                        0: hi and lo; -1 (default): 1 where d >= 512
  */
 #define LIRA_OPT_KEEP_TILES 1
 #define LIRA_OPT_SCREEN 2
@@ -162,6 +165,7 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
 #define LIRA_OPT_PIPELINE 13
 #define LIRA_OPT_RING 14
 #define LIRA_OPT_PROBES_HINT 15
+#define LIRA_OPT_XHI 16
 int lira_index_set_option(lira_index *idx, int option, int64_t value);
 int lira_index_get_option(const lira_index *idx, int option, int64_t *value);
 /* 1 if the index holds the fp32 tile copy (LIRA_OPT_KEEP_TILES at build time) */

@@ -48,6 +48,7 @@ struct lira_opts {
     int pipeline = 1;
     int ring = 0;
     int probes_hint = 0;
+    int xhi = -1;
 };
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device):

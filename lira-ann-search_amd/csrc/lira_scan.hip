@@ -175,6 +175,47 @@ __global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t
         head[0] = 0;
         head[1] = carry_b;
     }
+    if (!itab) return;
+    // XCD-aware item queues (the screen kernels): virtual partition v belongs to
+    // queue v % 8, queue r holds its partitions' items in v order (group 0, each
+    // query's nearest partition, first) and chunk-major, so the query blocks
+    // that stream one chunk run on one XCD back to back and share its L2.  The
+    // table is rewritten queue by queue: v' = r m + i <-> v = 8 i + r.
+    // head[2 + r]: queue r's claim counter (zeroed by the caller), head[10 + r]:
+    // its start, head[18]: the end of queue 7 (= the item total).
+    __syncthreads();
+    const int m = (n_virt + 7) / 8;
+    if (threadIdx.x == 0) carry_b = 0;
+    __syncthreads();
+    for (int base = 0; base < 8 * m; base += 1024) {
+        const int vv = base + threadIdx.x;
+        const int v = vv < 8 * m ? (vv % m) * 8 + vv / m : n_virt;
+        int items = 0, nqb = 0, nc = 0;
+        if (v < n_virt) {
+            nc = nch[v];
+            nqb = (cnt[v] + qr - 1) / qr;
+            items = nqb * nc;
+        }
+        s_b[threadIdx.x] = items;
+        __syncthreads();
+        for (int off = 1; off < 1024; off <<= 1) {
+            int vb = threadIdx.x >= off ? s_b[threadIdx.x - off] : 0;
+            __syncthreads();
+            s_b[threadIdx.x] += vb;
+            __syncthreads();
+        }
+        const int i0 = carry_b + s_b[threadIdx.x] - items;
+        if (vv < 8 * m && vv % m == 0) head[10 + vv / m] = i0;
+        if (v < n_virt && items) {
+            const int g0 = qblk_off[v];
+            for (int ch = 0; ch < nc; ++ch)
+                for (int qb = 0; qb < nqb; ++qb) itab[i0 + ch * nqb + qb] = make_int4(v, qb, ch, g0 + qb);
+        }
+        __syncthreads();
+        if (threadIdx.x == 1023) carry_b += s_b[1023];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) head[18] = carry_b;
 }
 
 // bucket -> pair ids.  Each block reserves its slice of every bucket once

@@ -112,8 +112,12 @@ __device__ __forceinline__ double err_E(double qnorm, double R, double d, int sp
                                         int centred = 0) {
     const double dl = d * 0x1p-140;
     if (split) {
-        const double ed = (2.0001 * 0x1p-16 + 4.0 * dp * 0x1p-22) * 1.02 * qnorm * R +
-                          4.0 * dp * 0x1p-96 * (qnorm + R + 1.0);
+        // split == 2 (hi-only x, k_screen_m<..., 2>): dot~ = sum (qh + ql) xh, x = xh + ex
+        // with |ex| <= 2^-8 |x_i|: |dot~ - q.x| <= (2^-8 + 2^-16 + 2 dpad 2^-22) 1.02 |q| R
+        const double ed = split == 2 ? (0x1p-8 + 1.0001 * 0x1p-16 + 2.0 * dp * 0x1p-22) * 1.02 * qnorm * R +
+                                           2.0 * dp * 0x1p-96 * (qnorm + R + 1.0)
+                                     : (2.0001 * 0x1p-16 + 4.0 * dp * 0x1p-22) * 1.02 * qnorm * R +
+                                           4.0 * dp * 0x1p-96 * (qnorm + R + 1.0);
         if (METRIC == LIRA_METRIC_L2) {
             const double s = qnorm + R;
             return 2.0 * ed + (1.05 * 8.0 + (centred ? 2.01 : 0.0)) * kU * s * s + dl;
@@ -258,16 +262,18 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
 }
 
 // ---- the screening kernel --------------------------------------------------
-template <int QR, int RL, bool MF = false>  // MF: the k_screen_m carve (xadj stage, block ranges)
+// MF: the k_screen_m carve (xadj stage, block ranges); HV: 16-key survivor
+// buffers and a doubled Q chunk (unused since 32-dim chunks measured no faster)
+template <int QR, int RL, bool MF = false, int HV = 0>
 struct SSmem {
-    static constexpr int RW = QR / 4, K2 = 32 * RL;
+    static constexpr int RW = QR / 4, K2 = 32 * RL, BC = HV ? 16 : 32;
     static constexpr int kXS = kSBT * kSDK * kTile * 4;      // X chunk: 16 KiB
-    static constexpr int kQS = kSDK * QR * 4;                // Q chunk: 4 / 2 KiB
+    static constexpr int kQS = (HV ? 2 : 1) * kSDK * QR * 4; // Q chunk: 4 / 2 KiB (HV: 8 / 4)
     static constexpr int kXA = MF ? kSBT * kTile * 4 : 0;    // the block's xadj (first chunk): 1 KiB
     static constexpr int kStage = kXS + kQS + kXA;
     static constexpr int kX = 2 * kStage;                    // 2-deep ring
     static constexpr int kLists = QR * K2 * 8;
-    static constexpr int kBufs = QR * 32 * 8;
+    static constexpr int kBufs = QR * BC * 8;
     // item; pair, bufc, (spare) per row; block-skip (A, B) x 2 parities and
     // ||q - pivot|| (lo, hi) doubles per row; (MF) the radius range of each of
     // an item's first kBR blocks
@@ -285,6 +291,25 @@ __device__ __forceinline__ void sglds16(const void *gsrc, uint32_t lds_addr) {
         : "=&s"(keep)
         : "v"(gsrc), "s"(lds_addr)
         : "memory");
+}
+
+// XCD-aware work queues (k_plan): claim the next item of this workgroup's own
+// XCD's queue, stealing from the others (in order) once it is empty; -1 when
+// every queue is.  Thread 0 only; xq[9] (LDS) = the queue starts + end, x /
+// tries the claimant's state.
+__device__ __forceinline__ int xcd_id() {
+    unsigned v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+    return (int)(v & 7u);
+}
+__device__ __forceinline__ int claim_item(int32_t *head, const int *xq, int &x, int &tries) {
+    while (tries < 8) {
+        const int i = xq[x] + atomicAdd(&head[2 + x], 1);
+        if (i < xq[x + 1]) return i;
+        x = (x + 1) & 7;
+        ++tries;
+    }
+    return -1;
 }
 
 // acc += x * splat(q.lo) / splat(q.hi) on packed fp32.  Inline asm: hipcc
@@ -420,17 +445,23 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen(ScreenArgs a) {
     const int nchunk = (int)(a.dpad / kSDK);
     const int ti = lane >> 4, col = (lane & 15) * 4;   // this lane's 4 candidates of a block
 
-    int nxt = tid == 0 ? atomicAdd(&a.head[0], 1) : 0;  // thread 0: the claimed next item
+    __shared__ int xq[9];  // the XCD queues' bounds (k_plan)
+    int qx = 0, qtries = 0, nxt = -1;  // thread 0: its queue, the claimed next item
+    if (tid == 0) {
+        for (int r = 0; r < 9; ++r) xq[r] = a.head[10 + r];
+        qx = xcd_id();
+        nxt = claim_item(a.head, xq, qx, qtries);
+    }  // thread 0: the claimed next item
     for (;;) {
         if (tid == 0) {
             // the next item is claimed one item ahead (its atomic completes
             // under this item's work); one table load decodes it
             const int item = nxt;
-            const int ok = item < a.head[1];
+            const int ok = item >= 0;
             int4 e = make_int4(0, 0, 0, 0);
             if (ok) {
                 e = a.itab[item];
-                nxt = atomicAdd(&a.head[0], 1);
+                nxt = claim_item(a.head, xq, qx, qtries);
             }
             meta[0] = ok;
             meta[1] = e.x;
@@ -717,11 +748,18 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // sums qh.(xh + xl) + ql.(xh + xl): 2 MFMAs of 16 cycles where the fp32 form
 // needs 4 of 32, same LDS bytes, B fragments read once for both.  The error
 // model is err_E(split = 1).
-template <int METRIC, int RL, int QR, int OCC, bool SPLIT = false>
+// SPLIT == 2 (LIRA_OPT_XHI): only the hi parts of x are staged and multiplied
+// -- half the bytes and half the MFMAs -- one v_mfma_f32_16x16x32_bf16 per tile
+// and 16 dims taking A = (qh, ql) of the 16 dims against B = (xh, xh); the
+// bound widens by 2^-8 |q| R (err_E(split = 2)), so more candidates reach the
+// exact re-check.
+template <int METRIC, int RL, int QR, int OCC, int SPLIT = 0>
 __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
     constexpr int NW = QR / 16, NT = QR * 4;  // waves of 16 rows each, threads
     typedef SSmem<QR, RL, true> S;
-    constexpr int K2 = S::K2, BC = 32;  // BC: survivor buffer keys per row
+    constexpr int K2 = S::K2, BC = S::BC;  // BC: survivor buffer keys per row
+    constexpr int DK = kSDK;               // dims per staged chunk
+    constexpr int ESPLIT = SPLIT;          // the error model's split mode
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float *Xs = (float *)smem;  // [2] x {X: [4 tiles][16 dims][64], Q: [16 dims][64]}
     u64 *lists = (u64 *)(smem + S::kX);
@@ -741,21 +779,27 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
     const float4 *Xg = (const float4 *)a.X;
     const uint32_t xs_lds = (uint32_t)(uintptr_t)(lds_void_t *)Xs;
     const int tstride = (int)a.dpad * (kTile / 4);
-    const int nchunk = (int)(a.dpad / kSDK);
+    const int nchunk = (int)(a.dpad / DK);
 
     long long t_0 = 0, t_1 = 0, t_2 = 0;  // (a.dbg & 8) phase clocks, thread 0
-    int nxt = tid == 0 ? atomicAdd(&a.head[0], 1) : 0;  // thread 0: the claimed next item
+    __shared__ int xq[9];  // the XCD queues' bounds (k_plan)
+    int qx = 0, qtries = 0, nxt = -1;  // thread 0: its queue, the claimed next item
+    if (tid == 0) {
+        for (int r = 0; r < 9; ++r) xq[r] = a.head[10 + r];
+        qx = xcd_id();
+        nxt = claim_item(a.head, xq, qx, qtries);
+    }  // thread 0: the claimed next item
     for (;;) {
         if ((a.dbg & 8) && tid == 0) t_0 = clock64();
         if (tid == 0) {
             // the next item is claimed one item ahead (its atomic completes
             // under this item's work); one table load decodes it
             const int item = nxt;
-            const int ok = item < a.head[1];
+            const int ok = item >= 0;
             int4 e = make_int4(0, 0, 0, 0);
             if (ok) {
                 e = a.itab[item];
-                nxt = atomicAdd(&a.head[0], 1);
+                nxt = claim_item(a.head, xq, qx, qtries);
             }
             meta[0] = ok;
             meta[1] = e.x;
@@ -789,7 +833,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
         const int my_pair = __float_as_int(qrec.z);
         const int my_q = my_pair >= 0 ? my_pair / a.nprobe : -1;
         const double my_qn = (double)qrec.x, my_qnorm = (double)qrec.y;
-        const double my_E = err_E<METRIC>(my_qnorm, R, dd, SPLIT, (double)a.dpad, a.centred);
+        const double my_E = err_E<METRIC>(my_qnorm, R, dd, ESPLIT, (double)a.dpad, a.centred);
         u64 *my_list = lists + my_row * K2;
         // this lane's 4 output rows 4g + reg: qn for the screened scores
         float qn_r[4];
@@ -802,10 +846,12 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
             const int ntv = min(kSBT, tb_end - tb);
             const uint32_t base = xs_lds + (uint32_t)(slot * S::kStage);
             // X: 16 pieces of 1 KiB per chunk (tile pc >> 2, dims jc + 4(pc & 3)
-            // .. +3); wave w moves pieces w, w + NW, ...
+            // .. +3; split: quarter (pc & 3) = part g); wave w moves pieces w, w + NW, ...
+            // (SPLIT 2: the 8 hi pieces, quarters 0 and 1)
+            constexpr int NP = SPLIT == 2 ? 8 : 16, QSH = SPLIT == 2 ? 1 : 2;
 #pragma unroll
-            for (int m = 0; m < 16 / NW; ++m) {
-                const int pc = wave + NW * m, t = pc >> 2, qq = pc & 3;
+            for (int m = 0; m < NP / NW; ++m) {
+                const int pc = wave + NW * m, t = pc >> QSH, qq = pc & ((1 << QSH) - 1);
                 sglds16(Xg + (int64_t)(tile0 + tb + min(t, ntv - 1)) * tstride + jc * (kTile / 4) + qq * 64 + lane,
                         __builtin_amdgcn_readfirstlane(base + (uint32_t)(t * (kSDK * kTile * 4) + qq * 1024)));
             }
@@ -966,7 +1012,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
                 {
-                    int njc = (c + 1) * kSDK, ntb = tb;
+                    int njc = (c + 1) * DK, ntb = tb;
                     if (c + 1 == nchunk) {
                         njc = 0;
                         ntb = skip_from(tb + kSBT, bi & 1);
@@ -980,7 +1026,20 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                     for (int t = 0; t < 4; ++t)
                         xa[t] = t < ntv ? *(const f4 *)(xs + t * kTile + 4 * cj) : (f4)(__builtin_inff());
                 }
-                if (SPLIT && !wdead && !(a.dbg & 1)) {
+                if (SPLIT == 2 && !wdead && !(a.dbg & 1)) {
+                    const char *sb = (const char *)Xs + slot * S::kStage;
+                    const bf16x8 aq = *(const bf16x8 *)(sb + S::kXS + ((g * QR + wave * 16 + cj) << 4));
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        bf16x8 bv[4];
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            bv[i] = *(const bf16x8 *)(sb + t * (kSDK * kTile * 4) + (((g & 1) * 64 + i * 16 + cj) << 4));
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            acc[t * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq, bv[i], acc[t * 4 + i], 0, 0, 0);
+                    }
+                } else if (SPLIT && !wdead && !(a.dbg & 1)) {
                     const char *sb = (const char *)Xs + slot * S::kStage;
                     const bf16x8 a_hi = *(const bf16x8 *)(sb + S::kXS + (((g & 1) * QR + wave * 16 + cj) << 4));
                     const bf16x8 a_lo = *(const bf16x8 *)(sb + S::kXS + (((2 + (g & 1)) * QR + wave * 16 + cj) << 4));
@@ -1085,7 +1144,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                     const float B = ord2f((uint32_t)__shfl((int)key16, 16 * g + j - 1, 64));
                     if (h == -__builtin_inff() && B < __builtin_inff()) {
                         const double qnorm_r = (double)__shfl((float)my_qnorm, 4 * g + reg, 64);
-                        const double E_r = err_E<METRIC>(qnorm_r, R, dd, SPLIT, (double)a.dpad, a.centred);
+                        const double E_r = err_E<METRIC>(qnorm_r, R, dd, ESPLIT, (double)a.dpad, a.centred);
                         h = row_h<METRIC>(s_lim<METRIC>(bound_P<METRIC>((double)B, E_r, dd), E_r, dd),
                                           (double)qn_r[reg], qnorm_r, R);
                         int pm2 = 0;
@@ -1154,7 +1213,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
         for (int r = 0; r < 16; ++r) {
             const int row = wave * 16 + r;
             const int bc = m_bufc[row];
-            if (bc > 0) s_flush<RL>(lists + row * K2, bufs + row * 32, bc);
+            if (bc > 0) s_flush<RL>(lists + row * K2, bufs + row * BC, bc);
             const int pr = m_pair[row];
             if (pr >= 0) {
                 u64 *dst = a.partial + ((int64_t)pr * a.nch_max + ch) * K2;
@@ -1273,15 +1332,21 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_s(ScreenArgs a) {
     const int tstride = (int)a.dpad * (kTile / 4);
     const int dpad = (int)a.dpad;
 
-    int nxt = tid == 0 ? atomicAdd(&a.head[0], 1) : 0;  // thread 0: the claimed next item
+    __shared__ int xq[9];  // the XCD queues' bounds (k_plan)
+    int qx = 0, qtries = 0, nxt = -1;  // thread 0: its queue, the claimed next item
+    if (tid == 0) {
+        for (int r = 0; r < 9; ++r) xq[r] = a.head[10 + r];
+        qx = xcd_id();
+        nxt = claim_item(a.head, xq, qx, qtries);
+    }  // thread 0: the claimed next item
     for (;;) {
         if (tid == 0) {
             const int item = nxt;
-            const int ok = item < a.head[1];
+            const int ok = item >= 0;
             int4 e = make_int4(0, 0, 0, 0);
             if (ok) {
                 e = a.itab[item];
-                nxt = atomicAdd(&a.head[0], 1);
+                nxt = claim_item(a.head, xq, qx, qtries);
             }
             meta[0] = ok;
             meta[1] = e.x;
@@ -2036,6 +2101,11 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // split-bf16 MFMA screen (k_screen_m<..., SPLIT>) where the index holds Xb;
     // LIRA_OPT_SPLIT = 0 keeps the fp32 MFMA screen (which reads the fp32 tiles)
     pl.split = split_wanted && pl.mfma && idx->Xb != nullptr;
+    // hi-only x (LIRA_OPT_XHI): k_screen_m at 64 queries per item
+    // (default on at dpad >= 512: GIST1M scan + merge 1.45 -> 1.30 ms mixture, 1.98
+    // -> 1.88 latent; SIFT1M slower, 0.71 -> 0.73 / 2.45 -> 2.57: more re-checks)
+    const int xhi = op.xhi >= 0 ? op.xhi : idx->dpad >= 512;
+    if (pl.split && xhi && pl.qr == 64 && !(op.pipeline && (pl.rl == 4 || op.ring > 0))) pl.split = 2;
     // the pipelined split screen (LIRA_OPT_PIPELINE): RL 1 at 128 queries per item
     // (8 waves, 4 ring slots, 16-key buffers), RL 2 at 64 (4 slots), RL 4 at 64 (3 slots)
     // (measured, SIFT1M / GIST1M, k = 10: every ring / QR variant of k_screen_s
@@ -2104,7 +2174,7 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     const size_t nl = 2 * (size_t)idx->n_lists;  // up to two groups of virtual partitions
     pl.off_cnt = take(nl * 4);
     pl.off_cursor = take(nl * 4);
-    pl.off_head = take(16);
+    pl.off_head = take(32 * 4);  // [0..1] totals, [2..9] XCD queue counters, [10..18] queue bounds
     pl.off_qoff = take((nl + 1) * 4);
     pl.off_item = take((nl + 1) * 4);
     pl.off_nch = take(nl * 4);
@@ -2136,7 +2206,8 @@ std::string screen_describe(const lira_index *idx, int64_t nq, int64_t nprobe, i
     SPlan pl = make_splan(idx, nq, nprobe, k, flags);
     std::string s = pl.v2 ? "k_screen_s split-bf16 v_mfma_f32_16x16x32_bf16 NS=" + std::to_string(pl.ns) +
                                 " BC=" + std::to_string(pl.bc)
-                    : pl.mfma ? (pl.split ? "k_screen_m split-bf16 v_mfma_f32_16x16x32_bf16"
+                    : pl.mfma ? (pl.split == 2 ? "k_screen_m hi-x split-bf16 v_mfma_f32_16x16x32_bf16"
+                                 : pl.split ? "k_screen_m split-bf16 v_mfma_f32_16x16x32_bf16"
                                         : "k_screen_m fp32 v_mfma_f32_16x16x4_f32")
                             : "k_screen VALU v_pk_fma_f32";
     s += " RL=" + std::to_string(pl.rl) + " QR=" + std::to_string(pl.qr) + " K2=" + std::to_string(pl.K2) +
@@ -2148,20 +2219,20 @@ template <int M, int RL, int QR>
 static hipError_t launch_screen(const ScreenArgs &a, const SPlan &pl, hipStream_t st) {
     constexpr int OCC = (160 * 1024) / SSmem<QR, RL>::total >= 2 ? 2 : 1;
     static std::atomic<uint64_t> attr{0};
-    hipError_t e = set_smem_attr_once(attr, (const void *)k_screen<M, RL, QR, OCC>, 160 * 1024);
+    constexpr int smem = SSmem<QR, RL>::total;  // (+ the kernel's small static LDS)
+    hipError_t e = set_smem_attr_once(attr, (const void *)k_screen<M, RL, QR, OCC>, smem);
     if (e != hipSuccess) return e;
-    constexpr int smem = SSmem<QR, RL>::total;
     hipLaunchKernelGGL((k_screen<M, RL, QR, OCC>), dim3(pl.grid), dim3(kSThreads), smem, st, a);
     return hipGetLastError();
 }
 
-template <int M, int RL, int QR, bool SPLIT = false>
+template <int M, int RL, int QR, int SPLIT = 0>
 static hipError_t launch_screen_m(const ScreenArgs &a, const SPlan &pl, hipStream_t st) {
     constexpr int OCC = (160 * 1024) / SSmem<QR, RL, true>::total >= 2 ? 2 : 1;
     static std::atomic<uint64_t> attr{0};
-    hipError_t e = set_smem_attr_once(attr, (const void *)k_screen_m<M, RL, QR, OCC, SPLIT>, 160 * 1024);
+    constexpr int smem = SSmem<QR, RL, true>::total;  // (+ the kernel's small static LDS)
+    hipError_t e = set_smem_attr_once(attr, (const void *)k_screen_m<M, RL, QR, OCC, SPLIT>, smem);
     if (e != hipSuccess) return e;
-    constexpr int smem = SSmem<QR, RL, true>::total;
     hipLaunchKernelGGL((k_screen_m<M, RL, QR, OCC, SPLIT>), dim3(pl.grid), dim3(QR * 4), smem, st, a);
     return hipGetLastError();
 }
@@ -2172,7 +2243,7 @@ static hipError_t launch_screen_s(const ScreenArgs &a, const SPlan &pl, hipStrea
     static_assert(smem <= 160 * 1024, "k_screen_s LDS");
     constexpr int OCC = (160 * 1024) / smem >= 2 ? 2 : 1;
     static std::atomic<uint64_t> attr{0};
-    hipError_t e = set_smem_attr_once(attr, (const void *)k_screen_s<M, RL, QR, NS, BC, OCC>, 160 * 1024);
+    hipError_t e = set_smem_attr_once(attr, (const void *)k_screen_s<M, RL, QR, NS, BC, OCC>, smem);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_screen_s<M, RL, QR, NS, BC, OCC>), dim3(pl.grid), dim3(QR * 4), smem, st, a);
     return hipGetLastError();
@@ -2191,12 +2262,17 @@ static hipError_t launch_screen_rl(const ScreenArgs &a, const SPlan &pl, hipStre
     }
     if (pl.mfma) {
         if (pl.qr == 128 && pl.split)
-            return pl.rl == 1 ? launch_screen_m<M, 1, 128, true>(a, pl, st) : launch_screen_m<M, 2, 128, true>(a, pl, st);
+            return pl.rl == 1 ? launch_screen_m<M, 1, 128, 1>(a, pl, st) : launch_screen_m<M, 2, 128, 1>(a, pl, st);
+        if (pl.split == 2) switch (pl.rl) {
+            case 1: return launch_screen_m<M, 1, 64, 2>(a, pl, st);
+            case 2: return launch_screen_m<M, 2, 64, 2>(a, pl, st);
+            default: return launch_screen_m<M, 4, 64, 2>(a, pl, st);
+        }
         if (pl.qr == 128) return pl.rl == 1 ? launch_screen_m<M, 1, 128>(a, pl, st) : launch_screen_m<M, 2, 128>(a, pl, st);
         if (pl.split) switch (pl.rl) {
-            case 1: return launch_screen_m<M, 1, 64, true>(a, pl, st);
-            case 2: return launch_screen_m<M, 2, 64, true>(a, pl, st);
-            default: return launch_screen_m<M, 4, 64, true>(a, pl, st);
+            case 1: return launch_screen_m<M, 1, 64, 1>(a, pl, st);
+            case 2: return launch_screen_m<M, 2, 64, 1>(a, pl, st);
+            default: return launch_screen_m<M, 4, 64, 1>(a, pl, st);
         }
         switch (pl.rl) {
             case 1: return launch_screen_m<M, 1, 64>(a, pl, st);
