@@ -63,6 +63,9 @@ def parse():
                          "(reported as contrast_data, outside the headline's timed region)")
     ap.add_argument("--opt", action="append", default=[],
                     help="index option name=value (include/lira_hip.h LIRA_OPT_*), repeatable")
+    ap.add_argument("--sweep", action="append", default=[],
+                    help="name=v1,v2,...: after the timed run, re-time the step with each value of an index "
+                         "option (include/lira_hip.h LIRA_OPT_*) on the same index and batch (rank 0, N=1)")
     ap.add_argument("--no-exact", action="store_true", help="skip the all-exact kernel comparison")
     ap.add_argument("--no-pipeline", action="store_true", help="skip the MLP-probed pipeline timing")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -206,6 +209,9 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
         e1.record(s)
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / reps
+
+    if args.sweep and world == 1:
+        out["sweep"] = sweep_options(args, index, local_step, D, I, nq, nprobe, k)
 
     out["kernels_ms_per_step"]["rank_nearest"] = event_ms(
         lambda: rank_nearest(q, centres, nprobe, out=probe, workspace=ws))
@@ -379,6 +385,47 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
                                         host, rows, Igt, dev)
     del index, x
     return out
+
+
+def sweep_options(args, index, local_step, D, I, nq, nprobe, k):
+    """Per option value: scan/merge/plan ms (HIP events, `args.steps` steps) and
+    whether the batch's output is bit-identical to the default run's."""
+    D0, I0 = D.clone(), I.clone()
+    rows = []
+    variants = []  # "a=1,2" -> two variants; "a=1 b=2" -> one variant setting both
+    for spec in args.sweep:
+        sets = [t.partition("=") for t in spec.split()]
+        if len(sets) == 1:
+            variants += [[(sets[0][0], int(v))] for v in sets[0][2].split(",")]
+        else:
+            variants.append([(n, int(v)) for n, _, v in sets])
+    for var in variants:
+        old = [(n, index.get_option(n)) for n, _ in var]
+        for n, v in var:
+            index.set_option(n, v)
+        tag = " ".join(f"{n}={v}" for n, v in var)
+        try:
+            local_step()
+            torch.cuda.synchronize()
+            index.set_profiling(True)
+            for _ in range(args.steps):
+                local_step()
+            torch.cuda.synchronize()
+            pr = index.profile_read()
+            index.set_profiling(False)
+            c = max(1, pr["calls"])
+            row = {"options": tag, "kernel": index.describe(nq, nprobe, k),
+                   "scan_ms": pr["scan_ms"] / c, "merge_ms": pr["merge_ms"] / c, "plan_ms": pr["plan_ms"] / c,
+                   "same_output": bool(torch.equal(I, I0) and torch.equal(D.view(torch.int32), D0.view(torch.int32)))}
+        except RuntimeError as e:
+            index.set_profiling(False)
+            row = {"options": tag, "error": str(e)[:200]}
+        log(f"sweep {tag}: {row}")
+        rows.append(row)
+        for n, v in old:
+            index.set_option(n, v)
+    local_step()
+    return rows
 
 
 def time_pipeline(args, oracle, index, x, centres, q, make_queries, k, nprobe, metric, host, rows, Igt, dev):

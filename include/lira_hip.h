@@ -149,6 +149,10 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *   LIRA_OPT_XHI         1: the split screen multiplies the query's hi + lo parts by x's hi part only
  *                        (half the staged bytes and MFMAs, a 2^-8 wider bound, more exact re-checks);
  *                        0: hi and lo; -1 (default): 1 where d >= 512
+ *   LIRA_OPT_ORDER       (build time: set before lira_index_add_partitions) 1 (default, L2): store
+ *                        each list's rows by ascending distance to the list's pivot, so tile radius
+ *                        ranges are narrow and the triangle-inequality skip drops more; 0: list order.
+ *                        Results never depend on it.
  */
 #define LIRA_OPT_KEEP_TILES 1
 #define LIRA_OPT_SCREEN 2
@@ -166,6 +170,7 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
 #define LIRA_OPT_RING 14
 #define LIRA_OPT_PROBES_HINT 15
 #define LIRA_OPT_XHI 16
+#define LIRA_OPT_ORDER 17
 int lira_index_set_option(lira_index *idx, int option, int64_t value);
 int lira_index_get_option(const lira_index *idx, int option, int64_t *value);
 /* 1 if the index holds the fp32 tile copy (LIRA_OPT_KEEP_TILES at build time) */

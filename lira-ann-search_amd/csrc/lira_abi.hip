@@ -7,6 +7,8 @@
 #include <string>
 #include <vector>
 
+#include <hipcub/hipcub.hpp>
+
 #include "lira_device.hpp"
 #include "lira_internal.hpp"
 
@@ -100,6 +102,46 @@ __global__ __launch_bounds__(256) void k_pivot_final(int64_t d, const int32_t *s
     for (int g = seg_first[b]; g < seg_first[b + 1]; ++g) s += psum[(int64_t)g * d + j];
     const int64_t n = list_off[b + 1] - list_off[b];
     pivot[(int64_t)b * d + j] = n > 0 ? (float)(s / (double)n) : 0.0f;
+}
+
+// The same pivot read straight from x through the list's ids (list order):
+// the radius-ordered build (LIRA_OPT_ORDER) needs it before the row gather.
+__global__ __launch_bounds__(256) void k_pivot_partial_ids(const float *x, int64_t d, const int32_t *list_ids,
+                                                           const int32_t *seg_list, const int32_t *seg_first,
+                                                           const int64_t *list_off, double *psum) {
+    const int s = blockIdx.x, b = seg_list[s];
+    const int64_t j = (int64_t)blockIdx.y * blockDim.x + threadIdx.x;
+    if (j >= d) return;
+    const int64_t n = list_off[b + 1] - list_off[b];
+    const int64_t r0 = (int64_t)(s - seg_first[b]) * kPivSeg, r1 = min(n, r0 + kPivSeg);
+    const int32_t *ids = list_ids + list_off[b];
+    double acc = 0.0;
+#pragma unroll 8
+    for (int64_t r = r0; r < r1; ++r) acc += (double)x[(int64_t)ids[r] * d + j];
+    psum[(int64_t)s * d + j] = acc;
+}
+
+// Sort key of every list entry for the radius-ordered build: the bits of
+// fl(||x - pivot||) (non-negative floats order as their bits), one thread per
+// entry; its list by binary search over the offsets.
+__global__ __launch_bounds__(256) void k_entry_radius(const float *x, int64_t d, const int32_t *list_ids,
+                                                      const int64_t *list_off, int64_t n_lists, const float *pivot,
+                                                      int64_t total, uint32_t *key) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t lo = 0, hi = n_lists;  // list_off[lo] <= i < list_off[hi]
+        while (hi - lo > 1) {
+            const int64_t m = (lo + hi) >> 1;
+            if (list_off[m] <= i) lo = m; else hi = m;
+        }
+        const float *row = x + (int64_t)list_ids[i] * d, *pv = pivot + lo * d;
+        double s = 0.0;
+        for (int64_t j = 0; j < d; ++j) {
+            const double df = (double)row[j] - (double)pv[j];
+            s = __builtin_fma(df, df, s);
+        }
+        key[i] = __float_as_uint((float)__builtin_sqrt(s));
+    }
 }
 
 // Radius bounds of every tile: lane r of a wave = row r of the tile.
@@ -385,8 +427,16 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
                                      " bytes for the lists failed");
     }
     int64_t *d_loff = nullptr;
-    int32_t *d_tlist = nullptr, *d_bad = nullptr, *d_seg = nullptr, *d_segf = nullptr;
+    int32_t *d_tlist = nullptr, *d_bad = nullptr, *d_seg = nullptr, *d_segf = nullptr, *d_sorted = nullptr;
+    uint32_t *d_key = nullptr, *d_key2 = nullptr;
+    void *d_tmp = nullptr;
     double *d_psum = nullptr;
+    const bool l2 = idx->metric == LIRA_METRIC_L2 && tiles > 0;
+    // radius-ordered lists (LIRA_OPT_ORDER, L2): a list's rows stored by
+    // ascending ||x - pivot||, so a tile's radius range is narrow and the
+    // triangle-inequality skip can drop it (results do not depend on the order)
+    const bool order = l2 && idx->opt.order && total > 0;
+    const unsigned dy = (unsigned)((d + 255) / 256);
     int rc = LIRA_OK;
     do {
         if (hipMalloc(&d_loff, (n_lists + 1) * 8) != hipSuccess ||
@@ -418,9 +468,60 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
                 break;
             }
         }
+        if (l2) {  // pivot (mean of a list's rows, double) and tile radius arrays
+            if (hipMalloc(&idx->pivot, (size_t)n_lists * d * 4) != hipSuccess ||
+                hipMalloc(&idx->tstat, (size_t)tiles * sizeof(float2)) != hipSuccess ||
+                hipMalloc(&d_seg, (size_t)std::max<int64_t>(segs, 1) * 4) != hipSuccess ||
+                hipMalloc(&d_segf, (size_t)(n_lists + 1) * 4) != hipSuccess ||
+                hipMalloc(&d_psum, (size_t)std::max<int64_t>(segs, 1) * d * 8) != hipSuccess) {
+                rc = fail(LIRA_ENOMEM, "hipMalloc of the pivot / tile radius arrays failed");
+                break;
+            }
+            e = hipMemcpyAsync(d_seg, seg_list.data(), (size_t)segs * 4, hipMemcpyHostToDevice, st);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(d_segf, seg_first.data(), (size_t)(n_lists + 1) * 4, hipMemcpyHostToDevice, st);
+            if (e != hipSuccess) {
+                rc = fail(LIRA_EHIP, std::string("upload failed: ") + hipGetErrorString(e));
+                break;
+            }
+        }
+        const int32_t *gather_ids = list_ids;
+        if (order) {
+            // pivots from x in list order, then a stable segmented radix sort of
+            // each list's ids by radius (ties keep list order)
+            if (segs > 0)
+                hipLaunchKernelGGL(k_pivot_partial_ids, dim3((unsigned)segs, dy), dim3(256), 0, st, x, d, list_ids,
+                                   d_seg, d_segf, d_loff, d_psum);
+            hipLaunchKernelGGL(k_pivot_final, dim3((unsigned)n_lists, dy), dim3(256), 0, st, d, d_segf, d_loff,
+                               d_psum, idx->pivot);
+            size_t tb = 0;
+            if (hipMalloc(&d_key, (size_t)total * 4) != hipSuccess ||
+                hipMalloc(&d_key2, (size_t)total * 4) != hipSuccess ||
+                hipMalloc(&d_sorted, (size_t)total * 4) != hipSuccess) {
+                rc = fail(LIRA_ENOMEM, "hipMalloc of the radius-order scratch failed (LIRA_OPT_ORDER = 0 skips it)");
+                break;
+            }
+            hipLaunchKernelGGL(k_entry_radius, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 65536)),
+                               dim3(256), 0, st, x, d, list_ids, d_loff, n_lists, idx->pivot, total, d_key);
+            e = hipGetLastError();
+            if (e == hipSuccess)
+                e = hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb, d_key, d_key2, list_ids, d_sorted,
+                                                                 (int)total, (int)n_lists, d_loff, d_loff + 1, 0, 32,
+                                                                 st);
+            if (e == hipSuccess) e = hipMalloc(&d_tmp, std::max<size_t>(tb, 1));
+            if (e == hipSuccess)
+                e = hipcub::DeviceSegmentedRadixSort::SortPairs(d_tmp, tb, d_key, d_key2, list_ids, d_sorted,
+                                                                 (int)total, (int)n_lists, d_loff, d_loff + 1, 0, 32,
+                                                                 st);
+            if (e != hipSuccess) {
+                rc = fail(LIRA_EHIP, std::string("radius order failed: ") + hipGetErrorString(e));
+                break;
+            }
+            gather_ids = d_sorted;
+        }
         if (tiles > 0) {
             const int grid = (int)std::min<int64_t>(tiles, 65536);
-            hipLaunchKernelGGL(k_row_gather, dim3(grid), dim3(256), 0, st, x, d, list_ids, d_loff, idx->tile_off,
+            hipLaunchKernelGGL(k_row_gather, dim3(grid), dim3(256), 0, st, x, d, gather_ids, d_loff, idx->tile_off,
                                d_tlist, tiles, idx->Xr, idx->ids);
         }
         e = hipGetLastError();
@@ -447,25 +548,14 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
                                d, d_tlist, tiles, idx->metric, idx->xadj, idx->rmax);
             e = hipGetLastError();
         }
-        if (e == hipSuccess && idx->metric == LIRA_METRIC_L2) {
-            if (hipMalloc(&idx->pivot, (size_t)n_lists * d * 4) != hipSuccess ||
-                hipMalloc(&idx->tstat, (size_t)tiles * sizeof(float2)) != hipSuccess ||
-                hipMalloc(&d_seg, (size_t)std::max<int64_t>(segs, 1) * 4) != hipSuccess ||
-                hipMalloc(&d_segf, (size_t)(n_lists + 1) * 4) != hipSuccess ||
-                hipMalloc(&d_psum, (size_t)std::max<int64_t>(segs, 1) * d * 8) != hipSuccess) {
-                rc = fail(LIRA_ENOMEM, "hipMalloc of the pivot / tile radius arrays failed");
-                break;
-            }
-            e = hipMemcpyAsync(d_seg, seg_list.data(), (size_t)segs * 4, hipMemcpyHostToDevice, st);
-            if (e == hipSuccess)
-                e = hipMemcpyAsync(d_segf, seg_first.data(), (size_t)(n_lists + 1) * 4, hipMemcpyHostToDevice, st);
-            const unsigned dy = (unsigned)((d + 255) / 256);
-            if (e == hipSuccess && segs > 0)
+        if (e == hipSuccess && l2) {
+            if (!order && segs > 0)
                 hipLaunchKernelGGL(k_pivot_partial, dim3((unsigned)segs, dy), dim3(256), 0, st, idx->Xr, d, d_seg,
                                    d_segf, idx->tile_off, d_loff, d_psum);
-            if (e == hipSuccess) {
-                hipLaunchKernelGGL(k_pivot_final, dim3((unsigned)n_lists, dy), dim3(256), 0, st, d, d_segf, d_loff,
-                                   d_psum, idx->pivot);
+            {
+                if (!order)
+                    hipLaunchKernelGGL(k_pivot_final, dim3((unsigned)n_lists, dy), dim3(256), 0, st, d, d_segf,
+                                       d_loff, d_psum, idx->pivot);
                 hipLaunchKernelGGL(k_tile_stats, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, idx->Xr,
                                    idx->ids, d, d_tlist, idx->pivot, tiles, idx->tstat);
                 e = hipGetLastError();
@@ -523,6 +613,10 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
     if (d_seg) hipFree(d_seg);
     if (d_segf) hipFree(d_segf);
     if (d_psum) hipFree(d_psum);
+    if (d_key) hipFree(d_key);
+    if (d_key2) hipFree(d_key2);
+    if (d_sorted) hipFree(d_sorted);
+    if (d_tmp) hipFree(d_tmp);
     if (rc != LIRA_OK) {
         free_storage(idx);
         return rc;
@@ -591,6 +685,7 @@ int lira_index_set_option(lira_index *idx, int option, int64_t value) {
         case LIRA_OPT_RING: if (!in(0, 4)) break; o.ring = v; return LIRA_OK;
         case LIRA_OPT_PROBES_HINT: if (!in(0, 1 << 20)) break; o.probes_hint = v; return LIRA_OK;
         case LIRA_OPT_XHI: if (!in(-1, 1)) break; o.xhi = v; return LIRA_OK;
+        case LIRA_OPT_ORDER: if (!in(0, 1)) break; o.order = v; return LIRA_OK;
         default: return fail(LIRA_EINVAL, "unknown option " + std::to_string(option));
     }
     return fail(LIRA_EINVAL, "value " + std::to_string(value) + " out of range for option " + std::to_string(option));
@@ -616,6 +711,7 @@ int lira_index_get_option(const lira_index *idx, int option, int64_t *value) {
         case LIRA_OPT_RING: *value = o.ring; break;
         case LIRA_OPT_PROBES_HINT: *value = o.probes_hint; break;
         case LIRA_OPT_XHI: *value = o.xhi; break;
+        case LIRA_OPT_ORDER: *value = o.order; break;
         default: return fail(LIRA_EINVAL, "unknown option " + std::to_string(option));
     }
     return LIRA_OK;

@@ -49,6 +49,7 @@ struct lira_opts {
     int ring = 0;
     int probes_hint = 0;
     int xhi = -1;
+    int order = 1;
 };
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device):

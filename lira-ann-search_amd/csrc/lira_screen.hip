@@ -262,16 +262,18 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
 }
 
 // ---- the screening kernel --------------------------------------------------
-// MF: the k_screen_m carve (xadj stage, block ranges); HV: 16-key survivor
-// buffers and a doubled Q chunk (unused since 32-dim chunks measured no faster)
-template <int QR, int RL, bool MF = false, int HV = 0>
+// MF: the k_screen_m carve (xadj stage, block ranges); XH: hi-only x
+// (k_screen_m<..., SPLIT = 2>): half the X bytes per chunk and a 3-deep ring
+template <int QR, int RL, bool MF = false, bool XH = false>
 struct SSmem {
-    static constexpr int RW = QR / 4, K2 = 32 * RL, BC = HV ? 16 : 32;
-    static constexpr int kXS = kSBT * kSDK * kTile * 4;      // X chunk: 16 KiB
-    static constexpr int kQS = (HV ? 2 : 1) * kSDK * QR * 4; // Q chunk: 4 / 2 KiB (HV: 8 / 4)
-    static constexpr int kXA = MF ? kSBT * kTile * 4 : 0;    // the block's xadj (first chunk): 1 KiB
+    static constexpr int RW = QR / 4, K2 = 32 * RL, BC = 32;
+    static constexpr int kXT = (XH ? 2 : 4) * 1024;         // one tile's chunk (XH: the hi parts)
+    static constexpr int kXS = kSBT * kXT;                  // X chunk: 16 KiB (XH: 8)
+    static constexpr int kQS = kSDK * QR * 4;               // Q chunk: 4 KiB at QR = 64
+    static constexpr int kXA = MF ? kSBT * kTile * 4 : 0;   // the block's xadj (first chunk): 1 KiB
     static constexpr int kStage = kXS + kQS + kXA;
-    static constexpr int kX = 2 * kStage;                    // 2-deep ring
+    static constexpr int NSL = XH ? 3 : 2;                  // ring slots
+    static constexpr int kX = NSL * kStage;
     static constexpr int kLists = QR * K2 * 8;
     static constexpr int kBufs = QR * BC * 8;
     // item; pair, bufc, (spare) per row; block-skip (A, B) x 2 parities and
@@ -756,7 +758,8 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 template <int METRIC, int RL, int QR, int OCC, int SPLIT = 0>
 __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
     constexpr int NW = QR / 16, NT = QR * 4;  // waves of 16 rows each, threads
-    typedef SSmem<QR, RL, true> S;
+    typedef SSmem<QR, RL, true, SPLIT == 2> S;
+    constexpr int NSL = S::NSL;  // ring slots: 3 for hi-only x, else 2
     constexpr int K2 = S::K2, BC = S::BC;  // BC: survivor buffer keys per row
     constexpr int DK = kSDK;               // dims per staged chunk
     constexpr int ESPLIT = SPLIT;          // the error model's split mode
@@ -782,6 +785,9 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
     const int nchunk = (int)(a.dpad / DK);
 
     long long t_0 = 0, t_1 = 0, t_2 = 0;  // (a.dbg & 8) phase clocks, thread 0
+    long long t_ref = 0, t_chk = 0, t_sel = 0, t_x = 0, n_slow = 0;  // (a.dbg & 8) block-loop split
+    const bool clk = (a.dbg & 8) && tid == 0;
+    unsigned long long *const cnt = (a.dbg & 8) ? nullptr : a.stats;  // work counters (off while timing)
     __shared__ int xq[9];  // the XCD queues' bounds (k_plan)
     int qx = 0, qtries = 0, nxt = -1;  // thread 0: its queue, the claimed next item
     if (tid == 0) {
@@ -841,26 +847,30 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
         for (int reg = 0; reg < 4; ++reg) qn_r[reg] = __shfl((float)my_qn, 4 * g + reg, 64);
 
         const float4 *qtg = (const float4 *)(a.QT + (int64_t)gqb * a.dpad * QR);
-        auto stage = [&](int tb, int jc, int slot) {
-            if (a.dbg & 4) return;  // timing experiment: no loads
+        // returns the DMA instructions this wave issued (the ring's vmcnt waits count them)
+        auto stage = [&](int tb, int jc, int slot) -> int {
+            if (a.dbg & 4) return 0;  // timing experiment: no loads
             const int ntv = min(kSBT, tb_end - tb);
             const uint32_t base = xs_lds + (uint32_t)(slot * S::kStage);
             // X: 16 pieces of 1 KiB per chunk (tile pc >> 2, dims jc + 4(pc & 3)
             // .. +3; split: quarter (pc & 3) = part g); wave w moves pieces w, w + NW, ...
-            // (SPLIT 2: the 8 hi pieces, quarters 0 and 1)
+            // (SPLIT 2: the 8 hi pieces, quarters 0 and 1, tile stride 2 KiB)
             constexpr int NP = SPLIT == 2 ? 8 : 16, QSH = SPLIT == 2 ? 1 : 2;
 #pragma unroll
             for (int m = 0; m < NP / NW; ++m) {
                 const int pc = wave + NW * m, t = pc >> QSH, qq = pc & ((1 << QSH) - 1);
                 sglds16(Xg + (int64_t)(tile0 + tb + min(t, ntv - 1)) * tstride + jc * (kTile / 4) + qq * 64 + lane,
-                        __builtin_amdgcn_readfirstlane(base + (uint32_t)(t * (kSDK * kTile * 4) + qq * 1024)));
+                        __builtin_amdgcn_readfirstlane(base + (uint32_t)(t * S::kXT + qq * 1024)));
             }
             // Q: QR/16 pieces of 1 KiB, one per wave
             sglds16(qtg + (int64_t)jc * (QR / 4) + wave * 64 + lane,
                     __builtin_amdgcn_readfirstlane(base + (uint32_t)S::kXS + (uint32_t)wave * 1024u));
-            if (jc == 0 && wave == 0)  // the block's xadj rides along (tiles past its end: masked on read)
+            if (jc == 0 && wave == 0) {  // the block's xadj rides along (tiles past its end: masked on read)
                 sglds16(a.xadj + (int64_t)(tile0 + tb + min(lane >> 4, ntv - 1)) * kTile + (lane & 15) * 4,
                         __builtin_amdgcn_readfirstlane(base + (uint32_t)(S::kXS + S::kQS)));
+                return NP / NW + 2;
+            }
+            return NP / NW + 1;
         };
 
         // Triangle-inequality block skip (L2), as k_scan: ||q - x|| >= |
@@ -890,6 +900,11 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
         // of one query -- the chunks of its nearest partition above all --
         // prune with each other's progress
         uint32_t own_pub = ~0u;
+        // Rb: the block's bound on ||x'|| (centred split screen with tile radius
+        // ranges: max ||x - c|| over its tiles, widened for fl(x - c)), else the
+        // list's R; the block's test threshold uses its own error bound Eb <= E
+        // (a row's list bound P keeps the list-wide E: its keys come from every block)
+        double Rb = R, Eb = my_E;
         auto refresh = [&](int par) {
             const u64 kk = my_list[k - 1];
             double T = kk == kEmptyKey ? __builtin_inf() : bound_P<METRIC>((double)key_score(kk), my_E, dd);
@@ -907,7 +922,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                 T = fmin(T, (double)ord2f(pub));
             }
             const float h = my_pair < 0 ? __builtin_inff()
-                                        : row_h<METRIC>(s_lim<METRIC>(T, my_E, dd), my_qn, my_qnorm, R);
+                                        : row_h<METRIC>(s_lim<METRIC>(T, Eb, dd), my_qn, my_qnorm, Rb);
             if (TRI && lane < 16) {
                 float2 ab = make_float2(-__builtin_inff(), __builtin_inff());  // never skip
                 const double F = 1.0 - (dd + 4.0) * kU;
@@ -970,7 +985,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                     float lo, hi;
                     block_range(t, lo, hi);
                     if (!__all((hi < ab.x || lo > ab.y) && (hi < ab2.x || lo > ab2.y))) break;
-                    if (a.stats && tid == 0) atomicAdd(a.stats + 4, 1ull);
+                    if (cnt && tid == 0) atomicAdd(cnt + 4, 1ull);
                     t += kSBT;
                 }
             }
@@ -984,12 +999,45 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
             __syncthreads();
             tb = skip_from(tb_begin, 1);
         }
-        if (tb < tb_end) stage(tb, 0, 0);
+        // The ring (NSL slots): the issuer stages chunk (itb, ijc) NSL - 1 chunks
+        // ahead of the consumer, crossing into the next unskipped block with the
+        // current block's skip intervals (looser than later ones: safe); the
+        // blocks it enters queue up for the consumer (at most 2: nchunk >= 2).
+        int itb = tb, ijc = 0, islot = 0, par_i = 1;
+        int q_n = 0, q_0 = tb_end, q_1 = tb_end;  // queued block starts
+        int n_cur = 0, n_nxt = 0;                 // this wave's DMAs of the chunks after the consumer's
+        auto issue = [&]() -> int {
+            if (itb >= tb_end) return 0;
+            const int n = stage(itb, ijc * DK, islot);
+            islot = islot + 1 == NSL ? 0 : islot + 1;
+            if (++ijc == nchunk) {
+                ijc = 0;
+                itb = skip_from(itb + kSBT, par_i);
+                if (q_n == 0) q_0 = itb; else q_1 = itb;
+                ++q_n;
+            }
+            return n;
+        };
+        n_cur = issue();
+        if (NSL == 3) n_nxt = issue();
 
         if ((a.dbg & 8) && tid == 0) t_1 = clock64();
+        auto pop = [&]() {  // the next block the issuer entered
+            const int v = q_0;
+            q_0 = q_1;
+            --q_n;
+            return v;
+        };
 #pragma unroll 1
-        for (int bi = 0, next_tb = tb_end; tb < tb_end; tb = next_tb, ++bi) {
+        for (int bi = 0; tb < tb_end; ++bi, tb = pop()) {
+            if (clk) t_x = clock64();
             const int ntv = min(kSBT, tb_end - tb);
+            float blo = 0.0f, bhi = 0.0f;
+            if (TRI) block_range(tb, blo, bhi);
+            if (TRI && SPLIT && a.centred) {
+                Rb = fmin(R, (double)bhi * (1.0 + 0x1p-20));
+                Eb = Rb < R ? err_E<METRIC>(my_qnorm, Rb, dd, ESPLIT, (double)a.dpad, a.centred) : my_E;
+            }
             const float h_l = refresh(bi & 1);
             f4 xa[4];  // xadj of my 16 candidates: tile t, i = 0..3 (+inf: padding / past the block);
                        // read from the ring at chunk 0 (staged with it)
@@ -997,28 +1045,38 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
             // computes nothing for it
             bool wdead = !__any(lane < 16 && my_pair >= 0);
             if (TRI && !wdead) {
-                float lo, hi;
-                block_range(tb, lo, hi);
                 const float2 ab = tri_s[(bi & 1) * QR + wave * 16 + cj];
-                wdead = __all(hi < ab.x || lo > ab.y);
+                wdead = __all(bhi < ab.x || blo > ab.y);
             }
 
             f4v acc[16];
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[i] = (f4v)(0.0f);
+            if (clk) {
+                const long long t = clock64();
+                t_ref += t - t_x;
+                t_x = t;
+            }
 
+            par_i = bi & 1;  // the issuer's skip test uses this block's intervals
 #pragma unroll 1
             for (int c = 0; c < nchunk; ++c) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                {
-                    int njc = (c + 1) * DK, ntb = tb;
-                    if (c + 1 == nchunk) {
-                        njc = 0;
-                        ntb = skip_from(tb + kSBT, bi & 1);
-                        next_tb = ntb;
-                    }
-                    if (ntb < tb_end) stage(ntb, njc, slot ^ 1);
+                // this chunk's DMAs landed (the ones issued after it may stay in
+                // flight: vmcnt counts this wave's vector-memory ops in order)
+                if (NSL == 3 && n_nxt > 0) {
+                    if (n_nxt >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                    else if (n_nxt == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+                    else if (n_nxt == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                    else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                __syncthreads();  // ... in every wave; and the slot issued next is free
+                n_cur = n_nxt;
+                n_nxt = issue();
+                if (NSL == 2) {
+                    n_cur = n_nxt;
+                    n_nxt = 0;
                 }
                 if (c == 0) {
                     const float *xs = (const float *)((const char *)Xs + slot * S::kStage + S::kXS + S::kQS);
@@ -1034,7 +1092,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                         bf16x8 bv[4];
 #pragma unroll
                         for (int i = 0; i < 4; ++i)
-                            bv[i] = *(const bf16x8 *)(sb + t * (kSDK * kTile * 4) + (((g & 1) * 64 + i * 16 + cj) << 4));
+                            bv[i] = *(const bf16x8 *)(sb + t * S::kXT + (((g & 1) * 64 + i * 16 + cj) << 4));
 #pragma unroll
                         for (int i = 0; i < 4; ++i)
                             acc[t * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq, bv[i], acc[t * 4 + i], 0, 0, 0);
@@ -1073,11 +1131,16 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                         }
                     }
                 }
-                slot ^= 1;
+                slot = slot + 1 == NSL ? 0 : slot + 1;
             }
-            if (a.stats && lane == 0) {
-                if (wave == 0) atomicAdd(a.stats + 2, 1ull);
-                if (!wdead) atomicAdd(a.stats + 0, 16ull * kSBT * kTile);  // (row, candidate) pairs screened
+            if (cnt && lane == 0) {
+                if (wave == 0) atomicAdd(cnt + 2, 1ull);
+                if (!wdead) atomicAdd(cnt + 0, 16ull * kSBT * kTile);  // (row, candidate) pairs screened
+            }
+            if (clk) {
+                const long long t = clock64();
+                t_chk += t - t_x;
+                t_x = t;
             }
             if (wdead || (a.dbg & 2)) continue;
 
@@ -1107,6 +1170,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                 const float m05 = fmaxf(fmaxf(wv[12], wv[13]), wv[14]);
                 const float mx = fmaxf(fmaxf(fmaxf(m01, m02), m03), fmaxf(fmaxf(m04, m05), wv[15]));
                 if (!__any(mx >= h)) continue;  // wave-uniform: none of the four rows has a candidate
+                if (clk) ++n_slow;
                 int pm = 0;  // passing candidates (padding, xadj = +inf, never)
 #pragma unroll
                 for (int i = 0; i < 16; ++i) pm |= (wv[i] >= h && xa[i >> 2][i & 3] != __builtin_inff()) << i;
@@ -1144,9 +1208,10 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                     const float B = ord2f((uint32_t)__shfl((int)key16, 16 * g + j - 1, 64));
                     if (h == -__builtin_inff() && B < __builtin_inff()) {
                         const double qnorm_r = (double)__shfl((float)my_qnorm, 4 * g + reg, 64);
-                        const double E_r = err_E<METRIC>(qnorm_r, R, dd, ESPLIT, (double)a.dpad, a.centred);
+                        // (bound from this block's keys: its own error bound serves both)
+                        const double E_r = err_E<METRIC>(qnorm_r, Rb, dd, ESPLIT, (double)a.dpad, a.centred);
                         h = row_h<METRIC>(s_lim<METRIC>(bound_P<METRIC>((double)B, E_r, dd), E_r, dd),
-                                          (double)qn_r[reg], qnorm_r, R);
+                                          (double)qn_r[reg], qnorm_r, Rb);
                         int pm2 = 0;
 #pragma unroll
                         for (int i = 0; i < 16; ++i) pm2 |= (acc[i][reg] - xa[i >> 2][i & 3] >= h) << i;
@@ -1200,11 +1265,12 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                     }
                     if (cj == 0) {
                         m_bufc[row] = total <= BC ? total : total - BC * ((total - 1) / BC);
-                        if (a.stats && rowtot) atomicAdd(a.stats + 7, (unsigned long long)rowtot);
+                        if (cnt && rowtot) atomicAdd(cnt + 7, (unsigned long long)rowtot);
                     }
                     __builtin_amdgcn_wave_barrier();
                 }
             }
+            if (clk) t_sel += clock64() - t_x;
         }
 
         if ((a.dbg & 8) && tid == 0) t_2 = clock64();
@@ -1234,6 +1300,13 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
             atomicAdd(a.stats + 1, (unsigned long long)(t_1 - t_0));
             atomicAdd(a.stats + 3, (unsigned long long)(t_2 - t_1));
             atomicAdd(a.stats + 6, (unsigned long long)(t_3 - t_2));
+            // the block loop's split (wave 0): refresh + skip test, chunk loop
+            // (staging + MFMA), selection (blocks that reach it), slow-path regs
+            atomicAdd(a.stats + 0, (unsigned long long)t_ref);
+            atomicAdd(a.stats + 2, (unsigned long long)t_chk);
+            atomicAdd(a.stats + 4, (unsigned long long)t_sel);
+            atomicAdd(a.stats + 7, (unsigned long long)n_slow);
+            t_ref = t_chk = t_sel = n_slow = 0;
         }
     }
 }
@@ -2127,11 +2200,14 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
                                      : pl.rl == 2 ? SSmem2<64, 2, 4, 32>::total : SSmem2<64, 4, 3, 32>::total)
               : !pl.mfma       ? screen_smem(pl.qr, pl.rl)
               : pl.qr == 128 ? (pl.rl == 1 ? SSmem<128, 1, true>::total : SSmem<128, 2, true>::total)
+              : pl.split == 2 ? (pl.rl == 1 ? SSmem<64, 1, true, true>::total
+                                 : pl.rl == 2 ? SSmem<64, 2, true, true>::total : SSmem<64, 4, true, true>::total)
               : pl.rl == 1   ? SSmem<64, 1, true>::total
               : pl.rl == 2   ? SSmem<64, 2, true>::total
                              : SSmem<64, 4, true>::total;
     const int64_t npairs = nq * nprobe;
     pl.grid = cu_count_s(idx->device) * std::max(1, std::min(2, (160 * 1024) / pl.smem));
+    if (op.debug & 32) pl.grid = cu_count_s(idx->device);  // timing experiment: one workgroup per CU
     // ~8 items per workgroup: fewer item prologues/epilogues and row lists to
     // merge than k_scan's 16 (measured: SIFT1M scan + merge 1.47 -> 1.22 ms on
     // the mixture, 4.80 -> 4.66 ms on latent data; 4 and 32 slower overall)
@@ -2158,6 +2234,13 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
         const int64_t est0 = std::min<int64_t>(nq, (nq + pl.qr - 1) / pl.qr + idx->n_lists);
         const int64_t split0 = std::max<int64_t>(1, ((int64_t)near_rounds * pl.grid + est0 - 1) / std::max<int64_t>(1, est0));
         pl.bpc_near = (int)std::min<int64_t>(pl.bpc, std::max<int64_t>(1, (max_blocks + split0 - 1) / split0));
+    }
+    // k_screen_m stages the radius ranges of an item's first kBR blocks in LDS; a
+    // longer item would read them from global memory inside the ring (whose
+    // compiler-inserted waits drain it): cap the chunk at kBR blocks
+    if (!pl.v2 && pl.mfma && idx->metric == LIRA_METRIC_L2 && idx->pivot) {
+        pl.bpc = std::min(pl.bpc, SSmem<64, 1, true>::kBR);
+        pl.bpc_near = std::min(pl.bpc_near, pl.bpc);
     }
     if (pl.v2 && idx->metric == LIRA_METRIC_L2 && idx->pivot) {  // k_screen_s stages <= kBR block ranges per item
         pl.bpc = std::min(pl.bpc, SSmem2<64, 1, 4, 32>::kBR);
@@ -2228,9 +2311,9 @@ static hipError_t launch_screen(const ScreenArgs &a, const SPlan &pl, hipStream_
 
 template <int M, int RL, int QR, int SPLIT = 0>
 static hipError_t launch_screen_m(const ScreenArgs &a, const SPlan &pl, hipStream_t st) {
-    constexpr int OCC = (160 * 1024) / SSmem<QR, RL, true>::total >= 2 ? 2 : 1;
+    constexpr int OCC = (160 * 1024) / SSmem<QR, RL, true, SPLIT == 2>::total >= 2 ? 2 : 1;
     static std::atomic<uint64_t> attr{0};
-    constexpr int smem = SSmem<QR, RL, true>::total;  // (+ the kernel's small static LDS)
+    constexpr int smem = SSmem<QR, RL, true, SPLIT == 2>::total;  // (+ the kernel's small static LDS)
     hipError_t e = set_smem_attr_once(attr, (const void *)k_screen_m<M, RL, QR, OCC, SPLIT>, smem);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_screen_m<M, RL, QR, OCC, SPLIT>), dim3(pl.grid), dim3(QR * 4), smem, st, a);

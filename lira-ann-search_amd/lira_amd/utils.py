@@ -15,8 +15,9 @@ Differences, all deliberate and documented in DESIGN.md:
 * distances are fp32 in search.cpp's sequential order (scipy's cdist works in
   float64 and casts; the two agree to ~1 ulp of the float32 result);
 * get_cmp_recall runs ONE batched scan of every bucket for every query instead
-  of n_bkt x n_q single-query faiss calls; the per-(query, bucket) wall time it
-  returns is that batch's time apportioned by bucket size;
+  of n_bkt x n_q single-query faiss calls; the per-(query, bucket) time it
+  returns is measured per bucket (one event-timed launch of the batch against
+  each bucket) and split evenly over the batch's queries;
 * a bucket with fewer than k vectors yields -1 labels (the reference indexes
   with -1 and wraps to the bucket's last id, LIRA_smallscale.py:169);
 * equal distances order by smaller id (faiss: heap order).
@@ -110,32 +111,66 @@ def create_inner_indexes(x_d, cluster_ids, cfg) -> BucketIndexes:
     return create_flat_indexes(x_d, cluster_ids, cfg, dis_metric=getattr(cfg, "dis_metric", "L2"))
 
 
-def get_cmp_recall(inner_indexes: BucketIndexes, x_q, xd_id_bkt, cfg, query_batch: int = 4096):
+def get_cmp_recall(inner_indexes: BucketIndexes, x_q, xd_id_bkt, cfg, query_batch: int = 4096,
+                   timing: str = "bucket"):
     """Top-k of every bucket for every query (LIRA_smallscale.py:145-174).
 
     Returns (search_time (nq, B) seconds, cmp_distr_all (nq, B) int,
     found_aknn_id (nq, B, k) int64 global ids, -1 where a bucket has < k rows).
+
+    The ids come from one batched PER_PARTITION scan.  search_time, which the
+    reference measures per (query, bucket) call (:167-172):
+    * ``timing="bucket"`` (default): every bucket is scanned again on its own --
+      one launch of the query batch against that bucket alone, timed with HIP
+      events on the launch stream -- and its time is split evenly over the
+      batch's queries (each does the same work there: |bucket| distances and a
+      top-k).  Measured per bucket, not per query.
+    * ``timing="apportion"``: the batched scan's time split by bucket size
+      (no extra launches).
     """
+    if timing not in ("bucket", "apportion"):
+        raise ValueError(f"timing must be 'bucket' or 'apportion', not {timing!r}")
     index = inner_indexes.index
     n_bkt, k = index.n_lists, int(cfg.k)
     q = _cuda(x_q)
     nq = q.shape[0]
     sizes = np.asarray(index.list_sizes, dtype=np.int64)
     found = np.full((nq, n_bkt, k), -1, dtype=np.int64)
+    search_time = np.zeros((nq, n_bkt))
     probe_all = torch.arange(n_bkt, dtype=torch.int32, device=q.device)
     elapsed = 0.0
     for s in range(0, nq, query_batch):
         qs = q[s:s + query_batch]
-        probe = probe_all.expand(qs.shape[0], n_bkt).contiguous()
+        nb = qs.shape[0]
+        probe = probe_all.expand(nb, n_bkt).contiguous()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         _, I, _ = index.search(qs, probe, k, dedup=False, per_partition=True)
         torch.cuda.synchronize()
         elapsed += time.perf_counter() - t0
-        found[s:s + qs.shape[0]] = I.cpu().numpy()
+        found[s:s + nb] = I.cpu().numpy()
+        if timing == "bucket":
+            stream = torch.cuda.current_stream()
+            one = torch.empty((nb, 1), dtype=torch.int32, device=q.device)
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(n_bkt)]
+            one.fill_(0)
+            index.search(qs, one, k, dedup=False, per_partition=True)  # (warm: workspace, plans)
+            for b in range(n_bkt):
+                if sizes[b] == 0:
+                    continue
+                one.fill_(b)
+                ev[b][0].record(stream)
+                index.search(qs, one, k, dedup=False, per_partition=True)
+                ev[b][1].record(stream)
+            torch.cuda.synchronize()
+            for b in range(n_bkt):
+                if sizes[b]:
+                    search_time[s:s + nb, b] = ev[b][0].elapsed_time(ev[b][1]) * 1e-3 / nb
     cmp_distr_all = np.broadcast_to(sizes, (nq, n_bkt)).astype(int)
-    per_cand = elapsed / max(1, int(sizes.sum()) * nq)
-    search_time = cmp_distr_all * per_cand
+    if timing == "apportion":
+        per_cand = elapsed / max(1, int(sizes.sum()) * nq)
+        search_time = cmp_distr_all * per_cand
     return search_time, cmp_distr_all, found
 
 

@@ -44,6 +44,12 @@ def test_get_cmp_recall_and_bucket_views():
     assert [v.ntotal for v in inner] == [len(b) for b in cluster_ids]
     t, cmp_, found = get_cmp_recall(inner, q, cluster_ids, cfg)
     assert t.shape == (60, 12) and (cmp_ == np.array([len(b) for b in cluster_ids])).all()
+    # measured per bucket (one timed launch each), the same for every query of the batch
+    assert (t > 0).all() and np.allclose(t, t[:1]) and (t < 1.0).all()
+    t2, _, found2 = get_cmp_recall(inner, q, cluster_ids, cfg, timing="apportion")
+    assert np.array_equal(found2, found) and (t2 > 0).all()
+    with pytest.raises(ValueError):
+        get_cmp_recall(inner, q, cluster_ids, cfg, timing="per-query")
     off = np.zeros(13, np.int64)
     off[1:] = np.cumsum([len(b) for b in cluster_ids])
     ids = np.concatenate([np.asarray(b, np.int32) for b in cluster_ids])

@@ -178,11 +178,23 @@ def test_device_csr_builder_matches_search_cpp():
     x = rng.standard_normal((n, 12), dtype=np.float32)
     d2b = rng.integers(-1, b, (n, 3)).astype(np.int32)
     d2b[::7, 1] = d2b[::7, 0]  # a bucket repeated inside a row (search.cpp:384 uniques it)
-    idx = PartitionedIndex(12, "L2").build(torch.from_numpy(d2b).cuda(), torch.from_numpy(x).cuda(), b)
     off, ids = oracle.build_csr(d2b, b)
+    # list order (LIRA_OPT_ORDER = 0): exactly search.cpp's CSR
+    idx0 = PartitionedIndex(12, "L2", order=0).build(torch.from_numpy(d2b).cuda(), torch.from_numpy(x).cuda(), b)
+    assert np.array_equal(idx0.list_sizes, np.diff(off))
+    for bb in range(b):
+        assert np.array_equal(idx0.list_ids(bb), ids[off[bb]:off[bb + 1]])
+    # default (L2): the same lists, each stored by ascending distance to its pivot
+    # (the mean of its rows); ties keep list order
+    idx = PartitionedIndex(12, "L2").build(torch.from_numpy(d2b).cuda(), torch.from_numpy(x).cuda(), b)
     assert np.array_equal(idx.list_sizes, np.diff(off))
     for bb in range(b):
-        assert np.array_equal(idx.list_ids(bb), ids[off[bb]:off[bb + 1]])
+        got, ref = idx.list_ids(bb), ids[off[bb]:off[bb + 1]]
+        assert np.array_equal(np.sort(got), np.sort(ref))
+        if len(ref):
+            piv = x[ref].astype(np.float64).mean(0)
+            rad = np.sqrt(((x[got].astype(np.float64) - piv) ** 2).sum(1)).astype(np.float32)
+            assert (np.diff(rad) >= -1e-5 * (1 + rad[1:])).all()
     distinct = max(len(set(r[r >= 0])) for r in d2b)
     assert idx.max_replicas == distinct
     q = rng.standard_normal((20, 12), dtype=np.float32)
@@ -365,6 +377,12 @@ def test_options_do_not_change_results(metric):
             D, I, nc = run(idx, q, probe, 10)
             assert np.array_equal(I, ref[1]) and np.array_equal(bits(D), bits(ref[0])), (name, v)
         idx.set_option(name, old)
+    # the build-time storage order (radius-ordered lists vs list order)
+    for k in (10, 100):
+        idx0 = make_index(x, d2b, 8, metric, order=0)
+        D0, I0, _ = run(idx0, q, probe, k)
+        D1, I1, _ = run(idx, q, probe, k)
+        assert np.array_equal(I0, I1) and np.array_equal(bits(D0), bits(D1)), ("order", k)
     # the pipelined screen's ring variants at both query-block sizes
     for qr, ring in ((64, 2), (64, 4), (128, 3), (128, 4)):
         idx.set_option("qr", qr)

@@ -24,16 +24,24 @@ q = mq(nq, 1335)
 probe = rank_nearest(q, c, nprobe)
 for _ in range(3):
     idx.search(q, probe, k)
-idx.set_option("debug", dbg | 8)
 idx.set_stats(True)
+idx.search(q, probe, k)
+work = idx.stats_read()  # (the work counters are off while the clocks run)
+idx.set_option("debug", dbg | 8)
 idx.set_profiling(True)
 idx.search(q, probe, k)
 torch.cuda.synchronize()
 st = idx.stats_read()
 pr = idx.profile_read()
 print(cfg, data, "debug", dbg, opts, "kernel", idx.describe(nq, nprobe, k))
-tot = st["chunks_nominal"] + st["blocks_dropped"] + st["rescans"]
+tot = max(1, st["chunks_nominal"] + st["blocks_dropped"] + st["rescans"])
 print("scan_ms %.3f  cycles: prologue %.3g  blocks %.3g  epilogue %.3g  (fractions %.2f / %.2f / %.2f)" % (
     pr["scan_ms"], st["chunks_nominal"], st["blocks_dropped"], st["rescans"],
     st["chunks_nominal"] / tot, st["blocks_dropped"] / tot, st["rescans"] / tot))
-print("blocks", st["blocks"], "skipped", st["blocks_skipped"])
+# k_screen_m: wave 0's block loop split (refresh + skip test / chunk loop / selection)
+bl = max(1, st["blocks_dropped"])
+print("block loop: refresh %.2f  chunks %.2f  selection %.2f  (slow-path regs %d)  per block: %.0f / %.0f / %.0f cycles"
+      % (st["chunks_computed"] / bl, st["blocks"] / bl, st["blocks_skipped"] / bl, st["survivors"],
+         st["chunks_computed"] / max(1, work["blocks"]), st["blocks"] / max(1, work["blocks"]),
+         st["blocks_skipped"] / max(1, work["blocks"])))
+print("blocks", work["blocks"], "skipped", work["blocks_skipped"], "survivors", work["survivors"])

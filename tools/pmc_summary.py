@@ -27,7 +27,7 @@ def main(d):
                     "calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                     "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"]),
                     "pct": float(r["Percentage"])}
-    for sub in ("fetch", "write", "sq1", "sq2"):
+    for sub in ("fetch", "write", "sq1", "sq2", "tcc"):
         f = os.path.join(d, sub, "run_counter_collection.csv")
         if not os.path.exists(f):
             continue
@@ -48,6 +48,10 @@ def main(d):
         p = e.get("pmc", {})
         if "FETCH_SIZE" in p and "WRITE_SIZE" in p:
             e["hbm_bytes_per_launch"] = (2 * p["FETCH_SIZE"] + p["WRITE_SIZE"]) * 1024
+        if "FETCH_SIZE" in p:
+            e["l2_miss_read_bytes_per_launch"] = 2 * p["FETCH_SIZE"] * 1024
+        if "TCC_HIT_sum" in p and "TCC_MISS_sum" in p and p["TCC_HIT_sum"] + p["TCC_MISS_sum"]:
+            e["l2_hit_rate"] = p["TCC_HIT_sum"] / (p["TCC_HIT_sum"] + p["TCC_MISS_sum"])
         if "SQ_ACTIVE_INST_VALU" in p and "GRBM_GUI_ACTIVE" in p and p["GRBM_GUI_ACTIVE"]:
             # VALUBusy as rocprof defines it: 100*sum(ACTIVE_INST_VALU)/CU_NUM/GRBM_GUI_ACTIVE
             # (ACTIVE_INST_VALU in quad-cycles; GRBM summed over 8 XCDs)
