@@ -270,10 +270,12 @@ struct SSmem {
     static constexpr int kXT = (XH ? 2 : 4) * 1024;         // one tile's chunk (XH: the hi parts)
     static constexpr int kXS = kSBT * kXT;                  // X chunk: 16 KiB (XH: 8)
     static constexpr int kQS = kSDK * QR * 4;               // Q chunk: 4 KiB at QR = 64
-    static constexpr int kXA = MF ? kSBT * kTile * 4 : 0;   // the block's xadj (first chunk): 1 KiB
+    static constexpr int kXA = 0;                           // (k_screen: none)
     static constexpr int kStage = kXS + kQS + kXA;
     static constexpr int NSL = XH ? 3 : 2;                  // ring slots
-    static constexpr int kX = NSL * kStage;
+    // (MF) the xadj of the last two blocks, [2][256] (staged with a block's first chunk)
+    static constexpr int kXB = MF ? 2 * kSBT * kTile * 4 : 0;
+    static constexpr int kX = NSL * kStage + kXB;
     static constexpr int kLists = QR * K2 * 8;
     static constexpr int kBufs = QR * BC * 8;
     // item; pair, bufc, (spare) per row; block-skip (A, B) x 2 parities and
@@ -294,6 +296,21 @@ __device__ __forceinline__ void sglds16(const void *gsrc, uint32_t lds_addr) {
         : "v"(gsrc), "s"(lds_addr)
         : "memory");
 }
+
+// The same DMA through the compiler builtin (hipcc sets M0 itself and counts
+// the load in its own vmcnt bookkeeping)
+__device__ __forceinline__ void sglds16b(const void *gsrc, uint32_t lds_addr) {
+    __builtin_amdgcn_global_load_lds(gsrc, (__attribute__((address_space(3))) void *)(uintptr_t)lds_addr, 16, 0, 0);
+}
+
+#ifdef LIRA_PHASE_CLOCKS
+static constexpr bool kPhaseClocks = true;
+#else
+static constexpr bool kPhaseClocks = false;
+#endif
+#ifndef LIRA_SGLDS
+#define LIRA_SGLDS sglds16
+#endif
 
 // XCD-aware work queues (k_plan): claim the next item of this workgroup's own
 // XCD's queue, stealing from the others (in order) once it is empty; -1 when
@@ -785,9 +802,11 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
     const int nchunk = (int)(a.dpad / DK);
 
     long long t_0 = 0, t_1 = 0, t_2 = 0;  // (a.dbg & 8) phase clocks, thread 0
-    long long t_ref = 0, t_chk = 0, t_sel = 0, t_x = 0, n_slow = 0;  // (a.dbg & 8) block-loop split
-    const bool clk = (a.dbg & 8) && tid == 0;
-    unsigned long long *const cnt = (a.dbg & 8) ? nullptr : a.stats;  // work counters (off while timing)
+    long long t_ref = 0, t_chk = 0, t_sel = 0, t_x = 0, n_slow = 0, t_wt = 0;  // (a.dbg & 8) block-loop split
+    // (phase clocks only in a -DLIRA_PHASE_CLOCKS build: their registers would
+    // otherwise be live across the whole kernel)
+    const bool clk = kPhaseClocks && (a.dbg & 8) && tid == 0;
+    unsigned long long *const cnt = kPhaseClocks && (a.dbg & 8) ? nullptr : a.stats;  // (off while timing)
     __shared__ int xq[9];  // the XCD queues' bounds (k_plan)
     int qx = 0, qtries = 0, nxt = -1;  // thread 0: its queue, the claimed next item
     if (tid == 0) {
@@ -796,7 +815,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
         nxt = claim_item(a.head, xq, qx, qtries);
     }  // thread 0: the claimed next item
     for (;;) {
-        if ((a.dbg & 8) && tid == 0) t_0 = clock64();
+        if (clk) t_0 = clock64();
         if (tid == 0) {
             // the next item is claimed one item ahead (its atomic completes
             // under this item's work); one table load decodes it
@@ -848,7 +867,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
 
         const float4 *qtg = (const float4 *)(a.QT + (int64_t)gqb * a.dpad * QR);
         // returns the DMA instructions this wave issued (the ring's vmcnt waits count them)
-        auto stage = [&](int tb, int jc, int slot) -> int {
+        auto stage = [&](int tb, int jc, int slot, int xpar) -> int {
             if (a.dbg & 4) return 0;  // timing experiment: no loads
             const int ntv = min(kSBT, tb_end - tb);
             const uint32_t base = xs_lds + (uint32_t)(slot * S::kStage);
@@ -859,15 +878,15 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
 #pragma unroll
             for (int m = 0; m < NP / NW; ++m) {
                 const int pc = wave + NW * m, t = pc >> QSH, qq = pc & ((1 << QSH) - 1);
-                sglds16(Xg + (int64_t)(tile0 + tb + min(t, ntv - 1)) * tstride + jc * (kTile / 4) + qq * 64 + lane,
+                LIRA_SGLDS(Xg + (int64_t)(tile0 + tb + min(t, ntv - 1)) * tstride + jc * (kTile / 4) + qq * 64 + lane,
                         __builtin_amdgcn_readfirstlane(base + (uint32_t)(t * S::kXT + qq * 1024)));
             }
             // Q: QR/16 pieces of 1 KiB, one per wave
-            sglds16(qtg + (int64_t)jc * (QR / 4) + wave * 64 + lane,
+            LIRA_SGLDS(qtg + (int64_t)jc * (QR / 4) + wave * 64 + lane,
                     __builtin_amdgcn_readfirstlane(base + (uint32_t)S::kXS + (uint32_t)wave * 1024u));
             if (jc == 0 && wave == 0) {  // the block's xadj rides along (tiles past its end: masked on read)
-                sglds16(a.xadj + (int64_t)(tile0 + tb + min(lane >> 4, ntv - 1)) * kTile + (lane & 15) * 4,
-                        __builtin_amdgcn_readfirstlane(base + (uint32_t)(S::kXS + S::kQS)));
+                LIRA_SGLDS(a.xadj + (int64_t)(tile0 + tb + min(lane >> 4, ntv - 1)) * kTile + (lane & 15) * 4,
+                           __builtin_amdgcn_readfirstlane(xs_lds + (uint32_t)(NSL * S::kStage + xpar * 1024)));
                 return NP / NW + 2;
             }
             return NP / NW + 1;
@@ -1003,15 +1022,16 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
         // ahead of the consumer, crossing into the next unskipped block with the
         // current block's skip intervals (looser than later ones: safe); the
         // blocks it enters queue up for the consumer (at most 2: nchunk >= 2).
-        int itb = tb, ijc = 0, islot = 0, par_i = 1;
+        int itb = tb, ijc = 0, islot = 0, par_i = 1, iblk = 0;  // iblk: the issuer's block count
         int q_n = 0, q_0 = tb_end, q_1 = tb_end;  // queued block starts
         int n_cur = 0, n_nxt = 0;                 // this wave's DMAs of the chunks after the consumer's
         auto issue = [&]() -> int {
             if (itb >= tb_end) return 0;
-            const int n = stage(itb, ijc * DK, islot);
+            const int n = stage(itb, ijc * DK, islot, iblk & 1);
             islot = islot + 1 == NSL ? 0 : islot + 1;
             if (++ijc == nchunk) {
                 ijc = 0;
+                ++iblk;
                 itb = skip_from(itb + kSBT, par_i);
                 if (q_n == 0) q_0 = itb; else q_1 = itb;
                 ++q_n;
@@ -1021,7 +1041,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
         n_cur = issue();
         if (NSL == 3) n_nxt = issue();
 
-        if ((a.dbg & 8) && tid == 0) t_1 = clock64();
+        if (clk) t_1 = clock64();
         auto pop = [&]() {  // the next block the issuer entered
             const int v = q_0;
             q_0 = q_1;
@@ -1039,8 +1059,6 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                 Eb = Rb < R ? err_E<METRIC>(my_qnorm, Rb, dd, ESPLIT, (double)a.dpad, a.centred) : my_E;
             }
             const float h_l = refresh(bi & 1);
-            f4 xa[4];  // xadj of my 16 candidates: tile t, i = 0..3 (+inf: padding / past the block);
-                       // read from the ring at chunk 0 (staged with it)
             // a wave whose 16 rows all skip the block (or hold no query)
             // computes nothing for it
             bool wdead = !__any(lane < 16 && my_pair >= 0);
@@ -1061,6 +1079,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
             par_i = bi & 1;  // the issuer's skip test uses this block's intervals
 #pragma unroll 1
             for (int c = 0; c < nchunk; ++c) {
+                const long long t_w0 = clk ? clock64() : 0;
                 // this chunk's DMAs landed (the ones issued after it may stay in
                 // flight: vmcnt counts this wave's vector-memory ops in order)
                 if (NSL == 3 && n_nxt > 0) {
@@ -1072,48 +1091,59 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
                 __syncthreads();  // ... in every wave; and the slot issued next is free
+                if (clk) t_wt += clock64() - t_w0;
                 n_cur = n_nxt;
                 n_nxt = issue();
                 if (NSL == 2) {
                     n_cur = n_nxt;
                     n_nxt = 0;
                 }
-                if (c == 0) {
-                    const float *xs = (const float *)((const char *)Xs + slot * S::kStage + S::kXS + S::kQS);
-#pragma unroll
-                    for (int t = 0; t < 4; ++t)
-                        xa[t] = t < ntv ? *(const f4 *)(xs + t * kTile + 4 * cj) : (f4)(__builtin_inff());
-                }
                 if (SPLIT == 2 && !wdead && !(a.dbg & 1)) {
                     const char *sb = (const char *)Xs + slot * S::kStage;
+                    // all 17 fragment reads first, then the 16 MFMAs (pinned by sched
+                    // groups: left to itself hipcc serialises read -> wait -> MFMA)
                     const bf16x8 aq = *(const bf16x8 *)(sb + S::kXS + ((g * QR + wave * 16 + cj) << 4));
+                    bf16x8 bv[16];
 #pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        bf16x8 bv[4];
-#pragma unroll
-                        for (int i = 0; i < 4; ++i)
-                            bv[i] = *(const bf16x8 *)(sb + t * S::kXT + (((g & 1) * 64 + i * 16 + cj) << 4));
+                    for (int t = 0; t < 4; ++t)
 #pragma unroll
                         for (int i = 0; i < 4; ++i)
-                            acc[t * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq, bv[i], acc[t * 4 + i], 0, 0, 0);
-                    }
+                            bv[t * 4 + i] = *(const bf16x8 *)(sb + t * S::kXT + (((g & 1) * 64 + i * 16 + cj) << 4));
+#pragma unroll
+                    for (int i = 0; i < 16; ++i)
+                        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq, bv[i], acc[i], 0, 0, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 9, 0);  // DS reads
+                    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // MFMAs
+                    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
                 } else if (SPLIT && !wdead && !(a.dbg & 1)) {
                     const char *sb = (const char *)Xs + slot * S::kStage;
                     const bf16x8 a_hi = *(const bf16x8 *)(sb + S::kXS + (((g & 1) * QR + wave * 16 + cj) << 4));
                     const bf16x8 a_lo = *(const bf16x8 *)(sb + S::kXS + (((2 + (g & 1)) * QR + wave * 16 + cj) << 4));
+                    bf16x8 bv[16];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            bv[t * 4 + i] = *(const bf16x8 *)(sb + t * S::kXT + ((g * 64 + i * 16 + cj) << 4));
 #pragma unroll
                     for (int t = 0; t < 4; ++t) {
-                        bf16x8 bv[4];
 #pragma unroll
                         for (int i = 0; i < 4; ++i)
-                            bv[i] = *(const bf16x8 *)(sb + t * (kSDK * kTile * 4) + ((g * 64 + i * 16 + cj) << 4));
+                            acc[t * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_hi, bv[t * 4 + i], acc[t * 4 + i], 0, 0, 0);
 #pragma unroll
                         for (int i = 0; i < 4; ++i)
-                            acc[t * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_hi, bv[i], acc[t * 4 + i], 0, 0, 0);
-#pragma unroll
-                        for (int i = 0; i < 4; ++i)
-                            acc[t * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_lo, bv[i], acc[t * 4 + i], 0, 0, 0);
+                            acc[t * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_lo, bv[t * 4 + i], acc[t * 4 + i], 0, 0, 0);
                     }
+                    // the next tile's B fragments in flight under this tile's 8 MFMAs
+                    __builtin_amdgcn_sched_group_barrier(0x100, 10, 0);  // A hi / lo + tiles 0, 1
+                    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
                 } else if (!SPLIT && !wdead && !(a.dbg & 1)) {
                     const float *sb = (const float *)((const char *)Xs + slot * S::kStage);
                     const float *xb = sb + g * kTile + 4 * cj;                   // + t*1024 + 4s*64
@@ -1143,6 +1173,14 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                 t_x = t;
             }
             if (wdead || (a.dbg & 2)) continue;
+            // xadj of my 16 candidates: tile t, i = 0..3 (+inf: padding / past the block)
+            f4 xa[4];
+            {
+                const float *xs = (const float *)((const char *)Xs + NSL * S::kStage + (bi & 1) * 1024);
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    xa[t] = t < ntv ? *(const f4 *)(xs + t * kTile + 4 * cj) : (f4)(__builtin_inff());
+            }
 
             float h_r[4];
 #pragma unroll
@@ -1273,7 +1311,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
             if (clk) t_sel += clock64() - t_x;
         }
 
-        if ((a.dbg & 8) && tid == 0) t_2 = clock64();
+        if (clk) t_2 = clock64();
         // ---- flush buffers, emit lists, publish bounds (wave-owned rows)
 #pragma unroll 1
         for (int r = 0; r < 16; ++r) {
@@ -1295,7 +1333,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
             }
         }
         __syncthreads();
-        if ((a.dbg & 8) && tid == 0 && a.stats) {  // timing experiment: cycles per phase
+        if (clk && a.stats) {  // timing experiment: cycles per phase
             const long long t_3 = clock64();
             atomicAdd(a.stats + 1, (unsigned long long)(t_1 - t_0));
             atomicAdd(a.stats + 3, (unsigned long long)(t_2 - t_1));
@@ -1306,7 +1344,8 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
             atomicAdd(a.stats + 2, (unsigned long long)t_chk);
             atomicAdd(a.stats + 4, (unsigned long long)t_sel);
             atomicAdd(a.stats + 7, (unsigned long long)n_slow);
-            t_ref = t_chk = t_sel = n_slow = 0;
+            atomicAdd(a.stats + 5, (unsigned long long)t_wt);  // of which: waits + barriers at chunk starts
+            t_ref = t_chk = t_sel = n_slow = t_wt = 0;
         }
     }
 }
@@ -1598,19 +1637,28 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_s(ScreenArgs a) {
             if (!wdead && !(a.dbg & 1)) {
                 const bf16x8 a_hi = *(const bf16x8 *)(sb + S::kX + (((g & 1) * QR + wave * 16 + cj) << 4));
                 const bf16x8 a_lo = *(const bf16x8 *)(sb + S::kX + (((2 + (g & 1)) * QR + wave * 16 + cj) << 4));
+                bf16x8 bv[16];
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        bv[t * 4 + i] = *(const bf16x8 *)(sb + t * (kSDK * kTile * 4) + ((g * 64 + i * 16 + cj) << 4));
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
-                    bf16x8 bv[4];
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
-                        bv[i] = *(const bf16x8 *)(sb + t * (kSDK * kTile * 4) + ((g * 64 + i * 16 + cj) << 4));
+                        acc[t * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_hi, bv[t * 4 + i], acc[t * 4 + i], 0, 0, 0);
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
-                        acc[t * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_hi, bv[i], acc[t * 4 + i], 0, 0, 0);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        acc[t * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_lo, bv[i], acc[t * 4 + i], 0, 0, 0);
+                        acc[t * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_lo, bv[t * 4 + i], acc[t * 4 + i], 0, 0, 0);
                 }
+                // the next tile's B fragments in flight under this tile's 8 MFMAs (k_screen_m)
+                __builtin_amdgcn_sched_group_barrier(0x100, 10, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
             }
             if (jc + kSDK < dpad) continue;
 
@@ -2175,9 +2223,10 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // LIRA_OPT_SPLIT = 0 keeps the fp32 MFMA screen (which reads the fp32 tiles)
     pl.split = split_wanted && pl.mfma && idx->Xb != nullptr;
     // hi-only x (LIRA_OPT_XHI): k_screen_m at 64 queries per item
-    // (default on at dpad >= 512: GIST1M scan + merge 1.45 -> 1.30 ms mixture, 1.98
-    // -> 1.88 latent; SIFT1M slower, 0.71 -> 0.73 / 2.45 -> 2.57: more re-checks)
-    const int xhi = op.xhi >= 0 ? op.xhi : idx->dpad >= 512;
+    // (default: with its 3-slot ring and pipelined fragment reads, measured
+    // SIFT1M scan 2.21 -> 1.93 ms latent, 0.56 -> 0.51 mixture; GIST1M 1.49 ->
+    // 1.10 latent, 1.25 -> 0.85 mixture -- more exact re-checks, fewer MFMAs)
+    const int xhi = op.xhi >= 0 ? op.xhi : 1;
     if (pl.split && xhi && pl.qr == 64 && !(op.pipeline && (pl.rl == 4 || op.ring > 0))) pl.split = 2;
     // the pipelined split screen (LIRA_OPT_PIPELINE): RL 1 at 128 queries per item
     // (8 waves, 4 ring slots, 16-key buffers), RL 2 at 64 (4 slots), RL 4 at 64 (3 slots)

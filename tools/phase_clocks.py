@@ -27,7 +27,7 @@ for _ in range(3):
 idx.set_stats(True)
 idx.search(q, probe, k)
 work = idx.stats_read()  # (the work counters are off while the clocks run)
-idx.set_option("debug", dbg | 8)
+idx.set_option("debug", dbg | 8 | opts.get("debug", 0))
 idx.set_profiling(True)
 idx.search(q, probe, k)
 torch.cuda.synchronize()
@@ -44,4 +44,6 @@ print("block loop: refresh %.2f  chunks %.2f  selection %.2f  (slow-path regs %d
       % (st["chunks_computed"] / bl, st["blocks"] / bl, st["blocks_skipped"] / bl, st["survivors"],
          st["chunks_computed"] / max(1, work["blocks"]), st["blocks"] / max(1, work["blocks"]),
          st["blocks_skipped"] / max(1, work["blocks"])))
+print("chunk-start waits + barriers: %.0f cycles per block (%.2f of the chunk loop)" % (
+    st["rechecked"] / max(1, work["blocks"]), st["rechecked"] / max(1, st["blocks"])))
 print("blocks", work["blocks"], "skipped", work["blocks_skipped"], "survivors", work["survivors"])
