@@ -142,13 +142,13 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *   LIRA_OPT_NEAR_ROUNDS the same for the nearest-probe group (default 2)
  *   LIRA_OPT_MFMA        screen engine: 1 auto (default), 0 VALU, 2 MFMA wherever it fits
  *   LIRA_OPT_DEBUG       timing experiments only (results invalid): bit mask, see lira_screen.hip
- *   LIRA_OPT_PIPELINE    1: the pipelined split screen k_screen_s (default); 0: k_screen_m
+ *   LIRA_OPT_PIPELINE    1: the pipelined split screen k_screen_s for k > 56; 0 (default): k_screen_m
  *   LIRA_OPT_RING        k_screen_s ring slots: 0 auto, 2..4
  *   LIRA_OPT_PROBES_HINT expected valid probes per query when the probe lists are mostly -1
  *                        padding (a threshold selection padded to B): sizes the work split (0 = nprobe_max)
  *   LIRA_OPT_XHI         1: the split screen multiplies the query's hi + lo parts by x's hi part only
  *                        (half the staged bytes and MFMAs, a 2^-8 wider bound, more exact re-checks);
- *                        0: hi and lo; -1 (default): 1
+ *                        0: hi and lo; -1 (default): 1 for L2 (centred copy), 0 for IP
  *   LIRA_OPT_ORDER       (build time: set before lira_index_add_partitions) 1 (default, L2): store
  *                        each list's rows by ascending distance to the list's pivot, so tile radius
  *                        ranges are narrow and the triangle-inequality skip drops more; 0: list order.

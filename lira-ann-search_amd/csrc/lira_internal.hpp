@@ -45,7 +45,7 @@ struct lira_opts {
     int near_rounds = 2;
     int mfma = 1;
     int debug = 0;
-    int pipeline = 1;
+    int pipeline = 0;
     int ring = 0;
     int probes_hint = 0;
     int xhi = -1;

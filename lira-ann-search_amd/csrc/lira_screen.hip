@@ -2209,11 +2209,12 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     pl.rl = screen_rl(k);
     // the split-bf16 screen unless asked off (it is the only one without the fp32 tiles)
     const bool split_wanted = (op.split && !(flags & LIRA_SCAN_NO_SPLIT)) || !idx->X;
-    // MFMA screen where its LDS (64-query lists) still fits 2 workgroups per
-    // CU; larger k (RL 4: DEEP10M's k = 100) measured faster on the VALU one,
-    // which needs the fp32 tiles (without them: MFMA up to RL 4)
+    // MFMA screen up to RL 4 (k <= 120) on the split-bf16 copy (DEEP10M's k =
+    // 100: 24.1 ms against 33.3 ms on the VALU screen); the fp32 MFMA form
+    // (no split copy or LIRA_OPT_SPLIT = 0) only while its LDS fits 2
+    // workgroups per CU (RL <= 2); without the fp32 tiles MFMA is all there is
     const int mfma_opt = idx->X ? op.mfma : 2;
-    pl.mfma = mfma_opt == 2 ? pl.rl <= 4 : mfma_opt && pl.rl <= (op.pipeline && idx->Xb && split_wanted ? 4 : 2);
+    pl.mfma = mfma_opt == 2 ? pl.rl <= 4 : mfma_opt && pl.rl <= (idx->Xb && split_wanted ? 4 : 2);
     // queries per item of the MFMA screen: 64 (4 waves); 128 (8 waves, k <= 56)
     // halves the L2 -> LDS bytes per FMA but measured slower on every config
     // (SIFT1M 1.10 -> 1.25 ms mixture, 4.45 -> 4.66 ms latent; GIST, BIGANN too)
@@ -2226,14 +2227,17 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // (default: with its 3-slot ring and pipelined fragment reads, measured
     // SIFT1M scan 2.21 -> 1.93 ms latent, 0.56 -> 0.51 mixture; GIST1M 1.49 ->
     // 1.10 latent, 1.25 -> 0.85 mixture -- more exact re-checks, fewer MFMAs)
-    const int xhi = op.xhi >= 0 ? op.xhi : 1;
+    // IP: not centred, so the hi-only bound 2^-8 |q| R is wide against the score
+    // spread (DEEP10M k = 100: merge 0.3 -> 36 ms); default off there
+    const int xhi = op.xhi >= 0 ? op.xhi : idx->metric == LIRA_METRIC_L2 && idx->pivot != nullptr;
     if (pl.split && xhi && pl.qr == 64 && !(op.pipeline && (pl.rl == 4 || op.ring > 0))) pl.split = 2;
     // the pipelined split screen (LIRA_OPT_PIPELINE): RL 1 at 128 queries per item
     // (8 waves, 4 ring slots, 16-key buffers), RL 2 at 64 (4 slots), RL 4 at 64 (3 slots)
     // (measured, SIFT1M / GIST1M, k = 10: every ring / QR variant of k_screen_s
-    // slower than k_screen_m's 2-slot ring at 2 workgroups per CU -- its LDS
-    // leaves 1 workgroup per CU; DEEP10M k = 100: 28.1 ms vs 33.4 ms on the VALU
-    // screen), so RL 4 only, unless LIRA_OPT_RING asks for it
+    // slower than k_screen_m's ring at 2 workgroups per CU -- its LDS leaves 1
+    // workgroup per CU; DEEP10M k = 100: 28.1 ms, k_screen_m 24.1 ms since its
+    // fragment reads are pipelined), so only where LIRA_OPT_PIPELINE = 1 (RL 4)
+    // or LIRA_OPT_RING asks for it
     pl.v2 = pl.split && op.pipeline && (pl.rl == 4 || op.ring > 0);
     if (pl.v2) {
         pl.qr = pl.rl == 1 && op.qr != 64 ? 128 : 64;

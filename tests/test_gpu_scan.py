@@ -383,6 +383,10 @@ def test_options_do_not_change_results(metric):
         D0, I0, _ = run(idx0, q, probe, k)
         D1, I1, _ = run(idx, q, probe, k)
         assert np.array_equal(I0, I1) and np.array_equal(bits(D0), bits(D1)), ("order", k)
+        idx.set_option("pipeline", 1)  # k_screen_s for k > 56
+        D2, I2, _ = run(idx, q, probe, k)
+        idx.set_option("pipeline", 0)
+        assert np.array_equal(I2, I1) and np.array_equal(bits(D2), bits(D1)), ("pipeline", k)
     # the pipelined screen's ring variants at both query-block sizes
     for qr, ring in ((64, 2), (64, 4), (128, 3), (128, 4)):
         idx.set_option("qr", qr)
