@@ -271,6 +271,29 @@ __global__ __launch_bounds__(256) void k_split_rows(const float *Xr, int64_t d, 
     }
 }
 
+// Per tile: max over its real rows of ||v - hi(v)||, v the values k_split_rows
+// splits (x - pivot with a pivot), hi(v) the bf16 part it stores first; double
+// sum, rounded up with a 2^-40 margin.  Lane = row of the tile.
+__global__ __launch_bounds__(256) void k_tile_hires(const float *Xr, const int32_t *ids, int64_t d,
+                                                    const float *pivot, const int32_t *tile_list, int64_t n_tiles,
+                                                    float *tres) {
+    const int lane = threadIdx.x & 63;
+    const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= n_tiles) return;
+    const float *x = Xr + (t * kTile + lane) * d;
+    const float *pv = pivot ? pivot + (int64_t)tile_list[t] * d : nullptr;
+    double s = 0.0;
+    for (int64_t j = 0; j < d; ++j) {
+        const float v = pv ? x[j] - pv[j] : x[j];
+        const double r = (double)v - (double)__uint_as_float(bf16_split_part(v, 0) << 16);
+        s = __builtin_fma(r, r, s);
+    }
+    float m = ids[t * kTile + lane] >= 0 ? __double2float_ru(__builtin_sqrt(s) * (1.0 + 0x1p-40)) : 0.0f;
+#pragma unroll
+    for (int k = 32; k >= 1; k >>= 1) m = fmaxf(m, __shfl_xor(m, k, 64));
+    if (lane == 0) tres[t] = m;
+}
+
 __global__ void k_check_ids(const int32_t *ids, int64_t n, int64_t n_rows, int32_t *bad) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x)
@@ -286,6 +309,8 @@ static void free_storage(lira_index *idx) {
     idx->Xr = nullptr;
     if (idx->Xb) hipFree(idx->Xb);
     idx->Xb = nullptr;
+    if (idx->tres) hipFree(idx->tres);
+    idx->tres = nullptr;
     if (idx->xadj) hipFree(idx->xadj);
     if (idx->rmax) hipFree(idx->rmax);
     if (idx->xadjc) hipFree(idx->xadjc);
@@ -584,6 +609,16 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
                 hipLaunchKernelGGL(k_split_rows, dim3((unsigned)std::min<int64_t>(tiles * (dpad / 16), 1 << 20)),
                                    dim3(256), 0, st, idx->Xr, d, tiles, dpad, idx->pivot, d_tlist, (uint4 *)idx->Xb);
             if (e == hipSuccess) e = hipGetLastError();
+            if (e == hipSuccess) {  // (best effort: without it the hi-only screen bounds by 2^-8 R)
+                if (hipMalloc(&idx->tres, (size_t)tiles * 4) == hipSuccess) {
+                    hipLaunchKernelGGL(k_tile_hires, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, idx->Xr,
+                                       idx->ids, d, idx->pivot, d_tlist, tiles, idx->tres);
+                    e = hipGetLastError();
+                } else {
+                    (void)hipGetLastError();
+                    idx->tres = nullptr;
+                }
+            }
         } else {
             (void)hipGetLastError();
             idx->Xb = nullptr;
@@ -659,7 +694,8 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes) {
              (idx->X ? rows * idx->dpad * 4 : 0) +                             // fp32 tiles (optional)
              (idx->xadj ? rows * 4 + idx->n_lists * 4 : 0) +                   // xadj, rmax
              (idx->xadjc ? rows * 4 + idx->n_lists * 4 : 0) +                  // centred xadj, rmax
-             (idx->pivot ? idx->n_lists * idx->d * 4 + idx->n_tiles * 8 : 0);  // pivots, tile radii
+             (idx->pivot ? idx->n_lists * idx->d * 4 + idx->n_tiles * 8 : 0) +  // pivots, tile radii
+             (idx->tres ? idx->n_tiles * 4 : 0);                                // tile hi residuals
     return LIRA_OK;
 }
 

@@ -91,6 +91,9 @@ struct lira_index_impl {
     // Split-bf16 copy of the tiles for the MFMA screen (lira_abi.hip
     // k_split_tiles; layout at k_screen_m<..., SPLIT>): same bytes as X.
     uint16_t *Xb = nullptr;
+    // per tile: max over its rows of ||x - hi(x)|| for the values Xb splits (L2:
+    // x - pivot), rounded up -- the hi-only screen's error bound per block
+    float *tres = nullptr;
     int32_t *err = nullptr;        // device error word
     void *ws = nullptr;            // cached scan workspace
     size_t ws_bytes = 0;

@@ -84,6 +84,7 @@ struct ScreenArgs {
     const float *Q;
     const float *pivot;
     const float2 *tstat;
+    const float *tres;  // per tile max ||x - hi(x)|| of the split copy (NULL: 2^-8 R bounds it)
     int share;     // k_screen_m: publish/re-read the query bound every block (else once per item)
     int split;     // k_screen_m<..., SPLIT = 1>: X is the split-bf16 copy (Xb), QT in the split layout
     int centred;   // (L2, split) Xb / QT hold x - c / q - c of the list's pivot; xadj, rmax, QN are theirs
@@ -109,12 +110,15 @@ struct ScreenArgs {
 // + R, on top of the screen's own error for q', x'.
 template <int METRIC>
 __device__ __forceinline__ double err_E(double qnorm, double R, double d, int split = 0, double dp = 0.0,
-                                        int centred = 0) {
+                                        int centred = 0, double hres = -1.0) {
     const double dl = d * 0x1p-140;
     if (split) {
-        // split == 2 (hi-only x, k_screen_m<..., 2>): dot~ = sum (qh + ql) xh, x = xh + ex
-        // with |ex| <= 2^-8 |x_i|: |dot~ - q.x| <= (2^-8 + 2^-16 + 2 dpad 2^-22) 1.02 |q| R
-        const double ed = split == 2 ? (0x1p-8 + 1.0001 * 0x1p-16 + 2.0 * dp * 0x1p-22) * 1.02 * qnorm * R +
+        // split == 2 (hi-only x, k_screen_m<..., 2>): dot~ = sum (qh + ql) xh, x = xh + ex:
+        // |dot~ - q.x| <= |q.ex| + |(q - qh - ql).xh| + rounding <= |q| ||ex|| +
+        // (2^-16 + 2 dpad 2^-22) 1.02 |q| R, with ||ex|| <= 2^-8 R (|ex_i| <= 2^-8 |x_i|)
+        // or, tighter, hres >= ||ex|| of every candidate concerned (k_tile_hires)
+        const double ex = hres >= 0.0 ? hres * 1.0001 : 0x1p-8 * 1.02 * R;
+        const double ed = split == 2 ? ex * qnorm + (1.0001 * 0x1p-16 + 2.0 * dp * 0x1p-22) * 1.02 * qnorm * R +
                                            2.0 * dp * 0x1p-96 * (qnorm + R + 1.0)
                                      : (2.0001 * 0x1p-16 + 4.0 * dp * 0x1p-22) * 1.02 * qnorm * R +
                                            4.0 * dp * 0x1p-96 * (qnorm + R + 1.0);
@@ -282,7 +286,7 @@ struct SSmem {
     // ||q - pivot|| (lo, hi) doubles per row; (MF) the radius range of each of
     // an item's first kBR blocks
     static constexpr int kBR = MF ? 128 : 0;
-    static constexpr int kMeta = 64 + QR * 4 * 3 + 2 * QR * 8 + QR * 16 + kBR * 8;
+    static constexpr int kMeta = 64 + QR * 4 * 3 + 2 * QR * 8 + QR * 16 + kBR * 8 + (XH ? kBR * 4 : 0);
     static constexpr int total = kX + kLists + kBufs + kMeta;
 };
 
@@ -789,6 +793,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
     float2 *tri_s = (float2 *)(meta + 16 + 3 * QR);         // [2][QR]
     double *dq_s = (double *)(meta + 16 + 3 * QR + 4 * QR); // [QR][2]
     float2 *br_s = (float2 *)(dq_s + 2 * QR);               // [kBR] block radius ranges
+    float *bres_s = (float *)(br_s + S::kBR);               // [kBR] (SPLIT 2) block hi residual bounds
     const bool TRI = METRIC == LIRA_METRIC_L2 && a.tstat != nullptr;
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -923,10 +928,12 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
         // ranges: max ||x - c|| over its tiles, widened for fl(x - c)), else the
         // list's R; the block's test threshold uses its own error bound Eb <= E
         // (a row's list bound P keeps the list-wide E: its keys come from every block)
-        double Rb = R, Eb = my_E;
+        // E_run: the largest Eb of the blocks whose keys the list holds (every
+        // key's screened score is within its block's Eb of the truth)
+        double Rb = R, Eb = my_E, E_run = 0.0;
         auto refresh = [&](int par) {
             const u64 kk = my_list[k - 1];
-            double T = kk == kEmptyKey ? __builtin_inf() : bound_P<METRIC>((double)key_score(kk), my_E, dd);
+            double T = kk == kEmptyKey ? __builtin_inf() : bound_P<METRIC>((double)key_score(kk), E_run, dd);
             if (a.share && a.qbound && my_q >= 0) {
                 if (kk != kEmptyKey && lane < 16) {
                     const uint32_t b = f2ord(__double2float_ru(T));
@@ -976,11 +983,19 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                 }
             }
         };
+        // (SPLIT 2) the blocks' max ||x - hi(x)||: a tighter hi-only error bound than 2^-8 Rb
+        const bool hres_on = SPLIT == 2 && br_lds && a.tres != nullptr;
         if (br_lds) {
             for (int i = tid; i < nblk; i += NT) {
                 float lo, hi;
                 block_range_g(tb_begin + i * kSBT, lo, hi);
                 br_s[i] = make_float2(lo, hi);
+                if (hres_on) {
+                    const int t0 = tb_begin + i * kSBT, nt = min(kSBT, tb_end - t0);
+                    float m = 0.0f;
+                    for (int u = 0; u < nt; ++u) m = fmaxf(m, a.tres[tile0 + t0 + u]);
+                    bres_s[i] = m;
+                }
             }
             __syncthreads();
         }
@@ -1056,9 +1071,12 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
             if (TRI) block_range(tb, blo, bhi);
             if (TRI && SPLIT && a.centred) {
                 Rb = fmin(R, (double)bhi * (1.0 + 0x1p-20));
-                Eb = Rb < R ? err_E<METRIC>(my_qnorm, Rb, dd, ESPLIT, (double)a.dpad, a.centred) : my_E;
+                const double hr = hres_on ? (double)bres_s[(tb - tb_begin) / kSBT] : -1.0;
+                Eb = Rb < R || hres_on ? err_E<METRIC>(my_qnorm, Rb, dd, ESPLIT, (double)a.dpad, a.centred, hr)
+                                       : my_E;
             }
             const float h_l = refresh(bi & 1);
+            E_run = fmax(E_run, Eb);  // (this block's keys join the list below)
             // a wave whose 16 rows all skip the block (or hold no query)
             // computes nothing for it
             bool wdead = !__any(lane < 16 && my_pair >= 0);
@@ -1247,7 +1265,8 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                     if (h == -__builtin_inff() && B < __builtin_inff()) {
                         const double qnorm_r = (double)__shfl((float)my_qnorm, 4 * g + reg, 64);
                         // (bound from this block's keys: its own error bound serves both)
-                        const double E_r = err_E<METRIC>(qnorm_r, Rb, dd, ESPLIT, (double)a.dpad, a.centred);
+                        const double E_r = err_E<METRIC>(qnorm_r, Rb, dd, ESPLIT, (double)a.dpad, a.centred,
+                                                         hres_on ? (double)bres_s[(tb - tb_begin) / kSBT] : -1.0);
                         h = row_h<METRIC>(s_lim<METRIC>(bound_P<METRIC>((double)B, E_r, dd), E_r, dd),
                                           (double)qn_r[reg], qnorm_r, Rb);
                         int pm2 = 0;
@@ -1328,7 +1347,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
         if (lane < 16 && a.qbound && my_q >= 0) {
             const u64 kk = my_list[k - 1];
             if (kk != kEmptyKey) {
-                const double P = bound_P<METRIC>((double)key_score(kk), my_E, dd);
+                const double P = bound_P<METRIC>((double)key_score(kk), E_run, dd);
                 atomicMin(a.qbound + my_q, f2ord(__double2float_ru(P)));
             }
         }
@@ -2541,6 +2560,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     a.Q = q;
     a.pivot = tri ? idx->pivot : nullptr;
     a.tstat = tri ? idx->tstat : nullptr;
+    a.tres = tri && centred && pl.split == 2 ? idx->tres : nullptr;
     a.dbg = o.debug;
     a.share = o.share;
     a.split = pl.split;
