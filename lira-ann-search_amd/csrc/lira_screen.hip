@@ -74,6 +74,7 @@ struct ScreenArgs {
     const float *QT;       // [qblk][dpad][QR]
     const float4 *QN;      // [qblk*QR]: qn, |q| (up), pair (int bits), 0
     u64 *partial;          // [pair][nch_max][K2]
+    float *pE;             // [pair][nch_max]: k_screen_m's bound on its listed keys' screening error
     uint32_t *qbound;      // [nq] f2ord(bound on the final k-th exact score); NULL = off
     int64_t d, dpad;
     int n_lists, n_virt, nprobe, k, bpc, nch_max;  // n_virt = groups * n_lists (virtual partitions)
@@ -714,6 +715,7 @@ __global__ __launch_bounds__(kSThreads, OCC) void k_screen(ScreenArgs a) {
 // ---- merge: exact re-check of the survivors, final selection ---------------
 struct SMergeArgs {
     const u64 *partial;
+    const float *pE;  // NULL, or the screen's error bound per row list (tighter than the list-wide one)
     const int32_t *probe, *nch, *list_size, *tile_off, *ids;
     const float *Q, *Xr, *rmax;
     const uint32_t *qbound;
@@ -1344,6 +1346,8 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
             }
         }
         __builtin_amdgcn_wave_barrier();
+        if (lane < 16 && my_pair >= 0 && a.pE)  // (>= every listed key's own block bound)
+            a.pE[(int64_t)my_pair * a.nch_max + ch] = __double2float_ru(fmax(E_run, 0x1p-126));
         if (lane < 16 && a.qbound && my_q >= 0) {
             const u64 kk = my_list[k - 1];
             if (kk != kEmptyKey) {
@@ -2117,8 +2121,9 @@ __global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
             bool over = false;
             if (p >= 0) {
                 const double qn_s = a.centred ? (double)a.pqn[q * a.nprobe + s] : qnorm;
-                lim = s_lim<METRIC>((double)T, err_E<METRIC>(qn_s, (double)a.rmax[p], dd, a.split, (double)a.dpad,
-                                                             a.centred), dd);
+                const double E = a.pE ? (double)a.pE[(q * a.nprobe + s) * (int64_t)NC + c]
+                                      : err_E<METRIC>(qn_s, (double)a.rmax[p], dd, a.split, (double)a.dpad, a.centred);
+                lim = s_lim<METRIC>((double)T, E, dd);
                 const u64 last = src[K2 - 1];
                 over = last != kEmptyKey && (double)key_score(last) <= lim;
             }
@@ -2152,8 +2157,10 @@ __global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
                 const u64 *base = a.partial + (q * a.nprobe + s) * (int64_t)a.nch_max * K2;
                 float T = __builtin_inff();  // the pair's own bound: min over its chunk lists
                 const int nc = a.nch[vnch(s, p)];
+                const float *pe = a.pE ? a.pE + (q * a.nprobe + s) * (int64_t)a.nch_max : nullptr;
                 for (int c0 = 0; c0 < nc; c0 += 64)
-                    if (c0 + lane < nc) T = fminf(T, list_bound(base + (int64_t)(c0 + lane) * K2, E));
+                    if (c0 + lane < nc)
+                        T = fminf(T, list_bound(base + (int64_t)(c0 + lane) * K2, pe ? (double)pe[c0 + lane] : E));
 #pragma unroll
                 for (int m = 32; m >= 1; m >>= 1) T = fminf(T, __shfl_xor(T, m, 64));
                 take_lists(s, s + 1, T);
@@ -2219,7 +2226,7 @@ struct SPlan {
     int v2 = 0, ns = 2, bc = 32;  // the pipelined split screen (k_screen_s): ring slots, buffer keys per row
     int64_t max_qblk = 0;
     size_t off_cnt, off_cursor, off_head, off_qoff, off_item, off_nch, off_qblk, off_itab, off_qlist, off_qt, off_qn,
-        off_partial, off_qbound, off_pqn, total;
+        off_partial, off_qbound, off_pqn, off_pe, total;
 };
 
 static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, unsigned flags) {
@@ -2249,7 +2256,8 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // IP: not centred, so the hi-only bound 2^-8 |q| R is wide against the score
     // spread (DEEP10M k = 100: merge 0.3 -> 36 ms); default off there
     const int xhi = op.xhi >= 0 ? op.xhi : idx->metric == LIRA_METRIC_L2 && idx->pivot != nullptr;
-    if (pl.split && xhi && pl.qr == 64 && !(op.pipeline && (pl.rl == 4 || op.ring > 0))) pl.split = 2;
+    if (pl.split && xhi && pl.rl <= (pl.qr == 64 ? 4 : 1) && !(op.pipeline && (pl.rl == 4 || op.ring > 0)))
+        pl.split = 2;
     // the pipelined split screen (LIRA_OPT_PIPELINE): RL 1 at 128 queries per item
     // (8 waves, 4 ring slots, 16-key buffers), RL 2 at 64 (4 slots), RL 4 at 64 (3 slots)
     // (measured, SIFT1M / GIST1M, k = 10: every ring / QR variant of k_screen_s
@@ -2271,7 +2279,8 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
                                      : pl.rl == 1 ? (pl.ns == 4 ? SSmem2<64, 1, 4, 32>::total : SSmem2<64, 1, 2, 32>::total)
                                      : pl.rl == 2 ? SSmem2<64, 2, 4, 32>::total : SSmem2<64, 4, 3, 32>::total)
               : !pl.mfma       ? screen_smem(pl.qr, pl.rl)
-              : pl.qr == 128 ? (pl.rl == 1 ? SSmem<128, 1, true>::total : SSmem<128, 2, true>::total)
+              : pl.qr == 128 ? (pl.split == 2 ? SSmem<128, 1, true, true>::total
+                                : pl.rl == 1 ? SSmem<128, 1, true>::total : SSmem<128, 2, true>::total)
               : pl.split == 2 ? (pl.rl == 1 ? SSmem<64, 1, true, true>::total
                                  : pl.rl == 2 ? SSmem<64, 2, true, true>::total : SSmem<64, 4, true, true>::total)
               : pl.rl == 1   ? SSmem<64, 1, true>::total
@@ -2341,6 +2350,7 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     pl.off_partial = take((size_t)npairs * pl.nch_max * pl.K2 * 8);
     pl.off_qbound = take((size_t)nq * 4);
     pl.off_pqn = take((size_t)npairs * 4);
+    pl.off_pe = take((size_t)npairs * pl.nch_max * 4);  // k_screen_m: the error bound of each row list
     pl.total = o;
     return pl;
 }
@@ -2416,6 +2426,7 @@ static hipError_t launch_screen_rl(const ScreenArgs &a, const SPlan &pl, hipStre
         }
     }
     if (pl.mfma) {
+        if (pl.qr == 128 && pl.split == 2) return launch_screen_m<M, 1, 128, 2>(a, pl, st);
         if (pl.qr == 128 && pl.split)
             return pl.rl == 1 ? launch_screen_m<M, 1, 128, 1>(a, pl, st) : launch_screen_m<M, 2, 128, 1>(a, pl, st);
         if (pl.split == 2) switch (pl.rl) {
@@ -2577,6 +2588,9 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     a.QT = QT;
     a.QN = QN;
     a.partial = partial;
+    // the lists' own error bounds (k_screen_m only; the merge otherwise takes the list-wide one)
+    float *pE = pl.mfma && !pl.v2 ? (float *)(w + pl.off_pe) : nullptr;
+    a.pE = pE;
     a.qbound = qbound;
     a.d = idx->d;
     a.dpad = idx->dpad;
@@ -2595,6 +2609,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
 
     SMergeArgs m;
     m.partial = partial;
+    m.pE = pE;
     m.probe = probe;
     m.nch = nch;
     m.list_size = idx->list_size;
