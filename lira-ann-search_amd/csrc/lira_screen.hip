@@ -1867,7 +1867,9 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_s(ScreenArgs a) {
 static constexpr int kSeedTiles = 4;
 // The same bound from the fp32 tiles where the index keeps them (one wave per
 // query, lane = candidate: each dim of a tile is one coalesced 256-B row).
-template <int METRIC>
+// NT tiles: 2 for k <= 32 (measured SIFT1M mixture: plan 0.217 -> 0.164 ms,
+// scan +0.02 ms), else NT.
+template <int METRIC, int NT = kSeedTiles>
 __global__ __launch_bounds__(256) void k_seed_t(const float *Q, const int32_t *probe, int nprobe, int n_lists,
                                                 const int32_t *tile_off, const int32_t *ids, const float *X,
                                                 int64_t d, int64_t dpad, int64_t nq, int k, uint32_t *qbound) {
@@ -1876,15 +1878,15 @@ __global__ __launch_bounds__(256) void k_seed_t(const float *Q, const int32_t *p
     if (q >= nq) return;
     const int p = probe[q * nprobe];
     if (p < 0 || p >= n_lists) return;
-    const int tile0 = tile_off[p], nt = min(kSeedTiles, tile_off[p + 1] - tile0);
+    const int tile0 = tile_off[p], nt = min(NT, tile_off[p + 1] - tile0);
     if (nt <= 0) return;
     const float *qrow = Q + q * d;
-    const float *xt[kSeedTiles];
+    const float *xt[NT];
 #pragma unroll
-    for (int t = 0; t < kSeedTiles; ++t) xt[t] = X + (int64_t)(tile0 + min(t, nt - 1)) * dpad * kTile + lane;
-    float acc[kSeedTiles];
+    for (int t = 0; t < NT; ++t) xt[t] = X + (int64_t)(tile0 + min(t, nt - 1)) * dpad * kTile + lane;
+    float acc[NT];
 #pragma unroll
-    for (int t = 0; t < kSeedTiles; ++t) acc[t] = 0.0f;
+    for (int t = 0; t < NT; ++t) acc[t] = 0.0f;
     for (int64_t j0 = 0; j0 < d; j0 += 64) {
         const float qv = j0 + lane < d ? qrow[j0 + lane] : 0.0f;
         const int nj = (int)min<int64_t>(64, d - j0);
@@ -1893,7 +1895,7 @@ __global__ __launch_bounds__(256) void k_seed_t(const float *Q, const int32_t *p
             for (int jj = 0; jj < 64; ++jj) {
                 const float qj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qv), jj));
 #pragma unroll
-                for (int t = 0; t < kSeedTiles; ++t) {
+                for (int t = 0; t < NT; ++t) {
                     const float xv = xt[t][(j0 + jj) * kTile];
                     if (METRIC == LIRA_METRIC_L2) {
                         const float df = qj - xv;
@@ -1907,7 +1909,7 @@ __global__ __launch_bounds__(256) void k_seed_t(const float *Q, const int32_t *p
             for (int jj = 0; jj < nj; ++jj) {
                 const float qj = __shfl(qv, jj, 64);
 #pragma unroll
-                for (int t = 0; t < kSeedTiles; ++t) {
+                for (int t = 0; t < NT; ++t) {
                     const float xv = xt[t][(j0 + jj) * kTile];
                     if (METRIC == LIRA_METRIC_L2) {
                         const float df = qj - xv;
@@ -1921,7 +1923,7 @@ __global__ __launch_bounds__(256) void k_seed_t(const float *Q, const int32_t *p
     }
     float m[4] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};  // 4 smallest
 #pragma unroll
-    for (int u = 0; u < kSeedTiles; ++u) {
+    for (int u = 0; u < NT; ++u) {
         float sc = METRIC == LIRA_METRIC_L2 ? acc[u] : -acc[u];
         if (u >= nt || ids[(tile0 + u) * kTile + lane] < 0 || !(sc == sc)) continue;
 #pragma unroll
@@ -2545,14 +2547,19 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     LIRA_HIP_TRY(hipGetLastError());
     // (measured: SIFT1M mixture 1.70 -> 1.44 ms, latent +1 %)
     if (qbound && o.seed && idx->X) {  // from the fp32 tiles (coalesced)
-        if (idx->metric == LIRA_METRIC_L2)
-            hipLaunchKernelGGL(k_seed_t<LIRA_METRIC_L2>, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, q, probe,
-                               (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad,
-                               nq, (int)k, qbound);
+        const dim3 g((unsigned)((nq + 3) / 4));
+        if (idx->metric == LIRA_METRIC_L2 && k <= 32)
+            hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2, 2>), g, dim3(256), 0, st, q, probe, (int)nprobe,
+                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound);
+        else if (idx->metric == LIRA_METRIC_L2)
+            hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2>), g, dim3(256), 0, st, q, probe, (int)nprobe,
+                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound);
+        else if (k <= 32)
+            hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_IP, 2>), g, dim3(256), 0, st, q, probe, (int)nprobe,
+                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound);
         else
-            hipLaunchKernelGGL(k_seed_t<LIRA_METRIC_IP>, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, q, probe,
-                               (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad,
-                               nq, (int)k, qbound);
+            hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_IP>), g, dim3(256), 0, st, q, probe, (int)nprobe,
+                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound);
         LIRA_HIP_TRY(hipGetLastError());
     } else if (qbound && o.seed) {  // compact index: from the row-major copy
         if (idx->metric == LIRA_METRIC_L2)
