@@ -225,9 +225,34 @@ __global__ __launch_bounds__(256) void k_rank_select(const float *__restrict__ A
         if (!__ballot(cand)) continue;
         u64 key = kEmptyKey;
         if (cand) {
+            // search.cpp:220-235's sequential sum; 16 dims of loads in flight
+            // per step (a load per dim left each lane waiting on L2 latency:
+            // GIST1M d = 960, 170 us per call)
             const float *cr = cent + (int64_t)b * d;
             float acc = 0.0f;
-            for (int64_t j = 0; j < d; ++j) {
+            int64_t j = 0;
+            if ((((uintptr_t)cr | (uintptr_t)qr) & 15) == 0) {
+                for (; j + 16 <= d; j += 16) {
+                    float4 cv[4], qv[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        cv[e] = *(const float4 *)(cr + j + 4 * e);
+                        qv[e] = *(const float4 *)(qr + j + 4 * e);
+                    }
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        float df = qv[e].x - cv[e].x;
+                        acc = acc + df * df;
+                        df = qv[e].y - cv[e].y;
+                        acc = acc + df * df;
+                        df = qv[e].z - cv[e].z;
+                        acc = acc + df * df;
+                        df = qv[e].w - cv[e].w;
+                        acc = acc + df * df;
+                    }
+                }
+            }
+            for (; j < d; ++j) {
                 float df = qr[j] - cr[j];
                 acc = acc + df * df;
             }

@@ -178,6 +178,7 @@ __device__ __forceinline__ float row_h(double lim, double qn, double qnorm, doub
 // cpivot (L2, split): centre the rows on their partition's pivot, fl(q - c),
 // before splitting; QN.x / QN.y are then the centred norms, and pqn[pair] =
 // QN.y (the merge's copy of the row's norm).
+static constexpr int kQSlabs = 2;  // 64-dim slabs per k_qstage workgroup
 template <int QR, bool SPLIT>
 __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64_t dpad, int nprobe,
                                                 int n_virt, int n_lists, const int32_t *cnt, const int32_t *qoff,
@@ -206,8 +207,11 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
     // query row, writes along QT's row axis, both coalesced
     constexpr int RT = QR < 64 ? QR : 64;  // rows per transpose tile
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // blockIdx.y: this workgroup's group of kQSlabs 64-dim slabs (high d: many
+    // workgroups per query block; measured GIST1M k_qstage 284 -> ? us)
+    const int64_t j_lo = (int64_t)blockIdx.y * kQSlabs * 64, j_hi = min<int64_t>(dpad, j_lo + kQSlabs * 64);
     for (int r0 = 0; r0 < QR; r0 += RT) {
-        for (int64_t j0 = 0; j0 < dpad; j0 += 64) {
+        for (int64_t j0 = j_lo; j0 < j_hi; j0 += 64) {
             const int64_t j = j0 + lane;
             for (int rr = wv; rr < RT; rr += 4) {
                 const int pr = pairs[r0 + rr];
@@ -237,6 +241,7 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
             __syncthreads();
         }
     }
+    if (blockIdx.y != 0) return;  // (the norms: slab group 0)
     for (int r = threadIdx.x >> 6; r < QR; r += 4) {
         const int pr = pairs[r];
         double s = 0.0, t = 0.0;
@@ -2529,20 +2534,21 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     const bool centred = pl.split && idx->xadjc != nullptr && idx->pivot != nullptr;
     const float *cpivot = centred ? idx->pivot : nullptr;
     float *pqn = centred ? (float *)(w + pl.off_pqn) : nullptr;
+    const dim3 qgrid((unsigned)pl.max_qblk, (unsigned)((idx->dpad + 64 * kQSlabs - 1) / (64 * kQSlabs)));
     if (pl.qr == 128 && pl.split)
-        hipLaunchKernelGGL((k_qstage<128, true>), dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
+        hipLaunchKernelGGL((k_qstage<128, true>), qgrid, dim3(256), 0, st, q, idx->d, idx->dpad,
                            (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn);
     else if (pl.qr == 128)
-        hipLaunchKernelGGL((k_qstage<128, false>), dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
+        hipLaunchKernelGGL((k_qstage<128, false>), qgrid, dim3(256), 0, st, q, idx->d, idx->dpad,
                            (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn);
     else if (pl.qr == 64 && pl.split)
-        hipLaunchKernelGGL((k_qstage<64, true>), dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
+        hipLaunchKernelGGL((k_qstage<64, true>), qgrid, dim3(256), 0, st, q, idx->d, idx->dpad,
                            (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn);
     else if (pl.qr == 64)
-        hipLaunchKernelGGL((k_qstage<64, false>), dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
+        hipLaunchKernelGGL((k_qstage<64, false>), qgrid, dim3(256), 0, st, q, idx->d, idx->dpad,
                            (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn);
     else
-        hipLaunchKernelGGL((k_qstage<32, false>), dim3((unsigned)pl.max_qblk), dim3(256), 0, st, q, idx->d, idx->dpad,
+        hipLaunchKernelGGL((k_qstage<32, false>), qgrid, dim3(256), 0, st, q, idx->d, idx->dpad,
                            (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn);
     LIRA_HIP_TRY(hipGetLastError());
     // (measured: SIFT1M mixture 1.70 -> 1.44 ms, latent +1 %)
