@@ -178,7 +178,7 @@ __device__ __forceinline__ float row_h(double lim, double qn, double qnorm, doub
 // cpivot (L2, split): centre the rows on their partition's pivot, fl(q - c),
 // before splitting; QN.x / QN.y are then the centred norms, and pqn[pair] =
 // QN.y (the merge's copy of the row's norm).
-static constexpr int kQSlabs = 2;  // 64-dim slabs per k_qstage workgroup
+static constexpr int kQSlabs = 1;  // 64-dim slabs per k_qstage workgroup
 template <int QR, bool SPLIT>
 __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64_t dpad, int nprobe,
                                                 int n_virt, int n_lists, const int32_t *cnt, const int32_t *qoff,
@@ -207,8 +207,8 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
     // query row, writes along QT's row axis, both coalesced
     constexpr int RT = QR < 64 ? QR : 64;  // rows per transpose tile
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    // blockIdx.y: this workgroup's group of kQSlabs 64-dim slabs (high d: many
-    // workgroups per query block; measured GIST1M k_qstage 284 -> ? us)
+    // blockIdx.y: this workgroup's group of kQSlabs 64-dim slabs (many
+    // workgroups per query block: GIST1M plan 0.38 -> 0.23 ms, SIFT1M 0.17 -> 0.15)
     const int64_t j_lo = (int64_t)blockIdx.y * kQSlabs * 64, j_hi = min<int64_t>(dpad, j_lo + kQSlabs * 64);
     for (int r0 = 0; r0 < QR; r0 += RT) {
         for (int64_t j0 = j_lo; j0 < j_hi; j0 += 64) {
@@ -241,8 +241,8 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
             __syncthreads();
         }
     }
-    if (blockIdx.y != 0) return;  // (the norms: slab group 0)
-    for (int r = threadIdx.x >> 6; r < QR; r += 4) {
+    // the rows' norms, spread over the slab groups (each row whole in one)
+    for (int r = blockIdx.y + gridDim.y * (threadIdx.x >> 6); r < QR; r += 4 * gridDim.y) {
         const int pr = pairs[r];
         double s = 0.0, t = 0.0;
         if (pr >= 0) {
