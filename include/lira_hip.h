@@ -136,7 +136,9 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *   LIRA_OPT_QR          queries per screen work item: 0 auto (default), 64, 128
  *   LIRA_OPT_TWO_PHASE   nearest-probe group first: 1 auto (default), 0 off, 2 always
  *   LIRA_OPT_PRUNE       L2 triangle-inequality block skip / exact early abandon (1)
- *   LIRA_OPT_SEED        exact starting bound per query before the screen (1)
+ *   LIRA_OPT_SEED        exact starting bound per query before the screen: 1 (default) per
+ *                        query; 2 / 3: per nearest-partition query block over 128 / 256
+ *                        rows where it applies (k <= 32, d <= 256, two groups); 0 off
  *   LIRA_OPT_SHARE       per-block exchange of query bounds between work items (1)
  *   LIRA_OPT_ROUNDS      work items per workgroup target (0 = kernel default)
  *   LIRA_OPT_NEAR_ROUNDS the same for the nearest-probe group (default 2)

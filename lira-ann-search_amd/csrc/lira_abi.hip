@@ -711,7 +711,7 @@ int lira_index_set_option(lira_index *idx, int option, int64_t value) {
         case LIRA_OPT_QR: if (value != 0 && value != 64 && value != 128) break; o.qr = v; return LIRA_OK;
         case LIRA_OPT_TWO_PHASE: if (!in(0, 2)) break; o.two_phase = v; return LIRA_OK;
         case LIRA_OPT_PRUNE: if (!in(0, 1)) break; o.prune = v; return LIRA_OK;
-        case LIRA_OPT_SEED: if (!in(0, 1)) break; o.seed = v; return LIRA_OK;
+        case LIRA_OPT_SEED: if (!in(0, 3)) break; o.seed = v; return LIRA_OK;
         case LIRA_OPT_SHARE: if (!in(0, 1)) break; o.share = v; return LIRA_OK;
         case LIRA_OPT_ROUNDS: if (!in(0, 1024)) break; o.rounds = v; return LIRA_OK;
         case LIRA_OPT_NEAR_ROUNDS: if (!in(1, 1024)) break; o.near_rounds = v; return LIRA_OK;

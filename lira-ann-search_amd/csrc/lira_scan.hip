@@ -151,14 +151,7 @@ __global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t
             qoff[p] = carry_a + s_a[threadIdx.x] - c;
             item_off[p] = carry_b + s_b[threadIdx.x] - items;
             if (qblk_off) qblk_off[p] = carry_c + s_c[threadIdx.x] - nqb;
-            // item table: item -> (v, query block, chunk, global query block),
-            // so a workgroup decodes its item with one load (no search)
-            if (itab && items) {
-                const int i0 = carry_b + s_b[threadIdx.x] - items, g0 = carry_c + s_c[threadIdx.x] - nqb;
-                const int nc = items / nqb;
-                for (int ch = 0; ch < nc; ++ch)
-                    for (int qb = 0; qb < nqb; ++qb) itab[i0 + ch * nqb + qb] = make_int4(p, qb, ch, g0 + qb);
-            }
+            // (the item table is written below, in queue order)
         }
         __syncthreads();
         if (threadIdx.x == 1023) {
@@ -180,9 +173,14 @@ __global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t
     // queue v % 8, queue r holds its partitions' items in v order (group 0, each
     // query's nearest partition, first) and chunk-major, so the query blocks
     // that stream one chunk run on one XCD back to back and share its L2.  The
-    // table is rewritten queue by queue: v' = r m + i <-> v = 8 i + r.
+    // table is written queue by queue: v' = r m + i <-> v = 8 i + r.
     // head[2 + r]: queue r's claim counter (zeroed by the caller), head[10 + r]:
     // its start, head[18]: the end of queue 7 (= the item total).
+    // The entries are written by the whole workgroup, item-parallel (entry i
+    // finds its partition by a binary search over the LDS prefix sums): one
+    // thread per partition writing its items in turn serialised ~30 stores
+    // per thread (SIFT1M: k_plan 26 -> ~8 us).
+    __shared__ int32_t s_g[1024];
     __syncthreads();
     const int m = (n_virt + 7) / 8;
     if (threadIdx.x == 0) carry_b = 0;
@@ -197,6 +195,9 @@ __global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t
             items = nqb * nc;
         }
         s_b[threadIdx.x] = items;
+        s_a[threadIdx.x] = v;
+        s_c[threadIdx.x] = nqb;
+        s_g[threadIdx.x] = v < n_virt ? qblk_off[v] : 0;
         __syncthreads();
         for (int off = 1; off < 1024; off <<= 1) {
             int vb = threadIdx.x >= off ? s_b[threadIdx.x - off] : 0;
@@ -206,10 +207,16 @@ __global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t
         }
         const int i0 = carry_b + s_b[threadIdx.x] - items;
         if (vv < 8 * m && vv % m == 0) head[10 + vv / m] = i0;
-        if (v < n_virt && items) {
-            const int g0 = qblk_off[v];
-            for (int ch = 0; ch < nc; ++ch)
-                for (int qb = 0; qb < nqb; ++qb) itab[i0 + ch * nqb + qb] = make_int4(v, qb, ch, g0 + qb);
+        const int total = s_b[1023];
+        for (int i = threadIdx.x; i < total; i += 1024) {
+            int lo = 0, hi = 1023;  // first slot whose inclusive prefix exceeds i
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (s_b[mid] > i) hi = mid; else lo = mid + 1;
+            }
+            const int local = i - (lo ? s_b[lo - 1] : 0), nq_b = s_c[lo];
+            const int ch = local / nq_b, qb = local - ch * nq_b;
+            itab[carry_b + i] = make_int4(s_a[lo], qb, ch, s_g[lo] + qb);
         }
         __syncthreads();
         if (threadIdx.x == 1023) carry_b += s_b[1023];

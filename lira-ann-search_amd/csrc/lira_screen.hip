@@ -178,30 +178,47 @@ __device__ __forceinline__ float row_h(double lim, double qn, double qnorm, doub
 // cpivot (L2, split): centre the rows on their partition's pivot, fl(q - c),
 // before splitting; QN.x / QN.y are then the centred norms, and pqn[pair] =
 // QN.y (the merge's copy of the row's norm).
+// Last v in [0, n) with off[v] <= b (off nondecreasing, off[0] <= b), by one
+// whole wave: a 64-ary search, ceil(log64 n) dependent rounds of loads instead
+// of log2 n (k_qstage's thread-0 binary search was ~7 dependent global loads
+// per workgroup).  Wave-uniform result.
+__device__ __forceinline__ int wave_find_owner(const int32_t *off, int n, int b) {
+    const int lane = threadIdx.x & 63;
+    int lo = 0;
+    while (n > 1) {
+        const int stride = (n + 63) / 64, o = lane * stride;
+        const bool ok = o < n && off[lo + o] <= b;
+        const int L = __popcll(__ballot(ok));  // lanes 0 .. L-1 (monotone; lane 0 always)
+        lo += (L - 1) * stride;
+        n = min(stride, n - (L - 1) * stride);
+    }
+    return lo;
+}
+
 static constexpr int kQSlabs = 1;  // 64-dim slabs per k_qstage workgroup
 template <int QR, bool SPLIT>
 __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64_t dpad, int nprobe,
                                                 int n_virt, int n_lists, const int32_t *cnt, const int32_t *qoff,
                                                 const int32_t *qlist, const int32_t *qblk_off, const float *pivot,
                                                 const float *cpivot, float *QT, float4 *QN, float *pqn) {
-    __shared__ int pairs[QR];
+    __shared__ int pairs[QR], qrow_s[QR];
     __shared__ int s_v;
     __shared__ float tr[64][65];
     const int b = blockIdx.x;
     if (b >= qblk_off[n_virt]) return;
-    if (threadIdx.x == 0) {
-        int lo = 0, hi = n_virt - 1;  // last v with qblk_off[v] <= b
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (qblk_off[mid] <= b) lo = mid; else hi = mid - 1;
-        }
-        s_v = lo;
+    if (threadIdx.x < 64) {
+        const int v = wave_find_owner(qblk_off, n_virt, b);
+        if (threadIdx.x == 0) s_v = v;
     }
     __syncthreads();
     const int v = s_v, qb = b - qblk_off[v];
     const int nval = min(QR, cnt[v] - qb * QR);
     const float *cpv = cpivot ? cpivot + (int64_t)(v >= n_lists ? v - n_lists : v) * d : nullptr;
-    if (threadIdx.x < QR) pairs[threadIdx.x] = (int)threadIdx.x < nval ? qlist[qoff[v] + qb * QR + threadIdx.x] : -1;
+    if (threadIdx.x < QR) {
+        const int pr = (int)threadIdx.x < nval ? qlist[qoff[v] + qb * QR + threadIdx.x] : -1;
+        pairs[threadIdx.x] = pr;
+        qrow_s[threadIdx.x] = pr >= 0 ? pr / nprobe : -1;
+    }
     __syncthreads();
     // transpose through LDS, 64 rows x 64 dims at a time: reads along the
     // query row, writes along QT's row axis, both coalesced
@@ -213,11 +230,17 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
     for (int r0 = 0; r0 < QR; r0 += RT) {
         for (int64_t j0 = j_lo; j0 < j_hi; j0 += 64) {
             const int64_t j = j0 + lane;
-            for (int rr = wv; rr < RT; rr += 4) {
-                const int pr = pairs[r0 + rr];
-                const float qv = pr >= 0 && j < d ? Q[(int64_t)(pr / nprobe) * d + j] : 0.0f;
-                tr[rr][lane] = cpv && j < d ? qv - cpv[j] : qv;
+            // the wave's RT/4 rows: every load issued before the first store
+            constexpr int PER = RT / 4;
+            float qv[PER];
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int qi = qrow_s[r0 + wv + 4 * i];
+                qv[i] = qi >= 0 && j < d ? Q[(int64_t)qi * d + j] : 0.0f;
             }
+            const float cv = cpv && j < d ? cpv[j] : 0.0f;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) tr[wv + 4 * i][lane] = cpv && j < d ? qv[i] - cv : qv[i];
             __syncthreads();
             if (SPLIT) {
                 // units (chunk cc of the slab, g, row): 16 B each, rows fastest
@@ -241,32 +264,60 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
             __syncthreads();
         }
     }
-    // the rows' norms, spread over the slab groups (each row whole in one)
-    for (int r = blockIdx.y + gridDim.y * (threadIdx.x >> 6); r < QR; r += 4 * gridDim.y) {
-        const int pr = pairs[r];
-        double s = 0.0, t = 0.0;
-        if (pr >= 0) {
-            const float *qr = Q + (int64_t)(pr / nprobe) * d;
-            const float *pv = pivot ? pivot + (int64_t)(v >= n_lists ? v - n_lists : v) * d : nullptr;
-            for (int64_t j = lane; j < d; j += 64) {
-                const double x = (double)qr[j];
-                const double xc = cpv ? (double)(qr[j] - cpv[j]) : x;  // the staged value
-                s = __builtin_fma(xc, xc, s);
+    // the rows' norms, spread over the slab groups (each row whole in one);
+    // four rows per wave at a time, so their loads are in flight together
+    const float *pv = pivot ? pivot + (int64_t)(v >= n_lists ? v - n_lists : v) * d : nullptr;
+    constexpr int NM = 4;  // rows per wave at a time (8: GIST1M plan 0.16 -> 0.21 ms)
+    const int rstep = 4 * gridDim.y;
+    for (int r0 = blockIdx.y + gridDim.y * wv; r0 < QR; r0 += NM * rstep) {
+        int qi[NM];
+        double s[NM], t[NM];
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+            const int r = r0 + m * rstep;
+            qi[m] = r < QR ? qrow_s[r] : -1;
+            s[m] = t[m] = 0.0;
+        }
+        for (int64_t j = lane; j < d; j += 64) {
+            const float cv = cpv ? cpv[j] : 0.0f, pj = pv ? pv[j] : 0.0f;
+            float xv[NM];
+#pragma unroll
+            for (int m = 0; m < NM; ++m) xv[m] = qi[m] >= 0 ? Q[(int64_t)qi[m] * d + j] : 0.0f;
+#pragma unroll
+            for (int m = 0; m < NM; ++m) {
+                if (qi[m] < 0) continue;  // (no pair: zero norms)
+                const double x = (double)xv[m];
+                const double xc = cpv ? (double)(xv[m] - cv) : x;  // the staged value
+                s[m] = __builtin_fma(xc, xc, s[m]);
                 if (pv) {
-                    const double df = x - (double)pv[j];
-                    t = __builtin_fma(df, df, t);
+                    const double df = x - (double)pj;
+                    t[m] = __builtin_fma(df, df, t[m]);
                 }
             }
         }
 #pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) {
-            s += __shfl_xor(s, m, 64);
-            t += __shfl_xor(t, m, 64);
+        for (int m = 0; m < NM; ++m) {
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {
+                s[m] += __shfl_xor(s[m], o, 64);
+                t[m] += __shfl_xor(t[m], o, 64);
+            }
         }
-        if (lane == 0) {
-            const float qnu = __double2float_ru(__builtin_sqrt(s) * (1.0 + 0x1p-40));
-            QN[(int64_t)b * QR + r] = make_float4((float)s, qnu, __int_as_float(pr), (float)__builtin_sqrt(t));
-            if (pqn && pr >= 0) pqn[pr] = qnu;
+        if (lane < NM) {  // lane m writes row r0 + m * rstep
+            double sm = s[0], tm = t[0];
+#pragma unroll
+            for (int m = 1; m < NM; ++m)
+                if (lane == m) {
+                    sm = s[m];
+                    tm = t[m];
+                }
+            const int r = r0 + lane * rstep;
+            if (r < QR) {
+                const int pr = pairs[r];
+                const float qnu = __double2float_ru(__builtin_sqrt(sm) * (1.0 + 0x1p-40));
+                QN[(int64_t)b * QR + r] = make_float4((float)sm, qnu, __int_as_float(pr), (float)__builtin_sqrt(tm));
+                if (pqn && pr >= 0) pqn[pr] = qnu;
+            }
         }
     }
 }
@@ -1870,6 +1921,192 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_s(ScreenArgs a) {
 // before k_screen, so no item starts unbounded (which would push a whole
 // first block per row through the selection).
 static constexpr int kSeedTiles = 4;
+// The same bound per group-0 query block (k_plan's first group: the QB pairs
+// whose first probe slot is partition p), one workgroup each: the queries of
+// a block share the partition, so its first NR storage rows (row-major Xr; in
+// radius order its central rows) are staged in LDS once, 32 dims at a time,
+// for all QB queries (k_seed_t reads them once per query).  Lane = query,
+// wave w = rows w, w + 4, ...; each (query, row) score is one lane's
+// sequential sum in search.cpp's order, two rows per packed fp32 instruction
+// (v_pk_add_f32 / v_pk_mul_f32 round each half like the scalar ops).  Each
+// lane keeps its 8 smallest valid scores per wave; the k-th smallest of the
+// four waves' lists has >= k distinct rows at or below it, so it bounds the
+// final k-th exact score (k <= 32).
+template <int METRIC, int QB, int NR>
+__global__ __launch_bounds__(256) void k_seed_b(const float *Q, int64_t d, int nprobe, int n_lists,
+                                                const int32_t *cnt, const int32_t *qoff, const int32_t *qlist,
+                                                const int32_t *qblk_off, const int32_t *tile_off,
+                                                const int32_t *ids, const float *Xr, int k, uint32_t *qbound) {
+    static_assert(QB == 64 && NR % 4 == 0, "lane = query");
+    constexpr int RW = NR / 4, DS = 32;
+    __shared__ float4 xs[NR][DS / 4];
+    __shared__ float qs[DS][QB + 1];
+    __shared__ int s_v, s_q[QB], s_ok[NR];
+    __shared__ float s_m[4][8][QB];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int b = blockIdx.x;
+    if (b >= qblk_off[n_lists]) return;  // (group 0: v < n_lists)
+    if (w == 0) {
+        const int v = wave_find_owner(qblk_off, n_lists, b);
+        if (lane == 0) s_v = v;
+    }
+    __syncthreads();
+    const int p = s_v, qb = b - qblk_off[p];
+    const int nval = min(QB, cnt[p] - qb * QB);
+    const int tile0 = tile_off[p], nrow = min(NR, (tile_off[p + 1] - tile0) * kTile);
+    const int64_t row0 = (int64_t)tile0 * kTile;
+    if (tid < QB) s_q[tid] = tid < nval ? qlist[qoff[p] + qb * QB + tid] / nprobe : -1;
+    for (int r = tid; r < NR; r += 256) s_ok[r] = r < nrow && ids[row0 + r] >= 0;
+    __syncthreads();
+    f2 acc[RW / 2];  // rows 8r + w, 8r + 4 + w (wave w: rows w, w + 4, ... -- every wave
+                     // gets central and outer rows of the radius order alike)
+#pragma unroll
+    for (int r = 0; r < RW / 2; ++r) acc[r] = (f2)(0.0f);
+    // staging: thread tid moves the 16-B pieces e = tid + 256 i (row e / 8,
+    // dims 4 (e % 8) ..), all loads of a slab in flight together, the next
+    // slab's loaded into registers while this one is computed
+    constexpr int XP = NR * DS / 4 / 256, QP = QB * DS / 4 / 256;  // pieces per thread
+    const bool v4 = (d & 3) == 0;
+    float4 xr[XP], qr[QP];
+    auto load = [&](int64_t j0) {
+        const int nj = (int)min<int64_t>(DS, d - j0);
+#pragma unroll
+        for (int i = 0; i < XP; ++i) {
+            const int e = tid + 256 * i, r = e >> 3, c = 4 * (e & 7);
+            const float *src = Xr + (row0 + r) * d + j0 + c;
+            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (r < nrow && v4 && c + 4 <= nj) {
+                v = *(const float4 *)src;
+            } else if (r < nrow) {
+                if (c < nj) v.x = src[0];
+                if (c + 1 < nj) v.y = src[1];
+                if (c + 2 < nj) v.z = src[2];
+                if (c + 3 < nj) v.w = src[3];
+            }
+            xr[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < QP; ++i) {
+            const int e = tid + 256 * i, qq = e >> 3, c = 4 * (e & 7), qi = s_q[qq];
+            const float *src = Q + (int64_t)qi * d + j0 + c;
+            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (qi >= 0 && v4 && c + 4 <= nj) {
+                v = *(const float4 *)src;
+            } else if (qi >= 0) {
+                if (c < nj) v.x = src[0];
+                if (c + 1 < nj) v.y = src[1];
+                if (c + 2 < nj) v.z = src[2];
+                if (c + 3 < nj) v.w = src[3];
+            }
+            qr[i] = v;
+        }
+    };
+    load(0);
+    for (int64_t j0 = 0; j0 < d; j0 += DS) {
+        const int nj = (int)min<int64_t>(DS, d - j0);
+#pragma unroll
+        for (int i = 0; i < XP; ++i) {
+            const int e = tid + 256 * i;
+            xs[e >> 3][e & 7] = xr[i];
+        }
+#pragma unroll
+        for (int i = 0; i < QP; ++i) {
+            const int e = tid + 256 * i, qq = e >> 3, c = 4 * (e & 7);
+            qs[c][qq] = qr[i].x;
+            qs[c + 1][qq] = qr[i].y;
+            qs[c + 2][qq] = qr[i].z;
+            qs[c + 3][qq] = qr[i].w;
+        }
+        __syncthreads();
+        if (j0 + DS < d) load(j0 + DS);
+        for (int c4 = 0; c4 < DS / 4 && 4 * c4 < nj; ++c4) {
+            const int nc = min(4, nj - 4 * c4);  // (workgroup-uniform)
+            const f2 q0 = (f2)(qs[4 * c4][lane]), q1 = (f2)(qs[4 * c4 + 1][lane]);
+            const f2 q2 = (f2)(qs[4 * c4 + 2][lane]), q3 = (f2)(qs[4 * c4 + 3][lane]);
+            if (nc == 4) {
+#pragma unroll
+                for (int r = 0; r < RW / 2; ++r) {  // rows 8r + w and 8r + 4 + w, packed
+                    const float4 xa = xs[8 * r + w][c4], xb = xs[8 * r + 4 + w][c4];
+                    const f2 x0 = {xa.x, xb.x}, x1 = {xa.y, xb.y}, x2 = {xa.z, xb.z}, x3 = {xa.w, xb.w};
+                    if (METRIC == LIRA_METRIC_L2) {
+                        f2 df = q0 - x0;
+                        acc[r] = acc[r] + df * df;
+                        df = q1 - x1;
+                        acc[r] = acc[r] + df * df;
+                        df = q2 - x2;
+                        acc[r] = acc[r] + df * df;
+                        df = q3 - x3;
+                        acc[r] = acc[r] + df * df;
+                    } else {
+                        acc[r] = acc[r] + q0 * x0;
+                        acc[r] = acc[r] + q1 * x1;
+                        acc[r] = acc[r] + q2 * x2;
+                        acc[r] = acc[r] + q3 * x3;
+                    }
+                }
+            } else {  // the last dims of d (d % 4 != 0)
+                const f2 qq[4] = {q0, q1, q2, q3};
+                for (int u = 0; u < nc; ++u) {
+#pragma unroll
+                    for (int r = 0; r < RW / 2; ++r) {
+                        const f2 xv = {((const float *)&xs[8 * r + w][c4])[u], ((const float *)&xs[8 * r + 4 + w][c4])[u]};
+                        if (METRIC == LIRA_METRIC_L2) {
+                            const f2 df = qq[u] - xv;
+                            acc[r] = acc[r] + df * df;
+                        } else {
+                            acc[r] = acc[r] + qq[u] * xv;
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // this lane's 8 smallest valid scores of the wave's RW rows, sorted
+    float m[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) m[i] = __builtin_inff();
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+        const int row = 8 * (r >> 1) + 4 * (r & 1) + w;
+        const float a = (r & 1) ? acc[r >> 1].y : acc[r >> 1].x;
+        const float sc = METRIC == LIRA_METRIC_L2 ? a : -a;
+        float v = s_ok[row] && sc == sc ? sc : __builtin_inff();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float lo = fminf(m[i], v), hi = fmaxf(m[i], v);
+            m[i] = lo;
+            v = hi;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s_m[w][i][lane] = m[i];
+    __syncthreads();
+    // the k-th smallest of the four lists' union: >= k rows at or below it
+    // (the exact k-th over all NR rows for k <= 8)
+    if (w == 0 && s_q[lane] >= 0) {
+        int h[4] = {0, 0, 0, 0};
+        float B = __builtin_inff();
+        for (int e = 0; e < k; ++e) {
+            float best = __builtin_inff();
+            int bw = -1;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const float v = h[u] < 8 ? s_m[u][h[u]][lane] : __builtin_inff();
+                if (v < best) {
+                    best = v;
+                    bw = u;
+                }
+            }
+            B = best;
+            if (bw < 0) break;  // fewer than k valid rows: no bound
+#pragma unroll
+            for (int u = 0; u < 4; ++u) h[u] += bw == u;
+        }
+        if (B < __builtin_inff()) qbound[s_q[lane]] = f2ord(B);
+    }
+}
+
 // The same bound from the fp32 tiles where the index keeps them (one wave per
 // query, lane = candidate: each dim of a tile is one coalesced 256-B row).
 // NT tiles: 2 for k <= 32 (measured SIFT1M mixture: plan 0.217 -> 0.164 ms,
@@ -2552,7 +2789,29 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
                            (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn);
     LIRA_HIP_TRY(hipGetLastError());
     // (measured: SIFT1M mixture 1.70 -> 1.44 ms, latent +1 %)
-    if (qbound && o.seed && idx->X) {  // from the fp32 tiles (coalesced)
+    // LIRA_OPT_SEED 2 / 3: per nearest-partition query block (k_seed_b, 128 /
+    // 256 rows) where the plan has that group.  Measured SIFT1M: the same
+    // survivors as k_seed_t's 128 rows, plan 0.122 -> 0.143 ms (~220 workgroups
+    // of exact VALU work leave most of the chip idle); 256 rows: survivors
+    // -28 %, scan -0.02 ms, plan +0.06 ms.  So the per-query seed is the default.
+    const bool seed_b = qbound && (o.seed == 2 || o.seed == 3) && groups == 2 && k <= 32 && pl.qr == 64 &&
+                        idx->d <= 256;
+    if (seed_b) {
+        const dim3 g((unsigned)std::min<int64_t>(pl.max_qblk, (nq + 63) / 64 + idx->n_lists));
+        if (idx->metric == LIRA_METRIC_L2 && o.seed == 3)
+            hipLaunchKernelGGL((k_seed_b<LIRA_METRIC_L2, 64, 256>), g, dim3(256), 0, st, q, idx->d, (int)nprobe,
+                               (int)idx->n_lists, cnt, qoff, qlist, qblk, idx->tile_off, idx->ids, idx->Xr, (int)k, qbound);
+        else if (idx->metric == LIRA_METRIC_L2)
+            hipLaunchKernelGGL((k_seed_b<LIRA_METRIC_L2, 64, 128>), g, dim3(256), 0, st, q, idx->d, (int)nprobe,
+                               (int)idx->n_lists, cnt, qoff, qlist, qblk, idx->tile_off, idx->ids, idx->Xr, (int)k, qbound);
+        else if (o.seed == 3)
+            hipLaunchKernelGGL((k_seed_b<LIRA_METRIC_IP, 64, 256>), g, dim3(256), 0, st, q, idx->d, (int)nprobe,
+                               (int)idx->n_lists, cnt, qoff, qlist, qblk, idx->tile_off, idx->ids, idx->Xr, (int)k, qbound);
+        else
+            hipLaunchKernelGGL((k_seed_b<LIRA_METRIC_IP, 64, 128>), g, dim3(256), 0, st, q, idx->d, (int)nprobe,
+                               (int)idx->n_lists, cnt, qoff, qlist, qblk, idx->tile_off, idx->ids, idx->Xr, (int)k, qbound);
+        LIRA_HIP_TRY(hipGetLastError());
+    } else if (qbound && o.seed && idx->X) {  // from the fp32 tiles (coalesced)
         const dim3 g((unsigned)((nq + 3) / 4));
         if (idx->metric == LIRA_METRIC_L2 && k <= 32)
             hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2, 2>), g, dim3(256), 0, st, q, probe, (int)nprobe,

@@ -368,7 +368,7 @@ def test_options_do_not_change_results(metric):
     x, q, d2b, probe = clustered_case(61, 20000, 48, 8, 700, 3)
     idx = make_index(x, d2b, 8, metric)
     ref = run(idx, q, probe, 10)
-    for name, vals in (("qr", (128,)), ("two_phase", (0, 2)), ("seed", (0,)), ("share", (0,)),
+    for name, vals in (("qr", (128,)), ("two_phase", (0, 2)), ("seed", (0, 2, 3)), ("share", (0,)),
                        ("prune", (0,)), ("split", (0,)), ("mfma", (0, 2)), ("rounds", (1, 64)),
                        ("near_rounds", (8,)), ("screen", (0,)), ("ring", (2, 3, 4)), ("probes_hint", (1, 4)), ("xhi", (0, 1))):
         old = idx.get_option(name)
