@@ -38,10 +38,27 @@ __device__ __forceinline__ int32_t key_gid(u64 k) { return (int32_t)(uint32_t)(k
 __device__ __forceinline__ u64 kmin(u64 a, u64 b) { return a < b ? a : b; }
 __device__ __forceinline__ u64 kmax(u64 a, u64 b) { return a < b ? b : a; }
 
+// lane ^ m exchange.  Inside a 16-lane DPP row it is VALU work: quad_perm for
+// m = 1, 2, row_ror:8 for 8, row_shl:4 / row_shr:4 and a select for 4;
+// m = 16 is one ds_swizzle (bit mode, within 32 lanes); only m = 32 takes a
+// ds_bpermute.  (__shfl_xor compiled every one of them to ds_bpermute, an LDS
+// round trip per step of the sorting networks.)  m is a constant after the
+// callers' unrolling, so the chain folds to one form.
+__device__ __forceinline__ uint32_t xor_u32(uint32_t v, int m) {
+    const int x = (int)v;
+    if (m == 1) return (uint32_t)__builtin_amdgcn_update_dpp(x, x, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+    if (m == 2) return (uint32_t)__builtin_amdgcn_update_dpp(x, x, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+    if (m == 4) {
+        const int up = __builtin_amdgcn_update_dpp(x, x, 0x104, 0xf, 0xf, false);  // row_shl:4: lane + 4
+        const int dn = __builtin_amdgcn_update_dpp(x, x, 0x114, 0xf, 0xf, false);  // row_shr:4: lane - 4
+        return (uint32_t)((threadIdx.x & 4) ? dn : up);
+    }
+    if (m == 8) return (uint32_t)__builtin_amdgcn_update_dpp(x, x, 0x128, 0xf, 0xf, false);  // row_ror:8
+    if (m == 16) return (uint32_t)__builtin_amdgcn_ds_swizzle(x, 0x401F);  // and 0x1f, xor 0x10
+    return (uint32_t)__shfl_xor(x, m, 64);
+}
 __device__ __forceinline__ u64 shfl_xor64(u64 v, int m) {
-    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-    lo = __shfl_xor((int)lo, m, 64);
-    hi = __shfl_xor((int)hi, m, 64);
+    const uint32_t lo = xor_u32((uint32_t)v, m), hi = xor_u32((uint32_t)(v >> 32), m);
     return ((u64)hi << 32) | lo;
 }
 __device__ __forceinline__ u64 shfl64(u64 v, int src) {

@@ -402,6 +402,33 @@ __device__ __forceinline__ void pkfma_hi(f2 &acc, f2 x, f2 q) {
     asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(x), "v"(q));
 }
 
+// Inclusive prefix sum within each 16-lane group (= DPP row): 4 row_shr
+// steps with zero fill, no LDS round trips (a __shfl_up chain was 4
+// dependent ds_bpermutes per selection pass)
+__device__ __forceinline__ int row16_incl_scan(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);  // row_shr:8
+    return v;
+}
+// lane 15 of each 16-lane group, broadcast to the group (the group's total)
+__device__ __forceinline__ int row16_total(int inc) {
+    const int t0 = __builtin_amdgcn_readlane(inc, 15), t1 = __builtin_amdgcn_readlane(inc, 31);
+    const int t2 = __builtin_amdgcn_readlane(inc, 47), t3 = __builtin_amdgcn_readlane(inc, 63);
+    const int g = (int)(threadIdx.x & 63) >> 4;
+    return g == 0 ? t0 : g == 1 ? t1 : g == 2 ? t2 : t3;
+}
+// the value lane 4 g + reg holds (lanes 0..15: one per query row), for every
+// lane of group g (4 v_readlane instead of a ds_bpermute)
+__device__ __forceinline__ float from_row_lane(float v, int reg, int g) {
+    const float a0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), reg));
+    const float a1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 4 + reg));
+    const float a2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 8 + reg));
+    const float a3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 12 + reg));
+    return g == 0 ? a0 : g == 1 ? a1 : g == 2 ? a2 : a3;
+}
+
 // 64 u32 values, one per lane: ascending bitonic sort.
 __device__ __forceinline__ uint32_t wave_sort64_u32(uint32_t v) {
     const int lane = lane_id();
@@ -409,7 +436,7 @@ __device__ __forceinline__ uint32_t wave_sort64_u32(uint32_t v) {
     for (int size = 2; size <= 64; size <<= 1) {
 #pragma unroll
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            const uint32_t o = (uint32_t)__shfl_xor((int)v, stride, 64);
+            const uint32_t o = xor_u32(v, stride);
             const bool lower = (lane & stride) == 0, asc = (lane & size) == 0;
             v = (lower == asc) ? min(v, o) : max(v, o);
         }
@@ -431,6 +458,25 @@ __device__ __forceinline__ void s_flush(u64 *L, const u64 *buf, int n) {
 #pragma unroll
         for (int r = 0; r < RL; ++r) L[r * 32 + hl] = lst[r];
     }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Two rows at once: half 0 merges buffer A (na keys) into list A, half 1
+// buffer B into list B (the half-wave network sorts both halves independently).
+template <int RL>
+__device__ __forceinline__ void s_flush2(u64 *LA, const u64 *bufA, int na, u64 *LB, const u64 *bufB, int nb) {
+    const int hl = lane_id() & 31;
+    const bool hi = lane_id() >= 32;
+    u64 *L = hi ? LB : LA;
+    const u64 *buf = hi ? bufB : bufA;
+    const int n = hi ? nb : na;
+    u64 lst[RL];
+#pragma unroll
+    for (int r = 0; r < RL; ++r) lst[r] = L[r * 32 + hl];
+    const u64 b = hl < n ? buf[hl] : kEmptyKey;
+    half_merge_batch1<RL>(lst, b);
+#pragma unroll
+    for (int r = 0; r < RL; ++r) L[r * 32 + hl] = lst[r];
     __builtin_amdgcn_wave_barrier();
 }
 
@@ -1260,7 +1306,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
 
             float h_r[4];
 #pragma unroll
-            for (int reg = 0; reg < 4; ++reg) h_r[reg] = __shfl(h_l, 4 * g + reg, 64);
+            for (int reg = 0; reg < 4; ++reg) h_r[reg] = from_row_lane(h_l, reg, g);
 
             // ---- selection: per output register reg, lane group g holds row
             // 4g + reg's 16 candidates; the four rows of a reg go together
@@ -1314,7 +1360,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                     for (int size = 2; size <= 16; size <<= 1)  // ascending sort within each 16-lane group
 #pragma unroll
                         for (int stride = size >> 1; stride > 0; stride >>= 1) {
-                            const uint32_t o = (uint32_t)__shfl_xor((int)key16, stride, 64);
+                            const uint32_t o = xor_u32(key16, stride);
                             const bool lower = (cj & stride) == 0, asc = (cj & size) == 0;
                             key16 = (lower == asc) ? min(key16, o) : max(key16, o);
                         }
@@ -1344,13 +1390,8 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                     const int row = wave * 16 + 4 * g + reg;
                     const int bc0 = m_bufc[row];
                     const int n_l = __builtin_popcount(pm);
-                    int inc = n_l;  // inclusive prefix over the group's 16 lanes
-#pragma unroll
-                    for (int dl = 1; dl < 16; dl <<= 1) {
-                        const int o = __shfl_up(inc, dl, 16);
-                        if (cj >= dl) inc += o;
-                    }
-                    const int rowtot = __shfl(inc, 16 * g + 15, 64);
+                    const int inc = row16_incl_scan(n_l);  // inclusive prefix over the group's 16 lanes
+                    const int rowtot = row16_total(inc);
                     const bool pre = bc0 > 0 && bc0 + rowtot > BC;  // merge the buffer first
                     const int total = (pre ? 0 : bc0) + rowtot;    // the row's keys in buffer order
                     const int base = (pre ? 0 : bc0) + inc - n_l;  // rank of my first key
@@ -1362,7 +1403,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                             const int gg = __builtin_ctzll(fl) >> 4;
                             fl &= fl - 1;
                             const int r = wave * 16 + 4 * gg + reg;
-                            s_flush<RL>(lists + r * K2, bufs + r * BC, r0 == 0 ? __shfl(bc0, 16 * gg, 64) : BC);
+                            s_flush<RL>(lists + r * K2, bufs + r * BC, r0 == 0 ? __builtin_amdgcn_readlane(bc0, 16 * gg) : BC);
                         }
                         int rank = base;
 #pragma unroll
@@ -1389,12 +1430,32 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
         }
 
         if (clk) t_2 = clock64();
-        // ---- flush buffers, emit lists, publish bounds (wave-owned rows)
+        // ---- flush buffers, emit lists, publish bounds (wave-owned rows);
+        // buffers flushed two rows per network pass (one row per half-wave:
+        // the per-item epilogue was ~8 % of the screen's cycles on SIFT1M latent)
+        {
+            const int nb = lane < 16 ? m_bufc[wave * 16 + lane] : 0;
+            u64 pend = __ballot(lane < 16 && nb > 0);
+            while (pend) {
+                const int ra = __builtin_ctzll(pend);
+                pend &= pend - 1;
+                int rb = -1;
+                if (pend) {
+                    rb = __builtin_ctzll(pend);
+                    pend &= pend - 1;
+                }
+                const int rowa = wave * 16 + ra, na = __builtin_amdgcn_readlane(nb, ra);
+                if (rb >= 0) {
+                    const int rowb = wave * 16 + rb, nbb = __builtin_amdgcn_readlane(nb, rb);
+                    s_flush2<RL>(lists + rowa * K2, bufs + rowa * BC, na, lists + rowb * K2, bufs + rowb * BC, nbb);
+                } else {
+                    s_flush<RL>(lists + rowa * K2, bufs + rowa * BC, na);
+                }
+            }
+        }
 #pragma unroll 1
         for (int r = 0; r < 16; ++r) {
             const int row = wave * 16 + r;
-            const int bc = m_bufc[row];
-            if (bc > 0) s_flush<RL>(lists + row * K2, bufs + row * BC, bc);
             const int pr = m_pair[row];
             if (pr >= 0) {
                 u64 *dst = a.partial + ((int64_t)pr * a.nch_max + ch) * K2;
@@ -1757,7 +1818,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_s(ScreenArgs a) {
                 const int tb = c_tb;
                 float h_r[4];
 #pragma unroll
-                for (int reg = 0; reg < 4; ++reg) h_r[reg] = __shfl(h_l, 4 * g + reg, 64);
+                for (int reg = 0; reg < 4; ++reg) h_r[reg] = from_row_lane(h_l, reg, g);
 #pragma unroll
                 for (int reg = 0; reg < 4; ++reg) {
                     float h = h_r[reg];
@@ -1804,7 +1865,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_s(ScreenArgs a) {
                         for (int size = 2; size <= 16; size <<= 1)
 #pragma unroll
                             for (int stride = size >> 1; stride > 0; stride >>= 1) {
-                                const uint32_t o = (uint32_t)__shfl_xor((int)key16, stride, 64);
+                                const uint32_t o = xor_u32(key16, stride);
                                 const bool lower = (cj & stride) == 0, asc = (cj & size) == 0;
                                 key16 = (lower == asc) ? min(key16, o) : max(key16, o);
                             }
@@ -1825,13 +1886,8 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_s(ScreenArgs a) {
                         const int row = wave * 16 + 4 * g + reg;
                         const int bc0 = m_bufc[row];
                         const int n_l = __builtin_popcount(pm);
-                        int inc = n_l;  // inclusive prefix over the group's 16 lanes
-#pragma unroll
-                        for (int dl = 1; dl < 16; dl <<= 1) {
-                            const int o = __shfl_up(inc, dl, 16);
-                            if (cj >= dl) inc += o;
-                        }
-                        const int rowtot = __shfl(inc, 16 * g + 15, 64);
+                        const int inc = row16_incl_scan(n_l);  // inclusive prefix over the group's 16 lanes
+                        const int rowtot = row16_total(inc);
                         const bool pre = bc0 > 0 && bc0 + rowtot > BC;
                         const int total = (pre ? 0 : bc0) + rowtot;
                         const int base = (pre ? 0 : bc0) + inc - n_l;
@@ -1841,7 +1897,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_s(ScreenArgs a) {
                                 const int gg = __builtin_ctzll(fl) >> 4;
                                 fl &= fl - 1;
                                 const int r = wave * 16 + 4 * gg + reg;
-                                s_flush<RL>(lists + r * K2, bufs + r * BC, r0 == 0 ? __shfl(bc0, 16 * gg, 64) : BC);
+                                s_flush<RL>(lists + r * K2, bufs + r * BC, r0 == 0 ? __builtin_amdgcn_readlane(bc0, 16 * gg) : BC);
                             }
                             int rank = base;
 #pragma unroll
