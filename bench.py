@@ -220,18 +220,19 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
     cand = int(ncand.sum().item())
     dpad = (d + 31) // 32 * 32
     qr = int(kernel.split("QR=")[1].split()[0]) if "QR=" in kernel else 64
-    split = "split-bf16" in kernel
+    hh = "hi-q" in kernel  # hi x hi: 1 product per dim (qh x xh), hi parts of x and q staged
+    split = "split-bf16" in kernel or hh
     hix = "hi-x" in kernel  # hi-only x: 2 products per dim (qh, ql) x xh, half the X bytes
     if kernel.startswith("k_screen_m"):
         # (row, cand) pairs x dpad x products x 2
-        flops = work["chunks_computed"] * dpad * (4 if hix else 8 if split else 2)
+        flops = work["chunks_computed"] * dpad * (2 if hh else 4 if hix else 8 if split else 2)
         mfma_peak = MFMA_BF16_PEAK_TFLOPS if split else MFMA_F32_PEAK_TFLOPS
         mfma_what = "bf16 MFMA" if split else "fp32 MFMA"
     else:
         flops = work["chunks_computed"] * dpad * 2
         mfma_peak, mfma_what = MFMA_F32_PEAK_TFLOPS, "fp32 VALU (v_pk_fma_f32)"
     # L2 -> LDS bytes (LDS-DMA) per launch: X (256 candidates), Q (qr rows), xadj
-    staged = work["blocks"] * (256 * dpad * (2 if hix else 4) + qr * dpad * 4 + 1024)
+    staged = work["blocks"] * (256 * dpad * (2 if hix else 4) + qr * dpad * (2 if hh else 4) + 1024)
     traffic, pmc_src = None, None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_scan_{args.config}_{data}.json")
     if os.path.exists(pmc_path):

@@ -150,7 +150,9 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *                        padding (a threshold selection padded to B): sizes the work split (0 = nprobe_max)
  *   LIRA_OPT_XHI         1: the split screen multiplies the query's hi + lo parts by x's hi part only
  *                        (half the staged bytes and MFMAs, a 2^-8 wider bound, more exact re-checks);
- *                        0: hi and lo; -1 (default): 1 for L2 (centred copy), 0 for IP
+ *                        0: hi and lo; 2: hi parts of x and of the queries, 32 dims per MFMA
+ *                        (k <= 24, else as 1; half the MFMAs again, bound + ||q - hi(q)|| (R + ..));
+ *                        -1 (default): 2 for L2 (centred copy), 0 for IP
  *   LIRA_OPT_ORDER       (build time: set before lira_index_add_partitions) 1 (default, L2): store
  *                        each list's rows by ascending distance to the list's pivot, so tile radius
  *                        ranges are narrow and the triangle-inequality skip drops more; 0: list order.

@@ -720,7 +720,7 @@ int lira_index_set_option(lira_index *idx, int option, int64_t value) {
         case LIRA_OPT_PIPELINE: if (!in(0, 1)) break; o.pipeline = v; return LIRA_OK;
         case LIRA_OPT_RING: if (!in(0, 4)) break; o.ring = v; return LIRA_OK;
         case LIRA_OPT_PROBES_HINT: if (!in(0, 1 << 20)) break; o.probes_hint = v; return LIRA_OK;
-        case LIRA_OPT_XHI: if (!in(-1, 1)) break; o.xhi = v; return LIRA_OK;
+        case LIRA_OPT_XHI: if (!in(-1, 2)) break; o.xhi = v; return LIRA_OK;
         case LIRA_OPT_ORDER: if (!in(0, 1)) break; o.order = v; return LIRA_OK;
         default: return fail(LIRA_EINVAL, "unknown option " + std::to_string(option));
     }

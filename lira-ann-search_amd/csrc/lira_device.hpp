@@ -68,6 +68,13 @@ __device__ __forceinline__ u64 shfl64(u64 v, int src) {
     return ((u64)hi << 32) | lo;
 }
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+// lane l <- lane (l & 32) | (31 - (l & 31)): reversal inside each 32-lane half,
+// one ds_swizzle (bit mode: and 0x1f, xor 0x1f) per dword
+__device__ __forceinline__ u64 rev32_u64(u64 v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)v, 0x7C1F);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)(v >> 32), 0x7C1F);
+    return ((u64)hi << 32) | lo;
+}
 
 // Full ascending bitonic sort of 64 keys, one per lane.
 __device__ __forceinline__ u64 wave_sort64(u64 v) {
@@ -222,8 +229,8 @@ __device__ __forceinline__ void half_merge_batch(u64 (&list)[R], u64 (&batch)[2]
     static_assert(R >= 2, "half-wave lists hold at least 64 keys");
     const int lane = lane_id();
     half_sort<2>(batch);
-    const int src = (lane & 32) | (31 - (lane & 31));
-    const u64 rev0 = shfl64(batch[1], src), rev1 = shfl64(batch[0], src);
+    (void)lane;
+    const u64 rev0 = rev32_u64(batch[1]), rev1 = rev32_u64(batch[0]);
     list[R - 2] = kmin(list[R - 2], rev0);
     list[R - 1] = kmin(list[R - 1], rev1);
     half_bitonic_merge<R>(list);
@@ -236,7 +243,8 @@ __device__ __forceinline__ void half_merge_batch1(u64 (&list)[R], u64 batch) {
     const int lane = lane_id();
     u64 b[1] = {batch};
     half_sort<1>(b);
-    const u64 rev = shfl64(b[0], (lane & 32) | (31 - (lane & 31)));
+    (void)lane;
+    const u64 rev = rev32_u64(b[0]);
     list[R - 1] = kmin(list[R - 1], rev);
     half_bitonic_merge<R>(list);
 }

@@ -73,6 +73,7 @@ struct ScreenArgs {
     int32_t *head;
     const float *QT;       // [qblk][dpad][QR]
     const float4 *QN;      // [qblk*QR]: qn, |q| (up), pair (int bits), 0
+    const float *QE;       // [qblk*QR]: ||q - hi(q)|| (up) of the staged row (SPLIT 3)
     u64 *partial;          // [pair][nch_max][K2]
     float *pE;             // [pair][nch_max]: k_screen_m's bound on its listed keys' screening error
     uint32_t *qbound;      // [nq] f2ord(bound on the final k-th exact score); NULL = off
@@ -109,10 +110,25 @@ struct ScreenArgs {
 // (q - c) e1 - (x - c) e2 with |e| <= u per component, so ||q'-x'||^2 differs
 // from D = ||q-x||^2 by at most u s (2 + u) s (1 + u) <= 2.01 u s^2, s = qnorm
 // + R, on top of the screen's own error for q', x'.
+//
+// split == 3 (hi x hi, k_screen_m<..., 3>): dot~ = sum qh xh, one product per
+// dim (exact in fp32), so q.x - dot~ = q.(x - xh) + (q - qh).xh and
+// |dot~ - q.x| <= |q| ||ex|| + qres (R + ||ex||) + (2 dpad 2^-22) 1.02 |q| (R +
+// ||ex||) + the subnormal term, qres >= ||q - qh|| of the row (k_qstage, QE).
 template <int METRIC>
 __device__ __forceinline__ double err_E(double qnorm, double R, double d, int split = 0, double dp = 0.0,
-                                        int centred = 0, double hres = -1.0) {
+                                        int centred = 0, double hres = -1.0, double qres = 0.0) {
     const double dl = d * 0x1p-140;
+    if (split == 3) {
+        const double ex = hres >= 0.0 ? hres * 1.0001 : 0x1p-8 * 1.02 * R;
+        const double ed = ex * qnorm + qres * (R + ex) * 1.0001 + 2.0 * dp * 0x1p-22 * 1.02 * qnorm * (R + ex) +
+                          2.0 * dp * 0x1p-96 * (qnorm + R + ex + 1.0);
+        if (METRIC == LIRA_METRIC_L2) {
+            const double s = qnorm + R;
+            return 2.0 * ed + (1.05 * 8.0 + (centred ? 2.01 : 0.0)) * kU * s * s + dl;
+        }
+        return 1.05 * (ed + (d + 2.0) * kU * qnorm * R) + dl;
+    }
     if (split) {
         // split == 2 (hi-only x, k_screen_m<..., 2>): dot~ = sum (qh + ql) xh, x = xh + ex:
         // |dot~ - q.x| <= |q.ex| + |(q - qh - ql).xh| + rounding <= |q| ||ex|| +
@@ -200,7 +216,8 @@ template <int QR, bool SPLIT>
 __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64_t dpad, int nprobe,
                                                 int n_virt, int n_lists, const int32_t *cnt, const int32_t *qoff,
                                                 const int32_t *qlist, const int32_t *qblk_off, const float *pivot,
-                                                const float *cpivot, float *QT, float4 *QN, float *pqn) {
+                                                const float *cpivot, float *QT, float4 *QN, float *pqn,
+                                                float *QE) {
     __shared__ int pairs[QR], qrow_s[QR];
     __shared__ int s_v;
     __shared__ float tr[64][65];
@@ -271,12 +288,12 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
     const int rstep = 4 * gridDim.y;
     for (int r0 = blockIdx.y + gridDim.y * wv; r0 < QR; r0 += NM * rstep) {
         int qi[NM];
-        double s[NM], t[NM];
+        double s[NM], t[NM], e[NM];  // e: the hi parts' residual (QE)
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
             const int r = r0 + m * rstep;
             qi[m] = r < QR ? qrow_s[r] : -1;
-            s[m] = t[m] = 0.0;
+            s[m] = t[m] = e[m] = 0.0;
         }
         for (int64_t j = lane; j < d; j += 64) {
             const float cv = cpv ? cpv[j] : 0.0f, pj = pv ? pv[j] : 0.0f;
@@ -287,8 +304,13 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
             for (int m = 0; m < NM; ++m) {
                 if (qi[m] < 0) continue;  // (no pair: zero norms)
                 const double x = (double)xv[m];
-                const double xc = cpv ? (double)(xv[m] - cv) : x;  // the staged value
+                const float sv = cpv ? xv[m] - cv : xv[m];  // the staged value
+                const double xc = (double)sv;
                 s[m] = __builtin_fma(xc, xc, s[m]);
+                if (SPLIT && QE) {  // sv - hi(sv): exact in fp32
+                    const double rr = (double)(sv - __uint_as_float(bf16_rne_sat(sv) << 16));
+                    e[m] = __builtin_fma(rr, rr, e[m]);
+                }
                 if (pv) {
                     const double df = x - (double)pj;
                     t[m] = __builtin_fma(df, df, t[m]);
@@ -301,15 +323,17 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
             for (int o = 32; o >= 1; o >>= 1) {
                 s[m] += __shfl_xor(s[m], o, 64);
                 t[m] += __shfl_xor(t[m], o, 64);
+                if (SPLIT && QE) e[m] += __shfl_xor(e[m], o, 64);
             }
         }
         if (lane < NM) {  // lane m writes row r0 + m * rstep
-            double sm = s[0], tm = t[0];
+            double sm = s[0], tm = t[0], em = e[0];
 #pragma unroll
             for (int m = 1; m < NM; ++m)
                 if (lane == m) {
                     sm = s[m];
                     tm = t[m];
+                    em = e[m];
                 }
             const int r = r0 + lane * rstep;
             if (r < QR) {
@@ -317,6 +341,7 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
                 const float qnu = __double2float_ru(__builtin_sqrt(sm) * (1.0 + 0x1p-40));
                 QN[(int64_t)b * QR + r] = make_float4((float)sm, qnu, __int_as_float(pr), (float)__builtin_sqrt(tm));
                 if (pqn && pr >= 0) pqn[pr] = qnu;
+                if (SPLIT && QE) QE[(int64_t)b * QR + r] = __double2float_ru(__builtin_sqrt(em) * (1.0 + 0x1p-40));
             }
         }
     }
@@ -325,15 +350,17 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
 // ---- the screening kernel --------------------------------------------------
 // MF: the k_screen_m carve (xadj stage, block ranges); XH: hi-only x
 // (k_screen_m<..., SPLIT = 2>): half the X bytes per chunk and a 3-deep ring
-template <int QR, int RL, bool MF = false, bool XH = false>
+// HH: the hi x hi screen (k_screen_m<..., SPLIT = 3>): a slot holds 32 dims, the
+// hi parts of x (4 KiB per tile) and of the queries (QR * 64 B), 2 slots
+template <int QR, int RL, bool MF = false, bool XH = false, bool HH = false>
 struct SSmem {
     static constexpr int RW = QR / 4, K2 = 32 * RL, BC = 32;
-    static constexpr int kXT = (XH ? 2 : 4) * 1024;         // one tile's chunk (XH: the hi parts)
+    static constexpr int kXT = (XH ? 2 : 4) * 1024;         // one tile's chunk (XH: the hi parts; HH: 32 dims of them)
     static constexpr int kXS = kSBT * kXT;                  // X chunk: 16 KiB (XH: 8)
-    static constexpr int kQS = kSDK * QR * 4;               // Q chunk: 4 KiB at QR = 64
+    static constexpr int kQS = kSDK * QR * 4;               // Q chunk: 4 KiB at QR = 64 (HH: 32 dims of hi parts)
     static constexpr int kXA = 0;                           // (k_screen: none)
     static constexpr int kStage = kXS + kQS + kXA;
-    static constexpr int NSL = XH ? 3 : 2;                  // ring slots
+    static constexpr int NSL = XH && !HH ? 3 : 2;           // ring slots
     // (MF) the xadj of the last two blocks, [2][256] (staged with a block's first chunk)
     static constexpr int kXB = MF ? 2 * kSBT * kTile * 4 : 0;
     static constexpr int kX = NSL * kStage + kXB;
@@ -343,7 +370,7 @@ struct SSmem {
     // ||q - pivot|| (lo, hi) doubles per row; (MF) the radius range of each of
     // an item's first kBR blocks
     static constexpr int kBR = MF ? 128 : 0;
-    static constexpr int kMeta = 64 + QR * 4 * 3 + 2 * QR * 8 + QR * 16 + kBR * 8 + (XH ? kBR * 4 : 0);
+    static constexpr int kMeta = 64 + QR * 4 * 3 + 2 * QR * 8 + QR * 16 + kBR * 8 + (XH || HH ? kBR * 4 : 0);
     static constexpr int total = kX + kLists + kBufs + kMeta;
 };
 
@@ -880,13 +907,18 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // and 16 dims taking A = (qh, ql) of the 16 dims against B = (xh, xh); the
 // bound widens by 2^-8 |q| R (err_E(split = 2)), so more candidates reach the
 // exact re-check.
+// SPLIT == 3 (LIRA_OPT_XHI = 2, hi x hi): only the hi parts of x AND of the
+// queries, 32 dims per v_mfma_f32_16x16x32_bf16 (lane group g: chunk half g >>
+// 1, dims 8 (g & 1) ..) and per ring slot: half the MFMAs, fragment reads and
+// chunk barriers of SPLIT 2 and half its query bytes, at the bound
+// err_E(split = 3) (+ ||q - qh|| (R + ||x - xh||), the row's qres from k_qstage).
 template <int METRIC, int RL, int QR, int OCC, int SPLIT = 0>
 __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
     constexpr int NW = QR / 16, NT = QR * 4;  // waves of 16 rows each, threads
-    typedef SSmem<QR, RL, true, SPLIT == 2> S;
+    typedef SSmem<QR, RL, true, SPLIT == 2, SPLIT == 3> S;
     constexpr int NSL = S::NSL;  // ring slots: 3 for hi-only x, else 2
     constexpr int K2 = S::K2, BC = S::BC;  // BC: survivor buffer keys per row
-    constexpr int DK = kSDK;               // dims per staged chunk
+    constexpr int DK = SPLIT == 3 ? 2 * kSDK : kSDK;  // dims per staged chunk
     constexpr int ESPLIT = SPLIT;          // the error model's split mode
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float *Xs = (float *)smem;  // [2] x {X: [4 tiles][16 dims][64], Q: [16 dims][64]}
@@ -967,7 +999,8 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
         const int my_pair = __float_as_int(qrec.z);
         const int my_q = my_pair >= 0 ? my_pair / a.nprobe : -1;
         const double my_qn = (double)qrec.x, my_qnorm = (double)qrec.y;
-        const double my_E = err_E<METRIC>(my_qnorm, R, dd, ESPLIT, (double)a.dpad, a.centred);
+        const double my_qres = SPLIT == 3 ? (double)a.QE[(int64_t)gqb * QR + my_row] : 0.0;
+        const double my_E = err_E<METRIC>(my_qnorm, R, dd, ESPLIT, (double)a.dpad, a.centred, -1.0, my_qres);
         u64 *my_list = lists + my_row * K2;
         // this lane's 4 output rows 4g + reg: qn for the screened scores
         float qn_r[4];
@@ -983,15 +1016,20 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
             // X: 16 pieces of 1 KiB per chunk (tile pc >> 2, dims jc + 4(pc & 3)
             // .. +3; split: quarter (pc & 3) = part g); wave w moves pieces w, w + NW, ...
             // (SPLIT 2: the 8 hi pieces, quarters 0 and 1, tile stride 2 KiB)
+            // (SPLIT 3: the 16 hi pieces of two 16-dim chunks, piece (t, chunk half
+            // qq >> 1, quarter qq & 1), tile stride 4 KiB)
             constexpr int NP = SPLIT == 2 ? 8 : 16, QSH = SPLIT == 2 ? 1 : 2;
 #pragma unroll
             for (int m = 0; m < NP / NW; ++m) {
                 const int pc = wave + NW * m, t = pc >> QSH, qq = pc & ((1 << QSH) - 1);
-                LIRA_SGLDS(Xg + (int64_t)(tile0 + tb + min(t, ntv - 1)) * tstride + jc * (kTile / 4) + qq * 64 + lane,
+                const int src = SPLIT == 3 ? (qq >> 1) * (kSDK * kTile / 4) + (qq & 1) * 64 : qq * 64;
+                LIRA_SGLDS(Xg + (int64_t)(tile0 + tb + min(t, ntv - 1)) * tstride + jc * (kTile / 4) + src + lane,
                         __builtin_amdgcn_readfirstlane(base + (uint32_t)(t * S::kXT + qq * 1024)));
             }
-            // Q: QR/16 pieces of 1 KiB, one per wave
-            LIRA_SGLDS(qtg + (int64_t)jc * (QR / 4) + wave * 64 + lane,
+            // Q: QR/16 pieces of 1 KiB, one per wave (SPLIT 3: the hi parts,
+            // chunk half wave >> 1, quarter wave & 1; QR = 64)
+            const int qsrc = SPLIT == 3 ? (wave >> 1) * (kSDK * QR / 4) + (wave & 1) * 64 : wave * 64;
+            LIRA_SGLDS(qtg + (int64_t)jc * (QR / 4) + qsrc + lane,
                     __builtin_amdgcn_readfirstlane(base + (uint32_t)S::kXS + (uint32_t)wave * 1024u));
             if (jc == 0 && wave == 0) {  // the block's xadj rides along (tiles past its end: masked on read)
                 LIRA_SGLDS(a.xadj + (int64_t)(tile0 + tb + min(lane >> 4, ntv - 1)) * kTile + (lane & 15) * 4,
@@ -1088,7 +1126,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
             }
         };
         // (SPLIT 2) the blocks' max ||x - hi(x)||: a tighter hi-only error bound than 2^-8 Rb
-        const bool hres_on = SPLIT == 2 && br_lds && a.tres != nullptr;
+        const bool hres_on = (SPLIT == 2 || SPLIT == 3) && br_lds && a.tres != nullptr;
         if (br_lds) {
             for (int i = tid; i < nblk; i += NT) {
                 float lo, hi;
@@ -1176,7 +1214,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
             if (TRI && SPLIT && a.centred) {
                 Rb = fmin(R, (double)bhi * (1.0 + 0x1p-20));
                 const double hr = hres_on ? (double)bres_s[(tb - tb_begin) / kSBT] : -1.0;
-                Eb = Rb < R || hres_on ? err_E<METRIC>(my_qnorm, Rb, dd, ESPLIT, (double)a.dpad, a.centred, hr)
+                Eb = Rb < R || hres_on ? err_E<METRIC>(my_qnorm, Rb, dd, ESPLIT, (double)a.dpad, a.centred, hr, my_qres)
                                        : my_E;
             }
             const float h_l = refresh(bi & 1);
@@ -1220,7 +1258,26 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                     n_cur = n_nxt;
                     n_nxt = 0;
                 }
-                if (SPLIT == 2 && !wdead && !(a.dbg & 1)) {
+                if (SPLIT == 3 && !wdead && !(a.dbg & 1)) {
+                    const char *sb = (const char *)Xs + slot * S::kStage;
+                    // A: the rows' qh of dims 8g .. 8g + 7 of the slot's 32; B: xh of the same dims
+                    const bf16x8 aq = *(const bf16x8 *)(sb + S::kXS + ((g * QR + wave * 16 + cj) << 4));
+                    bf16x8 bv[16];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            bv[t * 4 + i] = *(const bf16x8 *)(sb + t * S::kXT + ((g * 64 + i * 16 + cj) << 4));
+#pragma unroll
+                    for (int i = 0; i < 16; ++i)
+                        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq, bv[i], acc[i], 0, 0, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 9, 0);  // DS reads
+                    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // MFMAs
+                    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+                } else if (SPLIT == 2 && !wdead && !(a.dbg & 1)) {
                     const char *sb = (const char *)Xs + slot * S::kStage;
                     // all 17 fragment reads first, then the 16 MFMAs (pinned by sched
                     // groups: left to itself hipcc serialises read -> wait -> MFMA)
@@ -1368,9 +1425,10 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                     const float B = ord2f((uint32_t)__shfl((int)key16, 16 * g + j - 1, 64));
                     if (h == -__builtin_inff() && B < __builtin_inff()) {
                         const double qnorm_r = (double)__shfl((float)my_qnorm, 4 * g + reg, 64);
+                        const double qres_r = SPLIT == 3 ? (double)__shfl((float)my_qres, 4 * g + reg, 64) : 0.0;
                         // (bound from this block's keys: its own error bound serves both)
                         const double E_r = err_E<METRIC>(qnorm_r, Rb, dd, ESPLIT, (double)a.dpad, a.centred,
-                                                         hres_on ? (double)bres_s[(tb - tb_begin) / kSBT] : -1.0);
+                                                         hres_on ? (double)bres_s[(tb - tb_begin) / kSBT] : -1.0, qres_r);
                         h = row_h<METRIC>(s_lim<METRIC>(bound_P<METRIC>((double)B, E_r, dd), E_r, dd),
                                           (double)qn_r[reg], qnorm_r, Rb);
                         int pm2 = 0;
@@ -2526,7 +2584,7 @@ struct SPlan {
     int v2 = 0, ns = 2, bc = 32;  // the pipelined split screen (k_screen_s): ring slots, buffer keys per row
     int64_t max_qblk = 0;
     size_t off_cnt, off_cursor, off_head, off_qoff, off_item, off_nch, off_qblk, off_itab, off_qlist, off_qt, off_qn,
-        off_partial, off_qbound, off_pqn, off_pe, total;
+        off_partial, off_qbound, off_pqn, off_pe, off_qe, total;
 };
 
 static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, unsigned flags) {
@@ -2555,9 +2613,16 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // 1.10 latent, 1.25 -> 0.85 mixture -- more exact re-checks, fewer MFMAs)
     // IP: not centred, so the hi-only bound 2^-8 |q| R is wide against the score
     // spread (DEEP10M k = 100: merge 0.3 -> 36 ms); default off there
-    const int xhi = op.xhi >= 0 ? op.xhi : idx->metric == LIRA_METRIC_L2 && idx->pivot != nullptr;
+    // hi x hi (LIRA_OPT_XHI = 2, the L2 default): k_screen_m<..., 3>, 64 queries per
+    // item, RL 1 (its 32-dim slots leave room for K2 = 32 only at 2 workgroups
+    // per CU), else hi-only x.  Measured against hi-only x: SIFT1M scan 1.83 ->
+    // 1.44 ms latent, 0.47 -> 0.41 mixture; GIST1M 1.03 -> 0.77 latent, 0.84 ->
+    // 0.67 mixture (survivors +4 %: the bound's extra ||q - qh|| R is small
+    // against the score spread)
+    const int xhi = op.xhi >= 0 ? op.xhi : idx->metric == LIRA_METRIC_L2 && idx->pivot != nullptr ? 2 : 0;
     if (pl.split && xhi && pl.rl <= (pl.qr == 64 ? 4 : 1) && !(op.pipeline && (pl.rl == 4 || op.ring > 0)))
         pl.split = 2;
+    if (pl.split == 2 && xhi == 2 && pl.qr == 64 && pl.rl == 1) pl.split = 3;
     // the pipelined split screen (LIRA_OPT_PIPELINE): RL 1 at 128 queries per item
     // (8 waves, 4 ring slots, 16-key buffers), RL 2 at 64 (4 slots), RL 4 at 64 (3 slots)
     // (measured, SIFT1M / GIST1M, k = 10: every ring / QR variant of k_screen_s
@@ -2581,6 +2646,7 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
               : !pl.mfma       ? screen_smem(pl.qr, pl.rl)
               : pl.qr == 128 ? (pl.split == 2 ? SSmem<128, 1, true, true>::total
                                 : pl.rl == 1 ? SSmem<128, 1, true>::total : SSmem<128, 2, true>::total)
+              : pl.split == 3 ? SSmem<64, 1, true, false, true>::total
               : pl.split == 2 ? (pl.rl == 1 ? SSmem<64, 1, true, true>::total
                                  : pl.rl == 2 ? SSmem<64, 2, true, true>::total : SSmem<64, 4, true, true>::total)
               : pl.rl == 1   ? SSmem<64, 1, true>::total
@@ -2647,6 +2713,7 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     pl.off_qlist = take((size_t)npairs * 4);
     pl.off_qt = take((size_t)pl.max_qblk * pl.qr * idx->dpad * 4);
     pl.off_qn = take((size_t)pl.max_qblk * pl.qr * 16);
+    pl.off_qe = take((size_t)pl.max_qblk * pl.qr * 4);
     pl.off_partial = take((size_t)npairs * pl.nch_max * pl.K2 * 8);
     pl.off_qbound = take((size_t)nq * 4);
     pl.off_pqn = take((size_t)npairs * 4);
@@ -2671,7 +2738,8 @@ std::string screen_describe(const lira_index *idx, int64_t nq, int64_t nprobe, i
     SPlan pl = make_splan(idx, nq, nprobe, k, flags);
     std::string s = pl.v2 ? "k_screen_s split-bf16 v_mfma_f32_16x16x32_bf16 NS=" + std::to_string(pl.ns) +
                                 " BC=" + std::to_string(pl.bc)
-                    : pl.mfma ? (pl.split == 2 ? "k_screen_m hi-x split-bf16 v_mfma_f32_16x16x32_bf16"
+                    : pl.mfma ? (pl.split == 3 ? "k_screen_m hi-x hi-q bf16 v_mfma_f32_16x16x32_bf16"
+                                 : pl.split == 2 ? "k_screen_m hi-x split-bf16 v_mfma_f32_16x16x32_bf16"
                                  : pl.split ? "k_screen_m split-bf16 v_mfma_f32_16x16x32_bf16"
                                         : "k_screen_m fp32 v_mfma_f32_16x16x4_f32")
                             : "k_screen VALU v_pk_fma_f32";
@@ -2693,9 +2761,10 @@ static hipError_t launch_screen(const ScreenArgs &a, const SPlan &pl, hipStream_
 
 template <int M, int RL, int QR, int SPLIT = 0>
 static hipError_t launch_screen_m(const ScreenArgs &a, const SPlan &pl, hipStream_t st) {
-    constexpr int OCC = (160 * 1024) / SSmem<QR, RL, true, SPLIT == 2>::total >= 2 ? 2 : 1;
+    typedef SSmem<QR, RL, true, SPLIT == 2, SPLIT == 3> S;
+    constexpr int OCC = (160 * 1024) / S::total >= 2 ? 2 : 1;
     static std::atomic<uint64_t> attr{0};
-    constexpr int smem = SSmem<QR, RL, true, SPLIT == 2>::total;  // (+ the kernel's small static LDS)
+    constexpr int smem = S::total;  // (+ the kernel's small static LDS)
     hipError_t e = set_smem_attr_once(attr, (const void *)k_screen_m<M, RL, QR, OCC, SPLIT>, smem);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_screen_m<M, RL, QR, OCC, SPLIT>), dim3(pl.grid), dim3(QR * 4), smem, st, a);
@@ -2729,6 +2798,7 @@ static hipError_t launch_screen_rl(const ScreenArgs &a, const SPlan &pl, hipStre
         if (pl.qr == 128 && pl.split == 2) return launch_screen_m<M, 1, 128, 2>(a, pl, st);
         if (pl.qr == 128 && pl.split)
             return pl.rl == 1 ? launch_screen_m<M, 1, 128, 1>(a, pl, st) : launch_screen_m<M, 2, 128, 1>(a, pl, st);
+        if (pl.split == 3) return launch_screen_m<M, 1, 64, 3>(a, pl, st);
         if (pl.split == 2) switch (pl.rl) {
             case 1: return launch_screen_m<M, 1, 64, 2>(a, pl, st);
             case 2: return launch_screen_m<M, 2, 64, 2>(a, pl, st);
@@ -2797,6 +2867,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     int32_t *qlist = (int32_t *)(w + pl.off_qlist);
     float *QT = (float *)(w + pl.off_qt);
     float4 *QN = (float4 *)(w + pl.off_qn);
+    float *QE = pl.split == 3 ? (float *)(w + pl.off_qe) : nullptr;
     u64 *partial = (u64 *)(w + pl.off_partial);
     uint32_t *qbound = per_part ? nullptr : (uint32_t *)(w + pl.off_qbound);
     const int64_t npairs = nq * nprobe;
@@ -2830,19 +2901,19 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     const dim3 qgrid((unsigned)pl.max_qblk, (unsigned)((idx->dpad + 64 * kQSlabs - 1) / (64 * kQSlabs)));
     if (pl.qr == 128 && pl.split)
         hipLaunchKernelGGL((k_qstage<128, true>), qgrid, dim3(256), 0, st, q, idx->d, idx->dpad,
-                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn);
+                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn, QE);
     else if (pl.qr == 128)
         hipLaunchKernelGGL((k_qstage<128, false>), qgrid, dim3(256), 0, st, q, idx->d, idx->dpad,
-                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn);
+                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn, QE);
     else if (pl.qr == 64 && pl.split)
         hipLaunchKernelGGL((k_qstage<64, true>), qgrid, dim3(256), 0, st, q, idx->d, idx->dpad,
-                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn);
+                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn, QE);
     else if (pl.qr == 64)
         hipLaunchKernelGGL((k_qstage<64, false>), qgrid, dim3(256), 0, st, q, idx->d, idx->dpad,
-                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn);
+                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn, QE);
     else
         hipLaunchKernelGGL((k_qstage<32, false>), qgrid, dim3(256), 0, st, q, idx->d, idx->dpad,
-                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn);
+                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn, QE);
     LIRA_HIP_TRY(hipGetLastError());
     // (measured: SIFT1M mixture 1.70 -> 1.44 ms, latent +1 %)
     // LIRA_OPT_SEED 2 / 3: per nearest-partition query block (k_seed_b, 128 /
@@ -2899,7 +2970,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     a.Q = q;
     a.pivot = tri ? idx->pivot : nullptr;
     a.tstat = tri ? idx->tstat : nullptr;
-    a.tres = tri && centred && pl.split == 2 ? idx->tres : nullptr;
+    a.tres = tri && centred && (pl.split == 2 || pl.split == 3) ? idx->tres : nullptr;
     a.dbg = o.debug;
     a.share = o.share;
     a.split = pl.split;
@@ -2915,6 +2986,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     a.head = head;
     a.QT = QT;
     a.QN = QN;
+    a.QE = QE;
     a.partial = partial;
     // the lists' own error bounds (k_screen_m only; the merge otherwise takes the list-wide one)
     float *pE = pl.mfma && !pl.v2 ? (float *)(w + pl.off_pe) : nullptr;

@@ -80,7 +80,7 @@ def check_vs_oracle(x, q, d2b, probe, b, k, metric, dedup=True):
         assert np.array_equal(bits(D), bits(Do)), f"distances differ (exact={exact}, split={split})"
         assert np.array_equal(nc, nco)
     if k <= 56:
-        for xhi in (0, 1):  # hi + lo / hi-only x screen (wider bound, same results)
+        for xhi in (0, 1, 2):  # hi + lo / hi-only x / hi x hi screens (wider bounds, same results)
             idx.set_option("xhi", xhi)
             D, I, nc = run(idx, q, probe, k, dedup=dedup)
             assert np.array_equal(I, Io), f"ids differ (xhi={xhi})"
@@ -370,7 +370,7 @@ def test_options_do_not_change_results(metric):
     ref = run(idx, q, probe, 10)
     for name, vals in (("qr", (128,)), ("two_phase", (0, 2)), ("seed", (0, 2, 3)), ("share", (0,)),
                        ("prune", (0,)), ("split", (0,)), ("mfma", (0, 2)), ("rounds", (1, 64)),
-                       ("near_rounds", (8,)), ("screen", (0,)), ("ring", (2, 3, 4)), ("probes_hint", (1, 4)), ("xhi", (0, 1))):
+                       ("near_rounds", (8,)), ("screen", (0,)), ("ring", (2, 3, 4)), ("probes_hint", (1, 4)), ("xhi", (0, 1, 2))):
         old = idx.get_option(name)
         for v in vals:
             idx.set_option(name, v)
