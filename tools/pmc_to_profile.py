@@ -60,6 +60,19 @@ def main(cfg, data, src, tag):
         "lds_bank_conflicts": p.get("SQ_LDS_BANK_CONFLICT"),
         "source": f"profiles/{tag}_{cfg}_{data}_pmc_summary.json",
     }
+    # median launch of that kernel in the trace: the average also holds the
+    # bench's one work-counter launch (stats on: per-block atomics, ~7x slower)
+    tr = os.path.join(src, "trace", "run_kernel_trace.csv")
+    if os.path.exists(tr):
+        import csv
+        short = name.split("(")[0]
+        ds = sorted(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(tr))
+                    if r["Kernel_Name"].split("(")[0].replace("void ", "") == short)
+        if ds:
+            rec["median_ns_trace"] = ds[len(ds) // 2]
+            rec["launches_trace"] = len(ds)
+            rec["note_trace"] = ("avg_ns_trace includes the bench's single stats-on launch (work counters, "
+                                 "atomics per block); median_ns_trace is the timed launches' figure")
     out = os.path.join(root, "profiles")
     json.dump(rec, open(os.path.join(out, f"pmc_scan_{cfg}_{data}.json"), "w"), indent=1)
     shutil.copy(os.path.join(src, "summary.json"), os.path.join(out, f"{tag}_{cfg}_{data}_pmc_summary.json"))
