@@ -1073,6 +1073,9 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
         // E_run: the largest Eb of the blocks whose keys the list holds (every
         // key's screened score is within its block's Eb of the truth)
         double Rb = R, Eb = my_E, E_run = 0.0;
+        bool c_ok = false;  // refresh's cache of the T-only terms
+        double T_c = 0.0, A_c = 0.0;
+        float2 ab_c = make_float2(-__builtin_inff(), __builtin_inff());
         auto refresh = [&](int par) {
             const u64 kk = my_list[k - 1];
             double T = kk == kEmptyKey ? __builtin_inf() : bound_P<METRIC>((double)key_score(kk), E_run, dd);
@@ -1089,22 +1092,30 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
             } else if (pub != ~0u) {
                 T = fmin(T, (double)ord2f(pub));
             }
-            const float h = my_pair < 0 ? __builtin_inff()
-                                        : row_h<METRIC>(s_lim<METRIC>(T, Eb, dd), my_qn, my_qnorm, Rb);
-            if (TRI && lane < 16) {
-                float2 ab = make_float2(-__builtin_inff(), __builtin_inff());  // never skip
-                const double F = 1.0 - (dd + 4.0) * kU;
-                if (my_pair < 0) {
-                    ab = make_float2(__builtin_inff(), -__builtin_inff());       // no query: always
-                } else if (T < 1e300 && F > 0.5) {
-                    const double rad = __builtin_sqrt((fmax(T, 0.0) + dd * 0x1p-140) / F) * (1.0 + 0x1p-40);
-                    double A = dq_s[my_row * 2] - rad, B = dq_s[my_row * 2 + 1] + rad;
-                    A -= __builtin_fabs(A) * 0x1p-50;
-                    B += __builtin_fabs(B) * 0x1p-50;
-                    ab = make_float2(__double2float_rd(A), __double2float_ru(B));
+            // the T-only parts (s_lim's division, the skip radius's sqrt) are
+            // recomputed only when the row's bound moved (most blocks it does not)
+            if (!c_ok || T != T_c) {
+                c_ok = true;
+                T_c = T;
+                if (METRIC == LIRA_METRIC_L2) A_c = ((T + dd * 0x1p-140) / (1.0 - (dd + 4.0) * kU)) * (1.0 + 0x1p-50);
+                if (TRI) {
+                    ab_c = make_float2(-__builtin_inff(), __builtin_inff());  // never skip
+                    const double F = 1.0 - (dd + 4.0) * kU;
+                    if (my_pair < 0) {
+                        ab_c = make_float2(__builtin_inff(), -__builtin_inff());  // no query: always
+                    } else if (T < 1e300 && F > 0.5) {
+                        const double rad = __builtin_sqrt((fmax(T, 0.0) + dd * 0x1p-140) / F) * (1.0 + 0x1p-40);
+                        double A = dq_s[my_row * 2] - rad, B = dq_s[my_row * 2 + 1] + rad;
+                        A -= __builtin_fabs(A) * 0x1p-50;
+                        B += __builtin_fabs(B) * 0x1p-50;
+                        ab_c = make_float2(__double2float_rd(A), __double2float_ru(B));
+                    }
                 }
-                tri_s[par * QR + my_row] = ab;
             }
+            // (s_lim<L2>(T, Eb) = A_c + Eb, the same double operations)
+            const double lim = METRIC == LIRA_METRIC_L2 ? A_c + Eb : s_lim<METRIC>(T, Eb, dd);
+            const float h = my_pair < 0 ? __builtin_inff() : row_h<METRIC>(lim, my_qn, my_qnorm, Rb);
+            if (TRI && lane < 16) tri_s[par * QR + my_row] = ab_c;
             __builtin_amdgcn_wave_barrier();
             return h;
         };
