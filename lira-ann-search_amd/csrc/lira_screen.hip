@@ -320,10 +320,10 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
 #pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) {
-                s[m] += __shfl_xor(s[m], o, 64);
-                t[m] += __shfl_xor(t[m], o, 64);
-                if (SPLIT && QE) e[m] += __shfl_xor(e[m], o, 64);
+            for (int o = 32; o >= 1; o >>= 1) {  // (DPP / swizzle exchanges, lira_device.hpp)
+                s[m] += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, s[m]), o));
+                if (pivot) t[m] += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, t[m]), o));
+                if (SPLIT && QE) e[m] += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, e[m]), o));
             }
         }
         if (lane < NM) {  // lane m writes row r0 + m * rstep
@@ -1474,16 +1474,27 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                             const int r = wave * 16 + 4 * gg + reg;
                             s_flush<RL>(lists + r * K2, bufs + r * BC, r0 == 0 ? __builtin_amdgcn_readlane(bc0, 16 * gg) : BC);
                         }
-                        int rank = base;
+                        // each lane walks its own passing candidates (usually 0 or 1):
+                        // a 16-way select picks the accumulator, so only those are
+                        // scored (scoring all 16 unconditionally was ~150 VALU per pass)
+                        int rank = base, pmv = pm;
+                        while (pmv) {
+                            const int v = __builtin_ctz(pmv);
+                            pmv &= pmv - 1;
+                            if (rank >= r0 && rank < r0 + BC) {
+                                float dv = acc[0][reg], av = xa[0][0];
 #pragma unroll
-                        for (int v = 0; v < 16; ++v) {
-                            if ((pm >> v) & 1) {
-                                if (rank >= r0 && rank < r0 + BC)
-                                    bufs[row * BC + rank - r0] =
-                                        ((u64)f2ord(score(v)) << 32) |
-                                        (uint32_t)((tile0 + tb + (v >> 2)) * kTile + 4 * cj + (v & 3));
-                                ++rank;
+                                for (int i = 1; i < 16; ++i)
+                                    if (v == i) {
+                                        dv = acc[i][reg];
+                                        av = xa[i >> 2][i & 3];
+                                    }
+                                const float sc = METRIC == LIRA_METRIC_L2
+                                                     ? __builtin_fmaf(-2.0f, dv, qn_r[reg] + 2.0f * av) : -dv;
+                                bufs[row * BC + rank - r0] =
+                                    ((u64)f2ord(sc) << 32) | (uint32_t)((tile0 + tb + (v >> 2)) * kTile + 4 * cj + (v & 3));
                             }
+                            ++rank;
                         }
                         __builtin_amdgcn_wave_barrier();
                         if (!__any(total - r0 > BC)) break;
@@ -2411,7 +2422,7 @@ __global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
         qs = __builtin_fma(x, x, qs);
     }
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) qs += __shfl_xor(qs, m, 64);
+    for (int m = 32; m >= 1; m >>= 1) qs += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, qs), m));
     // rounded up by more than any summation-order difference to k_qstage's value
     const double qnorm = __builtin_sqrt(qs) * (1.0 + 0x1p-30);
     const int32_t *prow = a.probe + q * a.nprobe;
