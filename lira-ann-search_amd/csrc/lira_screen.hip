@@ -1179,6 +1179,8 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
             return t;
         };
 
+        // buffer fill of row 4 g + reg (this lane's group g), group-uniform
+        int bcr[4] = {0, 0, 0, 0};
         int slot = 0;
         int tb = tb_begin;
         if (TRI) {
@@ -1399,9 +1401,12 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                 const float mx = fmaxf(fmaxf(fmaxf(m01, m02), m03), fmaxf(fmaxf(m04, m05), wv[15]));
                 if (!__any(mx >= h)) continue;  // wave-uniform: none of the four rows has a candidate
                 if (clk) ++n_slow;
-                int pm = 0;  // passing candidates (padding, xadj = +inf, never)
+                // passing candidates; padding (xadj = +inf: wv = -inf) never, as
+                // h is clamped to the lowest finite value (one compare per candidate)
+                const float hp = fmaxf(h, -3.40282347e38f);
+                int pm = 0;
 #pragma unroll
-                for (int i = 0; i < 16; ++i) pm |= (wv[i] >= h && xa[i >> 2][i & 3] != __builtin_inff()) << i;
+                for (int i = 0; i < 16; ++i) pm |= (wv[i] >= hp) << i;
                 // screened score of candidate i (L2: qn + 2 xadj - 2 dot; IP: -dot)
                 auto score = [&](int i) {
                     const float av = xa[i >> 2][i & 3], dv = acc[i][reg];
@@ -1457,7 +1462,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                 // merge site, so the reg loop still unrolls (acc[v][reg] static).
                 {
                     const int row = wave * 16 + 4 * g + reg;
-                    const int bc0 = m_bufc[row];
+                    const int bc0 = bcr[reg];  // (group-uniform)
                     const int n_l = __builtin_popcount(pm);
                     const int inc = row16_incl_scan(n_l);  // inclusive prefix over the group's 16 lanes
                     const int rowtot = row16_total(inc);
@@ -1499,10 +1504,8 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
                         __builtin_amdgcn_wave_barrier();
                         if (!__any(total - r0 > BC)) break;
                     }
-                    if (cj == 0) {
-                        m_bufc[row] = total <= BC ? total : total - BC * ((total - 1) / BC);
-                        if (cnt && rowtot) atomicAdd(cnt + 7, (unsigned long long)rowtot);
-                    }
+                    bcr[reg] = total <= BC ? total : total - BC * ((total - 1) / BC);
+                    if (cj == 0 && cnt && rowtot) atomicAdd(cnt + 7, (unsigned long long)rowtot);
                     __builtin_amdgcn_wave_barrier();
                 }
             }
@@ -1510,6 +1513,11 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
         }
 
         if (clk) t_2 = clock64();
+        if (cj == 0) {  // the rows' buffer fills, from registers to LDS
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) m_bufc[wave * 16 + 4 * g + reg] = bcr[reg];
+        }
+        __builtin_amdgcn_wave_barrier();
         // ---- flush buffers, emit lists, publish bounds (wave-owned rows);
         // buffers flushed two rows per network pass (one row per half-wave:
         // the per-item epilogue was ~8 % of the screen's cycles on SIFT1M latent)
