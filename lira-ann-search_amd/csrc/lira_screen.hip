@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256) void k_qstage(const float *Q, int64_t d, int64
                 for (int u = threadIdx.x; u < 16 * RT; u += 256) {
                     const int row = u % RT, cg = u / RT, cc = cg >> 2, gg = cg & 3;
                     const int64_t c0 = j0 + 16 * cc;
-                    if (c0 >= dpad) continue;
+                    if (c0 >= dpad || (QE && gg >= 2)) continue;  // (hi x hi: lo parts unused)
                     uint32_t wd[4];
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
@@ -2277,19 +2277,29 @@ __global__ __launch_bounds__(256) void k_seed_t(const float *Q, const int32_t *p
         const float qv = j0 + lane < d ? qrow[j0 + lane] : 0.0f;
         const int nj = (int)min<int64_t>(64, d - j0);
         if (nj == 64) {
+            // two tiles per packed fp32 op (v_pk_add_f32 / v_pk_mul_f32 round
+            // each half like the scalar ops: the same per-lane sums)
+            f2 acc2[NT / 2];
+#pragma unroll
+            for (int t = 0; t < NT / 2; ++t) acc2[t] = (f2){acc[2 * t], acc[2 * t + 1]};
 #pragma unroll 16
             for (int jj = 0; jj < 64; ++jj) {
-                const float qj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qv), jj));
+                const f2 qj = (f2)(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(qv), jj)));
 #pragma unroll
-                for (int t = 0; t < NT; ++t) {
-                    const float xv = xt[t][(j0 + jj) * kTile];
+                for (int t = 0; t < NT / 2; ++t) {
+                    const f2 xv = {xt[2 * t][(j0 + jj) * kTile], xt[2 * t + 1][(j0 + jj) * kTile]};
                     if (METRIC == LIRA_METRIC_L2) {
-                        const float df = qj - xv;
-                        acc[t] = acc[t] + df * df;
+                        const f2 df = qj - xv;
+                        acc2[t] = acc2[t] + df * df;
                     } else {
-                        acc[t] = acc[t] + qj * xv;
+                        acc2[t] = acc2[t] + qj * xv;
                     }
                 }
+            }
+#pragma unroll
+            for (int t = 0; t < NT / 2; ++t) {
+                acc[2 * t] = acc2[t].x;
+                acc[2 * t + 1] = acc2[t].y;
             }
         } else {
             for (int jj = 0; jj < nj; ++jj) {
