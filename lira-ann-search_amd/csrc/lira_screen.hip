@@ -2526,13 +2526,22 @@ __global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
                 over = last != kEmptyKey && (double)key_score(last) <= lim;
             }
             bool active = p >= 0 && !over;
-            for (int e = 0; __any(active); ++e) {
-                u64 key = kEmptyKey;
-                if (active) {
-                    key = e < K2 ? src[e] : kEmptyKey;
-                    active = key != kEmptyKey && (double)key_score(key) <= lim;
+            // four keys per round (two 16-B loads; K2 % 4 == 0, lists 32-B aligned):
+            // the walk is one dependent load per round
+            for (int e0 = 0; __any(active); e0 += 4) {
+                u64 kv[4] = {kEmptyKey, kEmptyKey, kEmptyKey, kEmptyKey};
+                if (active && e0 < K2) {
+                    const ulonglong2 a0 = *(const ulonglong2 *)(src + e0), a1 = *(const ulonglong2 *)(src + e0 + 2);
+                    kv[0] = a0.x;
+                    kv[1] = a0.y;
+                    kv[2] = a1.x;
+                    kv[3] = a1.y;
                 }
-                add(active, (uint32_t)key);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (active) active = kv[u] != kEmptyKey && (double)key_score(kv[u]) <= lim;
+                    add(active, (uint32_t)kv[u]);
+                }
             }
             u64 ov = __ballot(over);
             while (ov) {
