@@ -133,7 +133,7 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *   LIRA_OPT_SCREEN      1: screened scan where supported (default); 0: always
  *                        the all-exact kernel
  *   LIRA_OPT_SPLIT       1: split-bf16 MFMA screen (default); 0: fp32 MFMA screen
- *   LIRA_OPT_QR          queries per screen work item: 0 auto (default), 64, 128
+ *   LIRA_OPT_QR          queries per screen work item: 0 auto (default), 64, 128; 32 (k > 56)
  *   LIRA_OPT_TWO_PHASE   nearest-probe group first: 1 auto (default), 0 off, 2 always
  *   LIRA_OPT_PRUNE       L2 triangle-inequality block skip / exact early abandon (1)
  *   LIRA_OPT_SEED        exact starting bound per query before the screen: 1 (default) per

@@ -708,7 +708,7 @@ int lira_index_set_option(lira_index *idx, int option, int64_t value) {
         case LIRA_OPT_KEEP_TILES: if (!in(0, 1)) break; o.keep_tiles = v; return LIRA_OK;
         case LIRA_OPT_SCREEN: if (!in(0, 1)) break; o.screen = v; return LIRA_OK;
         case LIRA_OPT_SPLIT: if (!in(0, 1)) break; o.split = v; return LIRA_OK;
-        case LIRA_OPT_QR: if (value != 0 && value != 64 && value != 128) break; o.qr = v; return LIRA_OK;
+        case LIRA_OPT_QR: if (value != 0 && value != 32 && value != 64 && value != 128) break; o.qr = v; return LIRA_OK;
         case LIRA_OPT_TWO_PHASE: if (!in(0, 2)) break; o.two_phase = v; return LIRA_OK;
         case LIRA_OPT_PRUNE: if (!in(0, 1)) break; o.prune = v; return LIRA_OK;
         case LIRA_OPT_SEED: if (!in(0, 3)) break; o.seed = v; return LIRA_OK;

@@ -1165,7 +1165,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
         // every wave tests all QR rows, QR/64 per lane, against the same LDS values)
         auto skip_from = [&](int t, int par) {
             if (TRI) {
-                const float2 ab = tri_s[par * QR + lane];
+                const float2 ab = lane < QR ? tri_s[par * QR + lane] : make_float2(__builtin_inff(), -__builtin_inff());
                 const float2 ab2 = QR > 64 ? tri_s[par * QR + (QR > 64 ? 64 : 0) + lane]
                                            : make_float2(__builtin_inff(), -__builtin_inff());
                 while (t < tb_end) {
@@ -2653,9 +2653,16 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // (SIFT1M 1.10 -> 1.25 ms mixture, 4.45 -> 4.66 ms latent; GIST, BIGANN too)
     const int qr_opt = op.qr == 128 ? 128 : 64;
     pl.qr = pl.mfma ? (pl.rl <= 2 ? qr_opt : 64) : screen_qr(pl.rl);
+    // 32 queries per item at RL 4 (LIRA_OPT_QR = 32; the full split screen):
+    // 2-wave workgroups whose 78 KB of LDS fit two per CU (64 queries: one).
+    // Measured DEEP10M: scan 22.4 -> 44.6 ms (twice the staged bytes per
+    // query; the occupancy did not pay for it), so opt-in only
+    const bool qr32 = pl.mfma && pl.rl == 4 && op.qr == 32;
+    if (qr32) pl.qr = 32;
     // split-bf16 MFMA screen (k_screen_m<..., SPLIT>) where the index holds Xb;
     // LIRA_OPT_SPLIT = 0 keeps the fp32 MFMA screen (which reads the fp32 tiles)
     pl.split = split_wanted && pl.mfma && idx->Xb != nullptr;
+    if (qr32 && !pl.split) pl.qr = 64;  // (built for the split copy only)
     // hi-only x (LIRA_OPT_XHI): k_screen_m at 64 queries per item
     // (default: with its 3-slot ring and pipelined fragment reads, measured
     // SIFT1M scan 2.21 -> 1.93 ms latent, 0.56 -> 0.51 mixture; GIST1M 1.49 ->
@@ -2669,7 +2676,7 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // 0.67 mixture (survivors +4 %: the bound's extra ||q - qh|| R is small
     // against the score spread)
     const int xhi = op.xhi >= 0 ? op.xhi : idx->metric == LIRA_METRIC_L2 && idx->pivot != nullptr ? 2 : 0;
-    if (pl.split && xhi && pl.rl <= (pl.qr == 64 ? 4 : 1) && !(op.pipeline && (pl.rl == 4 || op.ring > 0)))
+    if (pl.split && xhi && pl.qr != 32 && pl.rl <= (pl.qr == 64 ? 4 : 1) && !(op.pipeline && (pl.rl == 4 || op.ring > 0)))
         pl.split = 2;
     if (pl.split == 2 && xhi == 2 && pl.qr == 64 && pl.rl == 1) pl.split = 3;
     // the pipelined split screen (LIRA_OPT_PIPELINE): RL 1 at 128 queries per item
@@ -2679,7 +2686,7 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // workgroup per CU; DEEP10M k = 100: 28.1 ms, k_screen_m 24.1 ms since its
     // fragment reads are pipelined), so only where LIRA_OPT_PIPELINE = 1 (RL 4)
     // or LIRA_OPT_RING asks for it
-    pl.v2 = pl.split && op.pipeline && (pl.rl == 4 || op.ring > 0);
+    pl.v2 = pl.split && pl.qr != 32 && op.pipeline && (pl.rl == 4 || op.ring > 0);
     if (pl.v2) {
         pl.qr = pl.rl == 1 && op.qr != 64 ? 128 : 64;
         pl.ns = pl.rl == 4 ? 3 : 4;
@@ -2696,6 +2703,7 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
               : pl.qr == 128 ? (pl.split == 2 ? SSmem<128, 1, true, true>::total
                                 : pl.rl == 1 ? SSmem<128, 1, true>::total : SSmem<128, 2, true>::total)
               : pl.split == 3 ? SSmem<64, 1, true, false, true>::total
+              : pl.qr == 32  ? SSmem<32, 4, true>::total
               : pl.split == 2 ? (pl.rl == 1 ? SSmem<64, 1, true, true>::total
                                  : pl.rl == 2 ? SSmem<64, 2, true, true>::total : SSmem<64, 4, true, true>::total)
               : pl.rl == 1   ? SSmem<64, 1, true>::total
@@ -2848,6 +2856,7 @@ static hipError_t launch_screen_rl(const ScreenArgs &a, const SPlan &pl, hipStre
         if (pl.qr == 128 && pl.split)
             return pl.rl == 1 ? launch_screen_m<M, 1, 128, 1>(a, pl, st) : launch_screen_m<M, 2, 128, 1>(a, pl, st);
         if (pl.split == 3) return launch_screen_m<M, 1, 64, 3>(a, pl, st);
+        if (pl.qr == 32) return launch_screen_m<M, 4, 32, 1>(a, pl, st);
         if (pl.split == 2) switch (pl.rl) {
             case 1: return launch_screen_m<M, 1, 64, 2>(a, pl, st);
             case 2: return launch_screen_m<M, 2, 64, 2>(a, pl, st);
@@ -2953,6 +2962,9 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
                            (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn, QE);
     else if (pl.qr == 128)
         hipLaunchKernelGGL((k_qstage<128, false>), qgrid, dim3(256), 0, st, q, idx->d, idx->dpad,
+                           (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn, QE);
+    else if (pl.qr == 32 && pl.split)
+        hipLaunchKernelGGL((k_qstage<32, true>), qgrid, dim3(256), 0, st, q, idx->d, idx->dpad,
                            (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn, QE);
     else if (pl.qr == 64 && pl.split)
         hipLaunchKernelGGL((k_qstage<64, true>), qgrid, dim3(256), 0, st, q, idx->d, idx->dpad,

@@ -387,6 +387,10 @@ def test_options_do_not_change_results(metric):
         D2, I2, _ = run(idx, q, probe, k)
         idx.set_option("pipeline", 0)
         assert np.array_equal(I2, I1) and np.array_equal(bits(D2), bits(D1)), ("pipeline", k)
+        idx.set_option("qr", 32)  # 32 queries per item at RL 4 (k > 56, full split)
+        D3, I3, _ = run(idx, q, probe, k)
+        idx.set_option("qr", 0)
+        assert np.array_equal(I3, I1) and np.array_equal(bits(D3), bits(D1)), ("qr32", k)
     # the pipelined screen's ring variants at both query-block sizes
     for qr, ring in ((64, 2), (64, 4), (128, 3), (128, 4)):
         idx.set_option("qr", qr)
