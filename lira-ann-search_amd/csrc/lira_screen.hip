@@ -2426,7 +2426,7 @@ __device__ __forceinline__ void merge_batch_if(u64 (&lst)[R], u64 batch) {
 }
 
 template <int METRIC, int R>
-__global__ __launch_bounds__(256) void k_smerge(SMergeArgs a) {
+__global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 VGPRs: 4 waves per SIMD)
     __shared__ uint32_t s_pend[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t q = (int64_t)blockIdx.x * 4 + w;
