@@ -7,10 +7,13 @@
 // terms: fl(fl(q-x)^2) for L2 (3 VALU ops per candidate-dim, no FMA allowed)
 // and fl(q*x) for IP (2 ops).  Computing that for every candidate makes the
 // scan VALU-bound at 3 ops/dim.  Here every candidate is first *screened* with
-// an fp32 fused-multiply-add dot product (1 op/dim on v_pk_fma_f32), and only
-// the few candidates that can still reach the top-k are re-computed in the
-// reference's arithmetic.  Nothing is approximated: the screen is a rigorous
-// filter, so the output is bit-identical.
+// a dot product on the matrix cores -- by default bf16 parts of the (L2:
+// pivot-centred) vectors on v_mfma_f32_16x16x32_bf16 (k_screen_m, SPLIT 1-3;
+// the fp32 forms: v_mfma_f32_16x16x4_f32, or v_pk_fma_f32 in k_screen) -- and
+// only the few candidates that can still reach the top-k are re-computed in the
+// reference's arithmetic (k_smerge).  Nothing is approximated: the screen is a
+// rigorous filter, so the output is bit-identical.  The error model below is
+// the fp32 screen's; err_E carries the split forms' terms.
 //
 // Error model (u = 2^-24, per (query, partition); double on the host side of
 // each bound, fp32 values rounded in the safe direction):
@@ -1578,7 +1581,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
     }
 }
 
-// ---- the pipelined split-bf16 screen (default) -------------------------------
+// ---- the pipelined split-bf16 screen (LIRA_OPT_PIPELINE; measured slower) ----
 // k_screen_s: k_screen_m<..., SPLIT>'s work (same items, error model, row
 // lists and outputs) around an NS-slot LDS-DMA ring:
 //  * a wave waits only for its OWN DMA of the chunk it consumes, by a counted
