@@ -484,7 +484,7 @@ def time_pipeline(args, oracle, index, x, centres, q, make_queries, k, nprobe, m
         centroid_dist(pipe.q, pipe.C, pipe.mean, pipe.scale, out=pipe.dist)
         ev[1].record()
         with torch.no_grad():
-            pipe.scores = pipe.model(pipe.dist, pipe.q)
+            pipe.scores.copy_(pipe.model(pipe.dist, pipe.q))
         ev[2].record()
         from lira_amd import _lib
         _lib.call("lira_select_probes", _lib.ptr(pipe.scores), nq, B, pipe.mode, 0.5,

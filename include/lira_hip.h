@@ -157,6 +157,10 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *                        each list's rows by ascending distance to the list's pivot, so tile radius
  *                        ranges are narrow and the triangle-inequality skip drops more; 0: list order.
  *                        Results never depend on it.
+ *   LIRA_OPT_WIDE        1 (default): the wide screen k_screen_w (256 query rows per item, one
+ *                        512-thread workgroup per CU, v_mfma_f32_32x32x16_bf16) where it applies
+ *                        (L2 with the centred split copy, k <= 24, dpad 64 / 96 / 128, a seeded
+ *                        bound); 0: k_screen_m
  */
 #define LIRA_OPT_KEEP_TILES 1
 #define LIRA_OPT_SCREEN 2
@@ -175,6 +179,7 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
 #define LIRA_OPT_PROBES_HINT 15
 #define LIRA_OPT_XHI 16
 #define LIRA_OPT_ORDER 17
+#define LIRA_OPT_WIDE 18
 int lira_index_set_option(lira_index *idx, int option, int64_t value);
 int lira_index_get_option(const lira_index *idx, int option, int64_t *value);
 /* 1 if the index holds the fp32 tile copy (LIRA_OPT_KEEP_TILES at build time) */

@@ -174,6 +174,24 @@ __global__ __launch_bounds__(256) void k_tile_stats(const float *Xr, const int32
     if (lane == 0) tstat[t] = make_float2(lo, hi);
 }
 
+// Per list: the (min, max) of its tiles' radius ranges (+inf, -inf for an
+// empty list) -- one wave per list.
+__global__ __launch_bounds__(64) void k_list_stats(const float2 *tstat, const int32_t *tile_off, float2 *lstat) {
+    const int b = blockIdx.x, lane = threadIdx.x;
+    float lo = __builtin_inff(), hi = -__builtin_inff();
+    for (int t = tile_off[b] + lane; t < tile_off[b + 1]; t += 64) {
+        const float2 v = tstat[t];
+        lo = fminf(lo, v.x);
+        hi = fmaxf(hi, v.y);
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        lo = fminf(lo, __shfl_xor(lo, m, 64));
+        hi = fmaxf(hi, __shfl_xor(hi, m, 64));
+    }
+    if (lane == 0) lstat[b] = make_float2(lo, hi);
+}
+
 // Screening constants of every storage row (lane = row of a tile): xadj and
 // the list's rmax (atomicMax on the bits of a non-negative float).  Norms in
 // double; sqrt rounded up with a 2^-40 relative margin.
@@ -321,8 +339,10 @@ static void free_storage(lira_index *idx) {
     idx->rmaxc = nullptr;
     if (idx->pivot) hipFree(idx->pivot);
     if (idx->tstat) hipFree(idx->tstat);
+    if (idx->lstat) hipFree(idx->lstat);
     idx->pivot = nullptr;
     idx->tstat = nullptr;
+    idx->lstat = nullptr;
     idx->X = nullptr;
     idx->ids = nullptr;
     idx->tile_off = nullptr;
@@ -496,6 +516,7 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
         if (l2) {  // pivot (mean of a list's rows, double) and tile radius arrays
             if (hipMalloc(&idx->pivot, (size_t)n_lists * d * 4) != hipSuccess ||
                 hipMalloc(&idx->tstat, (size_t)tiles * sizeof(float2)) != hipSuccess ||
+                hipMalloc(&idx->lstat, (size_t)n_lists * sizeof(float2)) != hipSuccess ||
                 hipMalloc(&d_seg, (size_t)std::max<int64_t>(segs, 1) * 4) != hipSuccess ||
                 hipMalloc(&d_segf, (size_t)(n_lists + 1) * 4) != hipSuccess ||
                 hipMalloc(&d_psum, (size_t)std::max<int64_t>(segs, 1) * d * 8) != hipSuccess) {
@@ -583,6 +604,8 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
                                        d_loff, d_psum, idx->pivot);
                 hipLaunchKernelGGL(k_tile_stats, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, idx->Xr,
                                    idx->ids, d, d_tlist, idx->pivot, tiles, idx->tstat);
+                hipLaunchKernelGGL(k_list_stats, dim3((unsigned)n_lists), dim3(64), 0, st, idx->tstat, idx->tile_off,
+                                   idx->lstat);
                 e = hipGetLastError();
             }
         }
@@ -694,7 +717,7 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes) {
              (idx->X ? rows * idx->dpad * 4 : 0) +                             // fp32 tiles (optional)
              (idx->xadj ? rows * 4 + idx->n_lists * 4 : 0) +                   // xadj, rmax
              (idx->xadjc ? rows * 4 + idx->n_lists * 4 : 0) +                  // centred xadj, rmax
-             (idx->pivot ? idx->n_lists * idx->d * 4 + idx->n_tiles * 8 : 0) +  // pivots, tile radii
+             (idx->pivot ? idx->n_lists * idx->d * 4 + idx->n_tiles * 8 + idx->n_lists * 8 : 0) +  // pivots, radii
              (idx->tres ? idx->n_tiles * 4 : 0);                                // tile hi residuals
     return LIRA_OK;
 }
@@ -722,6 +745,7 @@ int lira_index_set_option(lira_index *idx, int option, int64_t value) {
         case LIRA_OPT_PROBES_HINT: if (!in(0, 1 << 20)) break; o.probes_hint = v; return LIRA_OK;
         case LIRA_OPT_XHI: if (!in(-1, 2)) break; o.xhi = v; return LIRA_OK;
         case LIRA_OPT_ORDER: if (!in(0, 1)) break; o.order = v; return LIRA_OK;
+        case LIRA_OPT_WIDE: if (!in(0, 1)) break; o.wide = v; return LIRA_OK;
         default: return fail(LIRA_EINVAL, "unknown option " + std::to_string(option));
     }
     return fail(LIRA_EINVAL, "value " + std::to_string(value) + " out of range for option " + std::to_string(option));
@@ -748,6 +772,7 @@ int lira_index_get_option(const lira_index *idx, int option, int64_t *value) {
         case LIRA_OPT_PROBES_HINT: *value = o.probes_hint; break;
         case LIRA_OPT_XHI: *value = o.xhi; break;
         case LIRA_OPT_ORDER: *value = o.order; break;
+        case LIRA_OPT_WIDE: *value = o.wide; break;
         default: return fail(LIRA_EINVAL, "unknown option " + std::to_string(option));
     }
     return LIRA_OK;

@@ -1,0 +1,101 @@
+// lira_bounds.hpp -- the screen's rigorous error model (double precision),
+// shared by the screening kernels (lira_screen.hip, lira_wscreen.hip).  The
+// derivation is in lira_screen.hip's header and DESIGN.md section 4.3.
+#pragma once
+#include "lira_device.hpp"
+
+namespace lira {
+
+static constexpr double kU = 0x1p-24;
+
+// ---- error model (double) -------------------------------------------------
+// split != 0: the dot product came from the split-bf16 MFMA screen
+// (k_screen_m<..., SPLIT>): q = qh + ql + eq, x = xh + xl + ex with every part a
+// bf16 round-to-nearest (|eq| <= 2^-16 |q_i|, |ex| <= 2^-16 |x_i|), the four
+// exact products qh xh, qh xl, ql xh, ql xl summed in fp32 in an unspecified
+// order (4 dpad terms, <= 2^-22 relative per add: any rounding mode the
+// matrix core may use), so |dot~ - q.x| <= ed = (2.0001 2^-16 + 4 dpad 2^-22)
+// 1.02 |q| R + an absolute term for flushed subnormal parts (values below
+// 2^-100 lose at most 2^-100 (|q| + R) per product).  The rest of the L2
+// score's error (qn, xn, their sum, the final fma) stays <= 8.4 u (|q|+R)^2.
+//
+// centred (L2, split screen): q' = fl(q - c), x' = fl(x - c) for the list's
+// pivot c, and qnorm, R the norms of q', x'.  Then (q' - x') - (q - x) =
+// (q - c) e1 - (x - c) e2 with |e| <= u per component, so ||q'-x'||^2 differs
+// from D = ||q-x||^2 by at most u s (2 + u) s (1 + u) <= 2.01 u s^2, s = qnorm
+// + R, on top of the screen's own error for q', x'.
+//
+// split == 3 (hi x hi, k_screen_m<..., 3>): dot~ = sum qh xh, one product per
+// dim (exact in fp32), so q.x - dot~ = q.(x - xh) + (q - qh).xh and
+// |dot~ - q.x| <= |q| ||ex|| + qres (R + ||ex||) + (2 dpad 2^-22) 1.02 |q| (R +
+// ||ex||) + the subnormal term, qres >= ||q - qh|| of the row (k_qstage, QE).
+template <int METRIC>
+__device__ __forceinline__ double err_E(double qnorm, double R, double d, int split = 0, double dp = 0.0,
+                                        int centred = 0, double hres = -1.0, double qres = 0.0) {
+    const double dl = d * 0x1p-140;
+    if (split == 3) {
+        const double ex = hres >= 0.0 ? hres * 1.0001 : 0x1p-8 * 1.02 * R;
+        const double ed = ex * qnorm + qres * (R + ex) * 1.0001 + 2.0 * dp * 0x1p-22 * 1.02 * qnorm * (R + ex) +
+                          2.0 * dp * 0x1p-96 * (qnorm + R + ex + 1.0);
+        if (METRIC == LIRA_METRIC_L2) {
+            const double s = qnorm + R;
+            return 2.0 * ed + (1.05 * 8.0 + (centred ? 2.01 : 0.0)) * kU * s * s + dl;
+        }
+        return 1.05 * (ed + (d + 2.0) * kU * qnorm * R) + dl;
+    }
+    if (split) {
+        // split == 2 (hi-only x, k_screen_m<..., 2>): dot~ = sum (qh + ql) xh, x = xh + ex:
+        // |dot~ - q.x| <= |q.ex| + |(q - qh - ql).xh| + rounding <= |q| ||ex|| +
+        // (2^-16 + 2 dpad 2^-22) 1.02 |q| R, with ||ex|| <= 2^-8 R (|ex_i| <= 2^-8 |x_i|)
+        // or, tighter, hres >= ||ex|| of every candidate concerned (k_tile_hires)
+        const double ex = hres >= 0.0 ? hres * 1.0001 : 0x1p-8 * 1.02 * R;
+        const double ed = split == 2 ? ex * qnorm + (1.0001 * 0x1p-16 + 2.0 * dp * 0x1p-22) * 1.02 * qnorm * R +
+                                           2.0 * dp * 0x1p-96 * (qnorm + R + 1.0)
+                                     : (2.0001 * 0x1p-16 + 4.0 * dp * 0x1p-22) * 1.02 * qnorm * R +
+                                           4.0 * dp * 0x1p-96 * (qnorm + R + 1.0);
+        if (METRIC == LIRA_METRIC_L2) {
+            const double s = qnorm + R;
+            return 2.0 * ed + (1.05 * 8.0 + (centred ? 2.01 : 0.0)) * kU * s * s + dl;
+        }
+        // IP: bound_P / s_lim carry no (1 +- g) factor, so E also covers
+        // search.cpp's own rounding of the exact sum, (d+2) u |q| R (L2 needs
+        // no such term: that error is the g of bound_P / s_lim)
+        return 1.05 * (ed + (d + 2.0) * kU * qnorm * R) + dl;
+    }
+    if (METRIC == LIRA_METRIC_L2) {
+        const double s = qnorm + R;
+        return 1.05 * ((d + 8.0) * kU * s * s) + dl;
+    }
+    return 1.05 * (2.0 * (d + 2.0) * kU * qnorm * R) + dl;
+}
+// bound on the final k-th exact score from a list's k-th screened score
+template <int METRIC>
+__device__ __forceinline__ double bound_P(double sk, double E, double d) {
+    if (METRIC == LIRA_METRIC_L2) return (sk + E) * (1.0 + (d + 4.0) * kU) * (1.0 + 0x1p-50) + d * 0x1p-140;
+    return (sk + E) + __builtin_fabs(sk + E) * 0x1p-50;
+}
+// largest screened score a candidate may have and still score <= T exactly
+template <int METRIC>
+__device__ __forceinline__ double s_lim(double T, double E, double d) {
+    if (METRIC == LIRA_METRIC_L2) return ((T + d * 0x1p-140) / (1.0 - (d + 4.0) * kU)) * (1.0 + 0x1p-50) + E;
+    return T + E + __builtin_fabs(T + E) * 0x1p-50;
+}
+// per-block test threshold on the dot product: pass iff fl(dot - xadj) >= h.
+// L2: s~ <= lim  <=>  dot - xn/2 >= (qn - lim)/2; fl(dot - xadj) is off by at
+// most u (|q| + R)^2.  IP: xadj = 0, -s~ = dot >= -lim.
+template <int METRIC>
+__device__ __forceinline__ float row_h(double lim, double qn, double qnorm, double R) {
+    if (!(lim < 1e300)) return -__builtin_inff();
+    double h;
+    if (METRIC == LIRA_METRIC_L2) {
+        const double s = qnorm + R;
+        h = (qn - lim) * 0.5 - 1.05 * kU * s * s;
+    } else {
+        h = -lim;
+    }
+    h -= __builtin_fabs(h) * 0x1p-50;
+    return __double2float_rd(h);
+}
+
+
+}  // namespace lira

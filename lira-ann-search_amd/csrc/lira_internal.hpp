@@ -50,6 +50,7 @@ struct lira_opts {
     int probes_hint = 0;
     int xhi = -1;
     int order = 1;
+    int wide = 1;
 };
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device):
@@ -73,6 +74,8 @@ struct lira_index_impl {
     // (lo, hi) with lo <= ||x - pivot|| <= hi for every real row of the tile.
     float *pivot = nullptr;
     float2 *tstat = nullptr;
+    // per list: (min, max) of its tiles' radius ranges (the scan's pair filter)
+    float2 *lstat = nullptr;
     // For the screened scan (lira_screen.hip): per storage row xadj = ||x||^2 / 2
     // (L2, the fp32 rounding of the double sum, halved) or 0 (IP), +inf for
     // padding rows; per list rmax >= max ||x|| over its rows (rounded up).

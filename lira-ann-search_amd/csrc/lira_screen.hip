@@ -47,10 +47,22 @@
 #include <cstdlib>
 #include <string>
 
+#include "lira_bounds.hpp"
 #include "lira_device.hpp"
 #include "lira_internal.hpp"
 
 namespace lira {
+
+// lira_wscreen.hip
+bool wscreen_shape_ok(int64_t dpad);
+int wscreen_smem();
+hipError_t launch_pairs(const float *Q, int64_t d, const int32_t *probe, int64_t npairs, int nprobe, int n_lists,
+                        const float *pivot, int centred, const float2 *lstat, const uint32_t *qbound,
+                        int32_t *probe_live, float4 *QN, float *QE, float *pqn, hipStream_t st);
+hipError_t launch_wscreen(const lira_index *idx, const float *q, const int32_t *cnt, const int32_t *qoff,
+                          const int32_t *qlist, const int4 *itab, int32_t *head, const float4 *QN, const float *QE,
+                          u64 *partial, float *pE, uint32_t *qbound, int nprobe, int k, int bpc, int bpc_near,
+                          int nch_max, int n_virt, int tri, int grid, int4 *wrec, int64_t max_items, hipStream_t st);
 
 hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npairs, int nprobe, int bpc,
                        int bpc_near,
@@ -65,7 +77,6 @@ typedef const __attribute__((address_space(4))) float cfloat;  // uniform addres
 static constexpr int kSBT = 4;     // tiles per candidate block (256 candidates)
 static constexpr int kSDK = 16;    // dims per staged chunk
 static constexpr int kSThreads = 256;
-static constexpr double kU = 0x1p-24;
 
 struct ScreenArgs {
     const float *X;        // [n_tiles][dpad][64]
@@ -96,95 +107,6 @@ struct ScreenArgs {
     int dbg;  // timing experiments only (env LIRA_SCAN_DEBUG; results invalid): 1 = no MFMA, 2 = no selection,
              // 4 = no X/Q staging, 8 = per-phase clocks into stats 1/3/6 (k_screen_m)
 };
-
-// ---- error model (double) -------------------------------------------------
-// split != 0: the dot product came from the split-bf16 MFMA screen
-// (k_screen_m<..., SPLIT>): q = qh + ql + eq, x = xh + xl + ex with every part a
-// bf16 round-to-nearest (|eq| <= 2^-16 |q_i|, |ex| <= 2^-16 |x_i|), the four
-// exact products qh xh, qh xl, ql xh, ql xl summed in fp32 in an unspecified
-// order (4 dpad terms, <= 2^-22 relative per add: any rounding mode the
-// matrix core may use), so |dot~ - q.x| <= ed = (2.0001 2^-16 + 4 dpad 2^-22)
-// 1.02 |q| R + an absolute term for flushed subnormal parts (values below
-// 2^-100 lose at most 2^-100 (|q| + R) per product).  The rest of the L2
-// score's error (qn, xn, their sum, the final fma) stays <= 8.4 u (|q|+R)^2.
-//
-// centred (L2, split screen): q' = fl(q - c), x' = fl(x - c) for the list's
-// pivot c, and qnorm, R the norms of q', x'.  Then (q' - x') - (q - x) =
-// (q - c) e1 - (x - c) e2 with |e| <= u per component, so ||q'-x'||^2 differs
-// from D = ||q-x||^2 by at most u s (2 + u) s (1 + u) <= 2.01 u s^2, s = qnorm
-// + R, on top of the screen's own error for q', x'.
-//
-// split == 3 (hi x hi, k_screen_m<..., 3>): dot~ = sum qh xh, one product per
-// dim (exact in fp32), so q.x - dot~ = q.(x - xh) + (q - qh).xh and
-// |dot~ - q.x| <= |q| ||ex|| + qres (R + ||ex||) + (2 dpad 2^-22) 1.02 |q| (R +
-// ||ex||) + the subnormal term, qres >= ||q - qh|| of the row (k_qstage, QE).
-template <int METRIC>
-__device__ __forceinline__ double err_E(double qnorm, double R, double d, int split = 0, double dp = 0.0,
-                                        int centred = 0, double hres = -1.0, double qres = 0.0) {
-    const double dl = d * 0x1p-140;
-    if (split == 3) {
-        const double ex = hres >= 0.0 ? hres * 1.0001 : 0x1p-8 * 1.02 * R;
-        const double ed = ex * qnorm + qres * (R + ex) * 1.0001 + 2.0 * dp * 0x1p-22 * 1.02 * qnorm * (R + ex) +
-                          2.0 * dp * 0x1p-96 * (qnorm + R + ex + 1.0);
-        if (METRIC == LIRA_METRIC_L2) {
-            const double s = qnorm + R;
-            return 2.0 * ed + (1.05 * 8.0 + (centred ? 2.01 : 0.0)) * kU * s * s + dl;
-        }
-        return 1.05 * (ed + (d + 2.0) * kU * qnorm * R) + dl;
-    }
-    if (split) {
-        // split == 2 (hi-only x, k_screen_m<..., 2>): dot~ = sum (qh + ql) xh, x = xh + ex:
-        // |dot~ - q.x| <= |q.ex| + |(q - qh - ql).xh| + rounding <= |q| ||ex|| +
-        // (2^-16 + 2 dpad 2^-22) 1.02 |q| R, with ||ex|| <= 2^-8 R (|ex_i| <= 2^-8 |x_i|)
-        // or, tighter, hres >= ||ex|| of every candidate concerned (k_tile_hires)
-        const double ex = hres >= 0.0 ? hres * 1.0001 : 0x1p-8 * 1.02 * R;
-        const double ed = split == 2 ? ex * qnorm + (1.0001 * 0x1p-16 + 2.0 * dp * 0x1p-22) * 1.02 * qnorm * R +
-                                           2.0 * dp * 0x1p-96 * (qnorm + R + 1.0)
-                                     : (2.0001 * 0x1p-16 + 4.0 * dp * 0x1p-22) * 1.02 * qnorm * R +
-                                           4.0 * dp * 0x1p-96 * (qnorm + R + 1.0);
-        if (METRIC == LIRA_METRIC_L2) {
-            const double s = qnorm + R;
-            return 2.0 * ed + (1.05 * 8.0 + (centred ? 2.01 : 0.0)) * kU * s * s + dl;
-        }
-        // IP: bound_P / s_lim carry no (1 +- g) factor, so E also covers
-        // search.cpp's own rounding of the exact sum, (d+2) u |q| R (L2 needs
-        // no such term: that error is the g of bound_P / s_lim)
-        return 1.05 * (ed + (d + 2.0) * kU * qnorm * R) + dl;
-    }
-    if (METRIC == LIRA_METRIC_L2) {
-        const double s = qnorm + R;
-        return 1.05 * ((d + 8.0) * kU * s * s) + dl;
-    }
-    return 1.05 * (2.0 * (d + 2.0) * kU * qnorm * R) + dl;
-}
-// bound on the final k-th exact score from a list's k-th screened score
-template <int METRIC>
-__device__ __forceinline__ double bound_P(double sk, double E, double d) {
-    if (METRIC == LIRA_METRIC_L2) return (sk + E) * (1.0 + (d + 4.0) * kU) * (1.0 + 0x1p-50) + d * 0x1p-140;
-    return (sk + E) + __builtin_fabs(sk + E) * 0x1p-50;
-}
-// largest screened score a candidate may have and still score <= T exactly
-template <int METRIC>
-__device__ __forceinline__ double s_lim(double T, double E, double d) {
-    if (METRIC == LIRA_METRIC_L2) return ((T + d * 0x1p-140) / (1.0 - (d + 4.0) * kU)) * (1.0 + 0x1p-50) + E;
-    return T + E + __builtin_fabs(T + E) * 0x1p-50;
-}
-// per-block test threshold on the dot product: pass iff fl(dot - xadj) >= h.
-// L2: s~ <= lim  <=>  dot - xn/2 >= (qn - lim)/2; fl(dot - xadj) is off by at
-// most u (|q| + R)^2.  IP: xadj = 0, -s~ = dot >= -lim.
-template <int METRIC>
-__device__ __forceinline__ float row_h(double lim, double qn, double qnorm, double R) {
-    if (!(lim < 1e300)) return -__builtin_inff();
-    double h;
-    if (METRIC == LIRA_METRIC_L2) {
-        const double s = qnorm + R;
-        h = (qn - lim) * 0.5 - 1.05 * kU * s * s;
-    } else {
-        h = -lim;
-    }
-    h -= __builtin_fabs(h) * 0x1p-50;
-    return __double2float_rd(h);
-}
 
 // ---- Q staging: transposed per-item query copy + norms ---------------------
 // Block b = one query block (virtual partition v, block qb of QR pairs).
@@ -849,6 +771,7 @@ struct SMergeArgs {
     const u64 *partial;
     const float *pE;  // NULL, or the screen's error bound per row list (tighter than the list-wide one)
     const int32_t *probe, *nch, *list_size, *tile_off, *ids;
+    const int32_t *plive;  // NULL, or probe with the pairs k_pairs filtered out set to -1 (they have no lists)
     const float *Q, *Xr, *rmax;
     const uint32_t *qbound;
     float *D;
@@ -2447,6 +2370,7 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
     // rounded up by more than any summation-order difference to k_qstage's value
     const double qnorm = __builtin_sqrt(qs) * (1.0 + 0x1p-30);
     const int32_t *prow = a.probe + q * a.nprobe;
+    const int32_t *plv = a.plive ? a.plive + q * a.nprobe : prow;  // the pairs that have lists
     uint32_t *pend = s_pend[w];
     int64_t ncand = 0;
     unsigned long long n_rechecked = 0, n_rescans = 0;
@@ -2514,7 +2438,7 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
             const int li = l0 + lane, s = s_lo + li / NC, c = li % NC;
             int p = -1;
             if (li < NL) {
-                p = prow[s];
+                p = plv[s];
                 if (p < 0 || p >= a.n_lists || c >= a.nch[vnch(s, p)]) p = -1;
             }
             const u64 *src = a.partial + ((q * a.nprobe + (p >= 0 ? s : 0)) * (int64_t)NC + (p >= 0 ? c : 0)) * K2;
@@ -2551,7 +2475,7 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
                 const int ln = __builtin_ctzll(ov);
                 ov &= ov - 1;
                 const int li2 = l0 + ln;
-                rescan(s_lo + li2 / NC, prow[s_lo + li2 / NC], li2 % NC, T);
+                rescan(s_lo + li2 / NC, plv[s_lo + li2 / NC], li2 % NC, T);
             }
         }
     };
@@ -2634,9 +2558,10 @@ static int screen_smem(int qr, int rl) {
 struct SPlan {
     int rl = 1, qr = 64, K2 = 32, bpc = 1, bpc_near = 1, nch_max = 1, grid = 1, smem = 0, mfma = 1, split = 0;
     int v2 = 0, ns = 2, bc = 32;  // the pipelined split screen (k_screen_s): ring slots, buffer keys per row
+    int wide = 0;                 // the wide screen (lira_wscreen.hip k_screen_w): 256 rows per item
     int64_t max_qblk = 0;
     size_t off_cnt, off_cursor, off_head, off_qoff, off_item, off_nch, off_qblk, off_itab, off_qlist, off_qt, off_qn,
-        off_partial, off_qbound, off_pqn, off_pe, off_qe, total;
+        off_partial, off_qbound, off_pqn, off_pe, off_qe, off_live, off_wrec, total;
 };
 
 static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, unsigned flags) {
@@ -2699,7 +2624,12 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
         pl.bc = pl.qr == 128 && pl.ns == 4 ? 16 : 32;
     }
     pl.K2 = 32 * pl.rl;
-    pl.smem = pl.v2 ? (pl.qr == 128 ? (pl.ns == 4 ? SSmem2<128, 1, 4, 16>::total : SSmem2<128, 1, 3, 32>::total)
+    // the wide screen (LIRA_OPT_WIDE): the hi x hi form at 256 rows per item where its
+    // shape applies; it needs the per-query seeded bound (not PER_PARTITION)
+    pl.wide = op.wide && pl.split == 3 && !pl.v2 && pl.rl == 1 && idx->xadjc && idx->tstat && idx->lstat &&
+              wscreen_shape_ok(idx->dpad) && !(flags & LIRA_SCAN_PER_PARTITION);
+    if (pl.wide) pl.qr = 256;
+    pl.smem = pl.wide ? wscreen_smem() : pl.v2 ? (pl.qr == 128 ? (pl.ns == 4 ? SSmem2<128, 1, 4, 16>::total : SSmem2<128, 1, 3, 32>::total)
                                      : pl.rl == 1 ? (pl.ns == 4 ? SSmem2<64, 1, 4, 32>::total : SSmem2<64, 1, 2, 32>::total)
                                      : pl.rl == 2 ? SSmem2<64, 2, 4, 32>::total : SSmem2<64, 4, 3, 32>::total)
               : !pl.mfma       ? screen_smem(pl.qr, pl.rl)
@@ -2713,12 +2643,12 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
               : pl.rl == 2   ? SSmem<64, 2, true>::total
                              : SSmem<64, 4, true>::total;
     const int64_t npairs = nq * nprobe;
-    pl.grid = cu_count_s(idx->device) * std::max(1, std::min(2, (160 * 1024) / pl.smem));
+    pl.grid = pl.wide ? cu_count_s(idx->device) : cu_count_s(idx->device) * std::max(1, std::min(2, (160 * 1024) / pl.smem));
     if (op.debug & 32) pl.grid = cu_count_s(idx->device);  // timing experiment: one workgroup per CU
     // ~8 items per workgroup: fewer item prologues/epilogues and row lists to
     // merge than k_scan's 16 (measured: SIFT1M scan + merge 1.47 -> 1.22 ms on
     // the mixture, 4.80 -> 4.66 ms on latent data; 4 and 32 slower overall)
-    const int rounds = op.rounds > 0 ? op.rounds : 8;
+    const int rounds = op.rounds > 0 ? op.rounds : pl.wide ? 4 : 8;
     const int64_t target = (int64_t)rounds * pl.grid;
     // (LIRA_OPT_PROBES_HINT: the probe lists are mostly -1 padding, e.g. a
     // threshold selection padded to B; size the chunking for the expected pairs)
@@ -2749,6 +2679,10 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
         pl.bpc = std::min(pl.bpc, SSmem<64, 1, true>::kBR);
         pl.bpc_near = std::min(pl.bpc_near, pl.bpc);
     }
+    if (pl.wide) {  // k_screen_w holds <= 128 blocks of 128 candidates per item in registers
+        pl.bpc = std::min(pl.bpc, 64);
+        pl.bpc_near = std::min(pl.bpc_near, pl.bpc);
+    }
     if (pl.v2 && idx->metric == LIRA_METRIC_L2 && idx->pivot) {  // k_screen_s stages <= kBR block ranges per item
         pl.bpc = std::min(pl.bpc, SSmem2<64, 1, 4, 32>::kBR);
         pl.bpc_near = std::min(pl.bpc_near, pl.bpc);
@@ -2770,10 +2704,13 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     pl.off_nch = take(nl * 4);
     pl.off_qblk = take((nl + 1) * 4);
     pl.off_itab = take((size_t)(pl.max_qblk + 1) * pl.nch_max * 16);  // items <= query blocks x chunks
+    pl.off_wrec = take(pl.wide ? (size_t)(pl.max_qblk + 1) * pl.nch_max * 32 : 0);  // (wide) per-item records
     pl.off_qlist = take((size_t)npairs * 4);
-    pl.off_qt = take((size_t)pl.max_qblk * pl.qr * idx->dpad * 4);
-    pl.off_qn = take((size_t)pl.max_qblk * pl.qr * 16);
-    pl.off_qe = take((size_t)pl.max_qblk * pl.qr * 4);
+    // (wide: no transposed query copy; QN / QE per pair, from k_pairs)
+    pl.off_qt = take(pl.wide ? 0 : (size_t)pl.max_qblk * pl.qr * idx->dpad * 4);
+    pl.off_qn = take(pl.wide ? (size_t)npairs * 16 : (size_t)pl.max_qblk * pl.qr * 16);
+    pl.off_qe = take(pl.wide ? (size_t)npairs * 4 : (size_t)pl.max_qblk * pl.qr * 4);
+    pl.off_live = take((size_t)npairs * 4);
     pl.off_partial = take((size_t)npairs * pl.nch_max * pl.K2 * 8);
     pl.off_qbound = take((size_t)nq * 4);
     pl.off_pqn = take((size_t)npairs * 4);
@@ -2796,7 +2733,8 @@ size_t screen_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, 
 // the kernel a screened scan of this shape runs (lira_scan_describe)
 std::string screen_describe(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, unsigned flags) {
     SPlan pl = make_splan(idx, nq, nprobe, k, flags);
-    std::string s = pl.v2 ? "k_screen_s split-bf16 v_mfma_f32_16x16x32_bf16 NS=" + std::to_string(pl.ns) +
+    std::string s = pl.wide ? "k_screen_w hi-x hi-q bf16 v_mfma_f32_32x32x16_bf16"
+                    : pl.v2 ? "k_screen_s split-bf16 v_mfma_f32_16x16x32_bf16 NS=" + std::to_string(pl.ns) +
                                 " BC=" + std::to_string(pl.bc)
                     : pl.mfma ? (pl.split == 3 ? "k_screen_m hi-x hi-q bf16 v_mfma_f32_16x16x32_bf16"
                                  : pl.split == 2 ? "k_screen_m hi-x split-bf16 v_mfma_f32_16x16x32_bf16"
@@ -2950,15 +2888,56 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     const int groups_env = o.two_phase;
     const bool fill = nq >= (int64_t)pl.qr * idx->n_lists || nq * nprobe >= 4 * (int64_t)pl.qr * idx->n_lists;
     const int groups = qbound && groups_env && nprobe >= 2 && (groups_env == 2 || fill) ? 2 : 1;
-    const int nvirt = groups * (int)idx->n_lists;
-    LIRA_HIP_TRY(launch_plan(idx, probe, npairs, (int)nprobe, pl.bpc, groups == 2 ? pl.bpc_near : pl.bpc, pl.qr, groups, cnt, cursor, qoff, item_off,
-                             nch, head, qlist, qblk, itab, st));
     const bool tri = o.prune && !(flags & LIRA_SCAN_NO_PRUNE) && pl.mfma && idx->pivot;
     const float *tri_pivot = tri ? idx->pivot : nullptr;
     // the split screen works on centred vectors where the index has them (L2)
     const bool centred = pl.split && idx->xadjc != nullptr && idx->pivot != nullptr;
     const float *cpivot = centred ? idx->pivot : nullptr;
     float *pqn = centred ? (float *)(w + pl.off_pqn) : nullptr;
+    // seed bound per query (k_seed_t / k_seed) before the plan, so that
+    // k_pairs can drop the pairs whose whole list lies outside the query's
+    // triangle interval under it (they get no work item and no lists); the
+    // block-shared seed k_seed_b (LIRA_OPT_SEED 2 / 3) needs the plan's query
+    // blocks and runs after it, without the filter
+    const bool seed_b = qbound && (o.seed == 2 || o.seed == 3) && groups == 2 && k <= 32 && pl.qr == 64 &&
+                        idx->d <= 256;
+    if (!seed_b && qbound && o.seed && idx->X) {  // from the fp32 tiles (coalesced)
+        const dim3 g((unsigned)((nq + 3) / 4));
+        if (idx->metric == LIRA_METRIC_L2 && k <= 32)
+            hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2, 2>), g, dim3(256), 0, st, q, probe, (int)nprobe,
+                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound);
+        else if (idx->metric == LIRA_METRIC_L2)
+            hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2>), g, dim3(256), 0, st, q, probe, (int)nprobe,
+                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound);
+        else if (k <= 32)
+            hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_IP, 2>), g, dim3(256), 0, st, q, probe, (int)nprobe,
+                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound);
+        else
+            hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_IP>), g, dim3(256), 0, st, q, probe, (int)nprobe,
+                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound);
+        LIRA_HIP_TRY(hipGetLastError());
+    } else if (!seed_b && qbound && o.seed) {  // compact index: from the row-major copy
+        if (idx->metric == LIRA_METRIC_L2)
+            hipLaunchKernelGGL(k_seed<LIRA_METRIC_L2>, dim3((unsigned)nq), dim3(256), 0, st, q, probe,
+                               (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->Xr, idx->d, nq,
+                               (int)k, qbound);
+        else
+            hipLaunchKernelGGL(k_seed<LIRA_METRIC_IP>, dim3((unsigned)nq), dim3(256), 0, st, q, probe,
+                               (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->Xr, idx->d, nq,
+                               (int)k, qbound);
+        LIRA_HIP_TRY(hipGetLastError());
+    }
+    const bool filter = qbound && tri && !seed_b && o.seed && idx->lstat != nullptr;
+    int32_t *plive = filter || pl.wide ? (int32_t *)(w + pl.off_live) : nullptr;
+    if (plive)
+        LIRA_HIP_TRY(launch_pairs(q, idx->d, probe, npairs, (int)nprobe, (int)idx->n_lists, idx->pivot,
+                                  centred ? 1 : 0, filter ? idx->lstat : nullptr, filter ? qbound : nullptr, plive,
+                                  pl.wide ? QN : nullptr, pl.wide ? QE : nullptr, pl.wide ? pqn : nullptr, st));
+    const int32_t *pprobe = plive ? plive : probe;  // the pairs that become work
+    const int nvirt = groups * (int)idx->n_lists;
+    LIRA_HIP_TRY(launch_plan(idx, pprobe, npairs, (int)nprobe, pl.bpc, groups == 2 ? pl.bpc_near : pl.bpc, pl.qr, groups, cnt, cursor, qoff, item_off,
+                             nch, head, qlist, qblk, itab, st));
+    if (!pl.wide) {
     const dim3 qgrid((unsigned)pl.max_qblk, (unsigned)((idx->dpad + 64 * kQSlabs - 1) / (64 * kQSlabs)));
     if (pl.qr == 128 && pl.split)
         hipLaunchKernelGGL((k_qstage<128, true>), qgrid, dim3(256), 0, st, q, idx->d, idx->dpad,
@@ -2979,14 +2958,13 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
         hipLaunchKernelGGL((k_qstage<32, false>), qgrid, dim3(256), 0, st, q, idx->d, idx->dpad,
                            (int)nprobe, nvirt, (int)idx->n_lists, cnt, qoff, qlist, qblk, tri_pivot, cpivot, QT, QN, pqn, QE);
     LIRA_HIP_TRY(hipGetLastError());
+    }
     // (measured: SIFT1M mixture 1.70 -> 1.44 ms, latent +1 %)
     // LIRA_OPT_SEED 2 / 3: per nearest-partition query block (k_seed_b, 128 /
     // 256 rows) where the plan has that group.  Measured SIFT1M: the same
     // survivors as k_seed_t's 128 rows, plan 0.122 -> 0.143 ms (~220 workgroups
     // of exact VALU work leave most of the chip idle); 256 rows: survivors
     // -28 %, scan -0.02 ms, plan +0.06 ms.  So the per-query seed is the default.
-    const bool seed_b = qbound && (o.seed == 2 || o.seed == 3) && groups == 2 && k <= 32 && pl.qr == 64 &&
-                        idx->d <= 256;
     if (seed_b) {
         const dim3 g((unsigned)std::min<int64_t>(pl.max_qblk, (nq + 63) / 64 + idx->n_lists));
         if (idx->metric == LIRA_METRIC_L2 && o.seed == 3)
@@ -3001,31 +2979,6 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
         else
             hipLaunchKernelGGL((k_seed_b<LIRA_METRIC_IP, 64, 128>), g, dim3(256), 0, st, q, idx->d, (int)nprobe,
                                (int)idx->n_lists, cnt, qoff, qlist, qblk, idx->tile_off, idx->ids, idx->Xr, (int)k, qbound);
-        LIRA_HIP_TRY(hipGetLastError());
-    } else if (qbound && o.seed && idx->X) {  // from the fp32 tiles (coalesced)
-        const dim3 g((unsigned)((nq + 3) / 4));
-        if (idx->metric == LIRA_METRIC_L2 && k <= 32)
-            hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2, 2>), g, dim3(256), 0, st, q, probe, (int)nprobe,
-                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound);
-        else if (idx->metric == LIRA_METRIC_L2)
-            hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2>), g, dim3(256), 0, st, q, probe, (int)nprobe,
-                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound);
-        else if (k <= 32)
-            hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_IP, 2>), g, dim3(256), 0, st, q, probe, (int)nprobe,
-                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound);
-        else
-            hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_IP>), g, dim3(256), 0, st, q, probe, (int)nprobe,
-                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound);
-        LIRA_HIP_TRY(hipGetLastError());
-    } else if (qbound && o.seed) {  // compact index: from the row-major copy
-        if (idx->metric == LIRA_METRIC_L2)
-            hipLaunchKernelGGL(k_seed<LIRA_METRIC_L2>, dim3((unsigned)nq), dim3(256), 0, st, q, probe,
-                               (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->Xr, idx->d, nq,
-                               (int)k, qbound);
-        else
-            hipLaunchKernelGGL(k_seed<LIRA_METRIC_IP>, dim3((unsigned)nq), dim3(256), 0, st, q, probe,
-                               (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->Xr, idx->d, nq,
-                               (int)k, qbound);
         LIRA_HIP_TRY(hipGetLastError());
     }
     if (ev[1]) LIRA_HIP_TRY(hipEventRecord(ev[1], st));
@@ -3066,8 +3019,12 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     a.bpc_near = groups == 2 ? pl.bpc_near : pl.bpc;
     a.nch_max = pl.nch_max;
     a.stats = idx->stats_on ? (unsigned long long *)idx->stats : nullptr;
-    hipError_t e = idx->metric == LIRA_METRIC_L2 ? launch_screen_rl<LIRA_METRIC_L2>(a, pl, st)
-                                                 : launch_screen_rl<LIRA_METRIC_IP>(a, pl, st);
+    hipError_t e = pl.wide ? launch_wscreen(idx, q, cnt, qoff, qlist, itab, head, QN, QE, partial, pE, qbound,
+                                            (int)nprobe, (int)k, pl.bpc, a.bpc_near, pl.nch_max, nvirt, tri ? 1 : 0,
+                                            pl.grid, (int4 *)(w + pl.off_wrec),
+                                            (int64_t)(pl.max_qblk + 1) * pl.nch_max, st)
+                   : idx->metric == LIRA_METRIC_L2 ? launch_screen_rl<LIRA_METRIC_L2>(a, pl, st)
+                                                   : launch_screen_rl<LIRA_METRIC_IP>(a, pl, st);
     if (e != hipSuccess) return fail(LIRA_EHIP, std::string("k_screen launch: ") + hipGetErrorString(e));
     if (ev[2]) LIRA_HIP_TRY(hipEventRecord(ev[2], st));
 
@@ -3075,6 +3032,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     m.partial = partial;
     m.pE = pE;
     m.probe = probe;
+    m.plive = plive;
     m.nch = nch;
     m.list_size = idx->list_size;
     m.tile_off = idx->tile_off;

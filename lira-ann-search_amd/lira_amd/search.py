@@ -84,25 +84,30 @@ class SearchEngine:
         dist = centroid_dist(q, self.centroids, self.mean, self.scale)
         return probe_scores(self.model, dist, q)
 
+    def pipeline(self, nq: int, k: int) -> "ProbePipeline":
+        """The ProbePipeline of a batch shape (built once per (nq, k); the
+        threshold is an argument of each run)."""
+        key = (int(nq), int(k))
+        if self._pipe is None or self._pipe_key != key:
+            self._pipe = ProbePipeline(self.index, self.centroids, self.mean, self.scale, self.model,
+                                       int(nq), int(k), 0.5, max_probe=self.n_bkt, dedup=self.dedup)
+            self._pipe_key = key
+        return self._pipe
+
     def search(self, q, threshold: float, k: int, scores: torch.Tensor | None = None):
-        """One threshold: returns (D, I, nprobe, ncand) device tensors.
+        """One threshold: returns fresh (D, I, nprobe, ncand) device tensors.
 
         Without precomputed ``scores`` this runs the ProbePipeline of the
         batch shape (distances + standardise in one kernel, MLP, select, scan
-        on preallocated buffers; the tensors returned are that pipeline's
-        buffers, valid until the next search of the same shape)."""
+        on preallocated buffers) and returns copies of its outputs, so a later
+        search never overwrites them."""
         q = q if isinstance(q, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(q))
         q = q.to(self.device, torch.float32).contiguous()
         if scores is None:
-            key = (q.shape[0], int(k), float(threshold))
-            if self._pipe is None or self._pipe_key != key:
-                self._pipe = ProbePipeline(self.index, self.centroids, self.mean, self.scale, self.model,
-                                           q.shape[0], k, threshold, max_probe=self.n_bkt, dedup=self.dedup)
-                self._pipe_key = key
-            self._pipe.q.copy_(q)
-            self._pipe.run()
-            p = self._pipe
-            return p.D, p.I, p.nprobe, p.ncand
+            p = self.pipeline(q.shape[0], k)
+            p.q.copy_(q)
+            p.run(threshold)
+            return p.D.clone(), p.I.clone(), p.nprobe.clone(), p.ncand.clone()
         probe, nprobe = select_probes(scores, "ge", self.n_bkt, threshold)
         D, I, ncand = self.index.search(q, probe, k, dedup=self.dedup)
         return D, I, nprobe, ncand
@@ -111,6 +116,7 @@ class SearchEngine:
         """search.cpp:413-548 for a query set; one row per threshold."""
         qt = torch.from_numpy(np.ascontiguousarray(q)).to(self.device)
         k = min(k, gt.shape[1])  # search.cpp:357-360 clamps k to the gt width
+        self.pipeline(qt.shape[0], k)  # (buffers allocated outside the timed region)
         rows = []
         for thr in thresholds(t_min, t_max, t_step):
             torch.cuda.synchronize()
@@ -162,20 +168,26 @@ class ProbePipeline:
         self.D = torch.empty((nq, k), dtype=torch.float32, device=dev)
         self.I = torch.empty((nq, k), dtype=torch.int64, device=dev)
         self.ncand = torch.empty(nq, dtype=torch.int64, device=dev)
-        self.scores = None
+        # the model's output lands in an fp32 buffer of its own (any output dtype or
+        # layout is converted by the copy; keeps the chain graph-capturable)
+        self.scores = torch.empty((nq, nb), dtype=torch.float32, device=dev)
         self.graph = None
         # search.cpp's set (>= thr, argmax fallback); ordered by descending score
         # where the list fits (same results, faster scan: most probable partition first)
         from . import _lib
         self.mode = _lib.LIRA_PROBE_THRESHOLD_GE | (_lib.LIRA_PROBE_BY_SCORE if self.max_probe <= 256 else 0)
-        if expect_probes:  # a performance hint for the scan's work split (LIRA_OPT_PROBES_HINT)
-            index.set_option("probes_hint", int(expect_probes))
+        # a performance hint for the scan's work split (LIRA_OPT_PROBES_HINT), applied
+        # around this pipeline's own scans only
+        self.expect_probes = int(expect_probes or 0)
 
     @torch.no_grad()
-    def run(self):
-        """One pass over self.q (stream-ordered, asynchronous)."""
+    def run(self, threshold: float | None = None):
+        """One pass over self.q (stream-ordered, asynchronous), at `threshold`
+        (default: the pipeline's own)."""
+        if threshold is not None:
+            self.thr = float(threshold)
         centroid_dist(self.q, self.C, self.mean, self.scale, out=self.dist)
-        self.scores = self.model(self.dist, self.q)
+        self.scores.copy_(self.model(self.dist, self.q))
         self._select_scan()
 
     def _select_scan(self):
@@ -184,7 +196,14 @@ class ProbePipeline:
             _lib.call("lira_select_probes", _lib.ptr(self.scores), self.q.shape[0], self.C.shape[0],
                       self.mode, self.thr, self.max_probe, _lib.ptr(self.probe), _lib.ptr(self.nprobe),
                       _lib.stream_ptr())
-        self.index.search(self.q, self.probe, self.k, dedup=self.dedup, out=(self.D, self.I, self.ncand))
+        old = self.index.get_option("probes_hint") if self.expect_probes else None
+        if self.expect_probes:
+            self.index.set_option("probes_hint", self.expect_probes)
+        try:
+            self.index.search(self.q, self.probe, self.k, dedup=self.dedup, out=(self.D, self.I, self.ncand))
+        finally:
+            if old is not None:
+                self.index.set_option("probes_hint", old)
 
     def capture(self):
         """Record run() into a HIP graph (after one eager warm-up run, so the

@@ -197,3 +197,37 @@ def test_probe_pipeline_graph_matches_eager_and_oracle():
     Do, Io, _ = oracle.scan_topk(q, off, ids, x[ids], pr, 10, oracle.L2, 1)
     assert np.array_equal(I0.cpu().numpy(), Io)
     assert np.array_equal(D0.cpu().numpy().view(np.uint32), Do.view(np.uint32))
+
+
+def test_search_engine_results_do_not_alias():
+    # SearchEngine.search returns fresh tensors (a later search of the same
+    # shape does not overwrite them), reuses one pipeline across thresholds and
+    # leaves the index's options as they were
+    from lira_amd.io import save_artifacts
+    from lira_amd.probing import MLP_2_Input
+    from lira_amd.search import SearchEngine
+    import tempfile
+    x, c, rng = mixture(6000, 32, 12, 5)
+    d2b = oracle.centroid_dist(x, c).argmin(1).astype(np.int32)[:, None]
+    q = (c[rng.integers(0, 12, 64)] + 0.35 * rng.standard_normal((64, 32), dtype=np.float32)).astype(np.float32)
+    dist = oracle.centroid_dist(x, c)
+    torch.manual_seed(1)
+    with tempfile.TemporaryDirectory() as td:
+        save_artifacts(td + "/a", c, d2b, x, dist.mean(0).astype(np.float32), dist.std(0).astype(np.float32),
+                       MLP_2_Input(12, 32, 12))
+        eng = SearchEngine(td + "/a")
+    qt = torch.from_numpy(q).cuda()
+    s = eng.scores(qt).cpu().numpy()
+    t1, t2 = float(np.quantile(s, 0.3)), float(np.quantile(s, 0.7))
+    D1, I1, n1, _ = eng.search(qt, t1, 10)
+    D1c, I1c, n1c = D1.clone(), I1.clone(), n1.clone()
+    pipe = eng._pipe
+    D2, I2, n2, _ = eng.search(qt, t2, 10)
+    assert eng._pipe is pipe
+    assert torch.equal(D1, D1c) and torch.equal(I1, I1c) and torch.equal(n1, n1c)
+    assert not torch.equal(n1, n2)
+    # each threshold's result equals a scan of its own selection
+    for thr, I, n in ((t1, I1, n1), (t2, I2, n2)):
+        pr, cnt = oracle.probe_threshold(s, thr)
+        assert np.array_equal(n.cpu().numpy(), cnt)
+    assert eng.index.get_option("probes_hint") == 0

@@ -86,6 +86,11 @@ def check_vs_oracle(x, q, d2b, probe, b, k, metric, dedup=True):
             assert np.array_equal(I, Io), f"ids differ (xhi={xhi})"
             assert np.array_equal(bits(D), bits(Do)), f"distances differ (xhi={xhi})"
         idx.set_option("xhi", -1)
+        # the 64-row screen k_screen_m where the wide one (k_screen_w) is the default
+        idx.set_option("wide", 0)
+        D, I, nc = run(idx, q, probe, k, dedup=dedup)
+        idx.set_option("wide", 1)
+        assert np.array_equal(I, Io) and np.array_equal(bits(D), bits(Do)), "differ (wide=0)"
     if k <= 120:
         # the compact index (no fp32 tiles: row-major + split-bf16 copies only)
         idc = make_index(x, d2b, b, metric, keep_tiles=False)
@@ -370,7 +375,8 @@ def test_options_do_not_change_results(metric):
     ref = run(idx, q, probe, 10)
     for name, vals in (("qr", (128,)), ("two_phase", (0, 2)), ("seed", (0, 2, 3)), ("share", (0,)),
                        ("prune", (0,)), ("split", (0,)), ("mfma", (0, 2)), ("rounds", (1, 64)),
-                       ("near_rounds", (8,)), ("screen", (0,)), ("ring", (2, 3, 4)), ("probes_hint", (1, 4)), ("xhi", (0, 1, 2))):
+                       ("near_rounds", (8,)), ("screen", (0,)), ("ring", (2, 3, 4)), ("probes_hint", (1, 4)), ("xhi", (0, 1, 2)),
+                       ("wide", (0,))):
         old = idx.get_option(name)
         for v in vals:
             idx.set_option(name, v)
@@ -391,12 +397,17 @@ def test_options_do_not_change_results(metric):
         D3, I3, _ = run(idx, q, probe, k)
         idx.set_option("qr", 0)
         assert np.array_equal(I3, I1) and np.array_equal(bits(D3), bits(D1)), ("qr32", k)
-    # the pipelined screen's ring variants at both query-block sizes
-    for qr, ring in ((64, 2), (64, 4), (128, 3), (128, 4)):
+    # the pipelined screen k_screen_s (LIRA_OPT_PIPELINE = 1 with a ring size):
+    # every RL 1 ring / query-block instantiation at k = 10, RL 2 at k = 40
+    idx.set_option("pipeline", 1)
+    for kk, qr, ring in ((10, 64, 2), (10, 64, 4), (10, 128, 3), (10, 128, 4), (40, 0, 4)):
         idx.set_option("qr", qr)
         idx.set_option("ring", ring)
-        D, I, nc = run(idx, q, probe, 10)
-        assert np.array_equal(I, ref[1]) and np.array_equal(bits(D), bits(ref[0])), (qr, ring)
+        want = ref if kk == 10 else run(make_index(x, d2b, 8, metric), q, probe, kk)
+        D, I, nc = run(idx, q, probe, kk)
+        assert "k_screen_s" in idx.describe(q.shape[0], probe.shape[1], kk), (qr, ring)
+        assert np.array_equal(I, want[1]) and np.array_equal(bits(D), bits(want[0])), (kk, qr, ring)
+    idx.set_option("pipeline", 0)
     idx.set_option("qr", 0)
     idx.set_option("ring", 0)
 
@@ -419,3 +430,46 @@ def test_split_screen_extreme_values(metric):
     d2b = rng.integers(0, b, (n, 1)).astype(np.int32)
     probe = np.tile(np.arange(b, dtype=np.int32), (q.shape[0], 1))
     check_vs_oracle(x, q, d2b, probe, b, 10, metric)
+
+
+@pytest.mark.parametrize("d,uniform,red", [(48, False, 0.0), (96, False, 0.2), (128, False, 0.0), (128, True, 0.0),
+                                           (100, True, 0.1)])
+def test_wide_screen_vs_oracle(d, uniform, red):
+    # the wide screen k_screen_w (256 rows per item, 128-candidate blocks, 16-KiB
+    # ring slots): several query blocks per list, lists of several chunks with a
+    # partial last block (one tile) and padded rows, partial query blocks,
+    # redundant rows with and without dedup
+    n, b, nq, nprobe, k = 60000, 10, 1500, 4, 10
+    x, q, d2b, probe = random_case(300 + d, n, d, b, nq, nprobe, "L2", red=red, uniform=uniform)
+    idx = make_index(x, d2b, b, "L2")
+    assert "k_screen_w" in idx.describe(nq, nprobe, k), idx.describe(nq, nprobe, k)
+    off, ids = oracle.build_csr(d2b, b)
+    vecs = oracle.gather_lists(x, off, ids)
+    for dedup in (True, False):
+        Do, Io, nco = oracle.scan_topk(q, off, ids, vecs, probe, k, oracle.L2, idx.max_replicas if dedup else 0)
+        for rounds in (0, 1, 64):  # items of whole lists, and many short chunks
+            idx.set_option("rounds", rounds)
+            D, I, nc = run(idx, q, probe, k, dedup=dedup)
+            assert np.array_equal(I, Io) and np.array_equal(bits(D), bits(Do)), (dedup, rounds)
+            assert np.array_equal(nc, nco)
+        idx.set_option("rounds", 0)
+
+
+def test_wide_screen_clustered_filter_and_ties():
+    # separated clusters: k_pairs drops the far pairs (no work items), the
+    # triangle skip drops blocks; small-integer vectors: exact ties at the k-th
+    x, q, d2b, probe = clustered_case(71, 40000, 128, 16, 900, 6, ints=True)
+    idx = make_index(x, d2b, 16, "L2")
+    assert "k_screen_w" in idx.describe(q.shape[0], probe.shape[1], 10)
+    off, ids = oracle.build_csr(d2b, 16)
+    vecs = oracle.gather_lists(x, off, ids)
+    for k in (1, 10, 24):
+        Do, Io, nco = oracle.scan_topk(q, off, ids, vecs, probe, k, oracle.L2, idx.max_replicas)
+        D, I, nc = run(idx, q, probe, k)
+        assert np.array_equal(I, Io) and np.array_equal(bits(D), bits(Do)), k
+        assert np.array_equal(nc, nco)
+        idx.set_stats(True)
+        run(idx, q, probe, k)
+        st = idx.stats_read()
+        idx.set_stats(False)
+        assert st["blocks"] > 0
