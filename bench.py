@@ -100,6 +100,58 @@ def oracle_sample(oracle, idx, x, q, probe, rows, k, metric, lists, threads=8):
                                     idx.max_replicas, threads)
 
 
+def blas_scan_topk(qs, off, ids, vecs, ps, k, ip):
+    """CPU approximation of faiss IndexFlatL2/IP.search's BLAS path
+    (LIRA_smallscale.py:168 calls inner_index.search per bucket): for every
+    probed list, the queries that probe it in one block -> one sgemm
+    (torch CPU, all threads), ||q||^2 - 2 q.x + ||x||^2 (norms computed per
+    search, as faiss' exhaustive_L2sqr_blas does), top-k per (query, list), then
+    top-k over each query's nprobe x k candidates (replicas not de-duplicated).
+    Not bit-exact with search.cpp's sequential sum; a baseline, not the oracle."""
+    n, P = ps.shape
+    worst = -np.inf if ip else np.inf
+    cD = torch.full((n * P, k), worst, dtype=torch.float32)
+    cI = torch.full((n * P, k), -1, dtype=torch.int64)
+    Q = torch.from_numpy(np.ascontiguousarray(qs))
+    qn = (Q * Q).sum(1)
+    flat = ps.ravel()
+    order = np.argsort(flat, kind="stable")
+    fs = flat[order]
+    cut = np.flatnonzero(np.diff(fs)) + 1
+    for grp in np.split(order, cut):
+        b = int(flat[grp[0]])
+        if b < 0 or off[b + 1] == off[b]:
+            continue
+        lo, hi = int(off[b]), int(off[b + 1])
+        X = torch.from_numpy(vecs[lo:hi])
+        qi = torch.from_numpy(grp // P)
+        G = Q[qi] @ X.T
+        if ip:
+            v, j = torch.topk(G, min(k, hi - lo), dim=1)
+        else:
+            G.mul_(-2).add_(qn[qi, None]).add_((X * X).sum(1)[None, :])
+            v, j = torch.topk(G, min(k, hi - lo), dim=1, largest=False)
+        rows = torch.from_numpy(grp)
+        cD[rows, :v.shape[1]] = v
+        cI[rows, :v.shape[1]] = torch.from_numpy(ids[lo:hi])[j.reshape(-1)].reshape(j.shape).long()
+    v, j = torch.topk(cD.view(n, P * k), k, dim=1, largest=ip)
+    return v.numpy(), torch.gather(cI.view(n, P * k), 1, j).numpy()
+
+
+def time_blas(qs, ps, host, k, ip, threads, budget_s=10.0):
+    """Times blas_scan_topk on a bounded prefix of the batch (pilot of 64
+    queries scaled to ~budget_s seconds).  Returns (n, seconds, D, I)."""
+    torch.set_num_threads(threads)
+    pilot = min(64, len(qs))
+    tp = time.perf_counter()
+    blas_scan_topk(qs[:pilot], *host, ps[:pilot], k, ip)
+    per_q = max(time.perf_counter() - tp, 1e-9) / pilot
+    n = int(min(len(qs), max(pilot, budget_s / per_q)))
+    tc = time.perf_counter()
+    D, I = blas_scan_topk(qs[:n], *host, ps[:n], k, ip)
+    return n, time.perf_counter() - tc, D, I
+
+
 def parse_opts(items, config):
     opts = {}
     if config == "bigann100m":
@@ -373,16 +425,39 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
             with ThreadPoolExecutor(threads) as ex:
                 list(ex.map(lambda a: oracle.scan_topk(*a, k, met, index.max_replicas), prep))
             cpu_s = time.perf_counter() - tc
+            prep_b = [(a[0], a[1], a[2], a[3], a[4]) for a in prep]
             del prep
-        out["cpu_baseline"] = {
+        scalar = {
             "value": n_cpu / cpu_s, "unit": "queries/s", "cores": threads, "kind": "port",
             "sample": f"{n_cpu} queries of the same batch and probe lists, scan + top-k (oracle/lira_oracle.c "
                       f"= search.cpp:471-514's sequential fp32 arithmetic), one query per thread",
-            "seconds": cpu_s, "single_thread_qps": st_qps, "nproc": os.cpu_count(),
-            "cpu_model": cpu_model(),
-            "note": "cores = threads used = the box's allotted CPU share (OMP_NUM_THREADS); nproc counts "
-                    "the whole machine; nproc_linear_estimate = single-thread QPS x nproc (not measured)",
+            "seconds": cpu_s, "single_thread_qps": st_qps,
             "nproc_linear_estimate_qps": st_qps * (os.cpu_count() or 1)}
+        # faiss-like blocked BLAS form (the stronger CPU; it is what value reports)
+        ip = metric == "inner_product"
+        if host is not None:
+            nb, bs, Db, Ib = time_blas(qh, ph, host, k, ip, threads)
+            gI = I[:nb].cpu().numpy()
+        else:
+            nb, bs, acc = len(prep_b), 0.0, []
+            torch.set_num_threads(threads)
+            for a in prep_b:
+                tc = time.perf_counter()
+                acc.append(blas_scan_topk(*a, k, ip)[1])
+                bs += time.perf_counter() - tc
+            Ib, gI = np.concatenate(acc), I[:nb].cpu().numpy()
+        agree = float(np.mean([len(set(Ib[i]) & set(gI[i])) / k for i in range(nb)]))
+        out["cpu_baseline"] = {
+            "value": nb / bs, "unit": "queries/s", "cores": threads, "kind": "port",
+            "sample": f"{nb} queries of the same batch and probe lists: faiss-like blocked sgemm + top-k "
+                      f"(torch CPU, {threads} threads; approximates faiss IndexFlat.search's BLAS path, "
+                      f"LIRA_smallscale.py:168) -- bench.py:blas_scan_topk",
+            "seconds": bs, "topk_agreement_with_gpu": agree,
+            "cores_of_nproc": f"{threads} of {os.cpu_count()}", "nproc": os.cpu_count(),
+            "cpu_model": cpu_model(), "scalar_port": scalar,
+            "note": "cores = threads used = the box's allotted CPU share (OMP_NUM_THREADS); nproc counts "
+                    "the whole machine (not all of it is ours); scalar_port = search.cpp's own one-query-"
+                    "per-thread form; nproc_linear_estimate = its single-thread QPS x nproc (not measured)"}
     # ---- the MLP-probed search.cpp pipeline, N = 1 ---------------
     if primary and world == 1 and B <= 256 and not args.no_pipeline:
         out["pipeline"] = time_pipeline(args, oracle, index, x, centres, q, make_queries, k, nprobe, metric,

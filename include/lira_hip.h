@@ -110,7 +110,10 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
  */
 int lira_index_build(lira_index *idx, int64_t n_lists, const int32_t *data_2_bkt, int64_t n,
                      int32_t n_mul, const float *x, void *stream);
-/* host copy of one bucket's row ids, in list order (ascending after lira_index_build) */
+/* host copy of one bucket's row ids, in STORAGE order: with LIRA_OPT_ORDER=1 (the L2
+ * default) rows are stored by ascending distance to the list's pivot, so this is a
+ * permutation of the ids passed to add/build (compare as sets; ordering never
+ * changes a search result) */
 int lira_index_list_ids(const lira_index *idx, int64_t list_no, int32_t *out_host, void *stream);
 
 /* sizes: ntotal = total rows incl. replicas (faiss .ntotal, LIRA_smallscale.py:171) */
@@ -123,7 +126,8 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
 
 /*
  * Per-handle tuning options (no process environment is read by the library).
- * None of them changes a result: every setting returns the same bits.
+ * None of them changes a result: every setting returns the same bits (the one
+ * exception, LIRA_OPT_DEBUG, is refused unless the library is built with -DLIRA_DEBUG).
  *   LIRA_OPT_KEEP_TILES  1 (default): keep the fp32 d-major tile copy that the
  *                        all-exact scan (LIRA_SCAN_EXACT / _FMA) and the VALU
  *                        screen read; 0: the index holds only the row-major
@@ -143,7 +147,9 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *   LIRA_OPT_ROUNDS      work items per workgroup target (0 = kernel default)
  *   LIRA_OPT_NEAR_ROUNDS the same for the nearest-probe group (default 2)
  *   LIRA_OPT_MFMA        screen engine: 1 auto (default), 0 VALU, 2 MFMA wherever it fits
- *   LIRA_OPT_DEBUG       timing experiments only (results invalid): bit mask, see lira_screen.hip
+ *   LIRA_OPT_DEBUG       timing experiments only (results invalid): bit mask, see lira_screen.hip.
+ *                        Production builds accept only 0 and return LIRA_EUNSUPPORTED otherwise;
+ *                        a -DLIRA_DEBUG build (tools/build_variant.sh) accepts 0..255
  *   LIRA_OPT_PIPELINE    1: the pipelined split screen k_screen_s for k > 56; 0 (default): k_screen_m
  *   LIRA_OPT_RING        k_screen_s ring slots: 0 auto, 2..4
  *   LIRA_OPT_PROBES_HINT expected valid probes per query when the probe lists are mostly -1
@@ -157,10 +163,10 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *                        each list's rows by ascending distance to the list's pivot, so tile radius
  *                        ranges are narrow and the triangle-inequality skip drops more; 0: list order.
  *                        Results never depend on it.
- *   LIRA_OPT_WIDE        1 (default): the wide screen k_screen_w (256 query rows per item, one
+ *   LIRA_OPT_WIDE        1: the wide screen k_screen_w (256 query rows per item, one
  *                        512-thread workgroup per CU, v_mfma_f32_32x32x16_bf16) where it applies
  *                        (L2 with the centred split copy, k <= 24, dpad 64 / 96 / 128, a seeded
- *                        bound); 0: k_screen_m
+ *                        bound); 0 (default): k_screen_m (measured faster on every config)
  */
 #define LIRA_OPT_KEEP_TILES 1
 #define LIRA_OPT_SCREEN 2

@@ -739,13 +739,17 @@ int lira_index_set_option(lira_index *idx, int option, int64_t value) {
         case LIRA_OPT_ROUNDS: if (!in(0, 1024)) break; o.rounds = v; return LIRA_OK;
         case LIRA_OPT_NEAR_ROUNDS: if (!in(1, 1024)) break; o.near_rounds = v; return LIRA_OK;
         case LIRA_OPT_MFMA: if (!in(0, 2)) break; o.mfma = v; return LIRA_OK;
-        case LIRA_OPT_DEBUG: if (!in(0, 255)) break; o.debug = v; return LIRA_OK;
+        case LIRA_OPT_DEBUG:
+            if (!in(0, 255)) break;
+            if (v && !debug_build())  // a production build never returns invalid results
+                return fail(LIRA_EUNSUPPORTED, "LIRA_OPT_DEBUG needs a library built with -DLIRA_DEBUG");
+            o.debug = v; return LIRA_OK;
         case LIRA_OPT_PIPELINE: if (!in(0, 1)) break; o.pipeline = v; return LIRA_OK;
         case LIRA_OPT_RING: if (!in(0, 4)) break; o.ring = v; return LIRA_OK;
         case LIRA_OPT_PROBES_HINT: if (!in(0, 1 << 20)) break; o.probes_hint = v; return LIRA_OK;
         case LIRA_OPT_XHI: if (!in(-1, 2)) break; o.xhi = v; return LIRA_OK;
         case LIRA_OPT_ORDER: if (!in(0, 1)) break; o.order = v; return LIRA_OK;
-        case LIRA_OPT_WIDE: if (!in(0, 1)) break; o.wide = v; return LIRA_OK;
+        case LIRA_OPT_WIDE: if (!in(0, 2)) break; o.wide = v; return LIRA_OK;
         default: return fail(LIRA_EINVAL, "unknown option " + std::to_string(option));
     }
     return fail(LIRA_EINVAL, "value " + std::to_string(value) + " out of range for option " + std::to_string(option));

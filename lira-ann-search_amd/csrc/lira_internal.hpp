@@ -14,6 +14,9 @@ namespace lira {
 // thread-local message behind lira_last_error()
 void set_error(const std::string &msg);
 int fail(int code, const std::string &msg);
+// true only when lira_screen.hip is compiled with -DLIRA_DEBUG (or -DLIRA_PHASE_CLOCKS):
+// then LIRA_OPT_DEBUG's result-invalidating timing switches are accepted
+bool debug_build();
 
 #define LIRA_HIP_TRY(expr)                                                                     \
     do {                                                                                       \
@@ -50,7 +53,7 @@ struct lira_opts {
     int probes_hint = 0;
     int xhi = -1;
     int order = 1;
-    int wide = 1;
+    int wide = 0;
 };
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device):

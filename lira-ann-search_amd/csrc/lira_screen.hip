@@ -64,6 +64,15 @@ hipError_t launch_wscreen(const lira_index *idx, const float *q, const int32_t *
                           u64 *partial, float *pE, uint32_t *qbound, int nprobe, int k, int bpc, int bpc_near,
                           int nch_max, int n_virt, int tri, int grid, int4 *wrec, int64_t max_items, hipStream_t st);
 
+// lira_vscreen.hip
+bool vscreen_shape_ok(int64_t dpad);
+int vscreen_smem();
+int vscreen_max_tiles();
+hipError_t launch_vscreen(const lira_index *idx, const float *q, const int32_t *cnt, const int32_t *qoff,
+                          const int32_t *qlist, const int4 *itab, int32_t *head, const float4 *QN, const float *QE,
+                          u64 *partial, float *pE, uint32_t *qbound, int nprobe, int k, int bpc, int bpc_near,
+                          int nch_max, int n_virt, int tri, int grid, int4 *vrec, int64_t max_items, hipStream_t st);
+
 hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npairs, int nprobe, int bpc,
                        int bpc_near,
                        int qr, int groups, int32_t *cnt, int32_t *cursor, int32_t *qoff, int32_t *item_off,
@@ -104,7 +113,7 @@ struct ScreenArgs {
     int share;     // k_screen_m: publish/re-read the query bound every block (else once per item)
     int split;     // k_screen_m<..., SPLIT = 1>: X is the split-bf16 copy (Xb), QT in the split layout
     int centred;   // (L2, split) Xb / QT hold x - c / q - c of the list's pivot; xadj, rmax, QN are theirs
-    int dbg;  // timing experiments only (env LIRA_SCAN_DEBUG; results invalid): 1 = no MFMA, 2 = no selection,
+    int dbg;  // timing experiments only (LIRA_OPT_DEBUG, -DLIRA_DEBUG builds; results invalid): 1 = no MFMA, 2 = no selection,
              // 4 = no X/Q staging, 8 = per-phase clocks into stats 1/3/6 (k_screen_m)
 };
 
@@ -320,6 +329,11 @@ __device__ __forceinline__ void sglds16b(const void *gsrc, uint32_t lds_addr) {
 static constexpr bool kPhaseClocks = true;
 #else
 static constexpr bool kPhaseClocks = false;
+#endif
+#if defined(LIRA_DEBUG) || defined(LIRA_PHASE_CLOCKS)
+bool debug_build() { return true; }
+#else
+bool debug_build() { return false; }
 #endif
 #ifndef LIRA_SGLDS
 #define LIRA_SGLDS sglds16
@@ -784,6 +798,7 @@ struct SMergeArgs {
     int centred;           // ... on centred vectors: pqn[pair] = the row's norm, rmax the centred one
     const float *pqn;
     unsigned long long *stats;
+    int unsorted;  // a list may hold its keys unsorted (k_screen_v): walk it to its first empty key
 };
 
 // exact score of the candidate at storage row pos (search.cpp:253-269 order)
@@ -2466,8 +2481,12 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    if (active) active = kv[u] != kEmptyKey && (double)key_score(kv[u]) <= lim;
-                    add(active, (uint32_t)kv[u]);
+                    bool take = false;
+                    if (active) {
+                        take = kv[u] != kEmptyKey && (double)key_score(kv[u]) <= lim;
+                        active = a.unsorted ? kv[u] != kEmptyKey : take;
+                    }
+                    add(take, (uint32_t)kv[u]);
                 }
             }
             u64 ov = __ballot(over);
@@ -2558,7 +2577,8 @@ static int screen_smem(int qr, int rl) {
 struct SPlan {
     int rl = 1, qr = 64, K2 = 32, bpc = 1, bpc_near = 1, nch_max = 1, grid = 1, smem = 0, mfma = 1, split = 0;
     int v2 = 0, ns = 2, bc = 32;  // the pipelined split screen (k_screen_s): ring slots, buffer keys per row
-    int wide = 0;                 // the wide screen (lira_wscreen.hip k_screen_w): 256 rows per item
+    int wide = 0;                 // 1: the wide screen (lira_wscreen.hip k_screen_w), 256 rows per item;
+                                  // 2: the wave-resident screen (lira_vscreen.hip k_screen_v), 64 rows per wave
     int64_t max_qblk = 0;
     size_t off_cnt, off_cursor, off_head, off_qoff, off_item, off_nch, off_qblk, off_itab, off_qlist, off_qt, off_qn,
         off_partial, off_qbound, off_pqn, off_pe, off_qe, off_live, off_wrec, total;
@@ -2626,10 +2646,12 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     pl.K2 = 32 * pl.rl;
     // the wide screen (LIRA_OPT_WIDE): the hi x hi form at 256 rows per item where its
     // shape applies; it needs the per-query seeded bound (not PER_PARTITION)
+    // (both need the per-query seeded bound: not PER_PARTITION, LIRA_OPT_SEED on)
     pl.wide = op.wide && pl.split == 3 && !pl.v2 && pl.rl == 1 && idx->xadjc && idx->tstat && idx->lstat &&
-              wscreen_shape_ok(idx->dpad) && !(flags & LIRA_SCAN_PER_PARTITION);
-    if (pl.wide) pl.qr = 256;
-    pl.smem = pl.wide ? wscreen_smem() : pl.v2 ? (pl.qr == 128 ? (pl.ns == 4 ? SSmem2<128, 1, 4, 16>::total : SSmem2<128, 1, 3, 32>::total)
+              (op.wide == 2 ? vscreen_shape_ok(idx->dpad) : wscreen_shape_ok(idx->dpad)) && op.seed &&
+              !(flags & LIRA_SCAN_PER_PARTITION) ? op.wide : 0;
+    if (pl.wide) pl.qr = pl.wide == 2 ? 64 : 256;
+    pl.smem = pl.wide == 2 ? vscreen_smem() : pl.wide ? wscreen_smem() : pl.v2 ? (pl.qr == 128 ? (pl.ns == 4 ? SSmem2<128, 1, 4, 16>::total : SSmem2<128, 1, 3, 32>::total)
                                      : pl.rl == 1 ? (pl.ns == 4 ? SSmem2<64, 1, 4, 32>::total : SSmem2<64, 1, 2, 32>::total)
                                      : pl.rl == 2 ? SSmem2<64, 2, 4, 32>::total : SSmem2<64, 4, 3, 32>::total)
               : !pl.mfma       ? screen_smem(pl.qr, pl.rl)
@@ -2648,7 +2670,8 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // ~8 items per workgroup: fewer item prologues/epilogues and row lists to
     // merge than k_scan's 16 (measured: SIFT1M scan + merge 1.47 -> 1.22 ms on
     // the mixture, 4.80 -> 4.66 ms on latent data; 4 and 32 slower overall)
-    const int rounds = op.rounds > 0 ? op.rounds : pl.wide ? 4 : 8;
+    // (k_screen_v: a workgroup is 4 independent waves, each its own item)
+    const int rounds = op.rounds > 0 ? op.rounds : pl.wide == 2 ? 16 : pl.wide ? 4 : 8;
     const int64_t target = (int64_t)rounds * pl.grid;
     // (LIRA_OPT_PROBES_HINT: the probe lists are mostly -1 padding, e.g. a
     // threshold selection padded to B; size the chunking for the expected pairs)
@@ -2679,8 +2702,9 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
         pl.bpc = std::min(pl.bpc, SSmem<64, 1, true>::kBR);
         pl.bpc_near = std::min(pl.bpc_near, pl.bpc);
     }
-    if (pl.wide) {  // k_screen_w holds <= 128 blocks of 128 candidates per item in registers
-        pl.bpc = std::min(pl.bpc, 64);
+    if (pl.wide) {  // k_screen_w holds <= 128 blocks of 128 candidates per item in registers,
+                    // k_screen_v <= 128 tiles
+        pl.bpc = std::min(pl.bpc, pl.wide == 2 ? vscreen_max_tiles() / kSBT : 64);
         pl.bpc_near = std::min(pl.bpc_near, pl.bpc);
     }
     if (pl.v2 && idx->metric == LIRA_METRIC_L2 && idx->pivot) {  // k_screen_s stages <= kBR block ranges per item
@@ -2733,7 +2757,8 @@ size_t screen_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, 
 // the kernel a screened scan of this shape runs (lira_scan_describe)
 std::string screen_describe(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, unsigned flags) {
     SPlan pl = make_splan(idx, nq, nprobe, k, flags);
-    std::string s = pl.wide ? "k_screen_w hi-x hi-q bf16 v_mfma_f32_32x32x16_bf16"
+    std::string s = pl.wide == 2 ? "k_screen_v hi-x hi-q bf16 v_mfma_f32_16x16x32_bf16"
+                    : pl.wide ? "k_screen_w hi-x hi-q bf16 v_mfma_f32_32x32x16_bf16"
                     : pl.v2 ? "k_screen_s split-bf16 v_mfma_f32_16x16x32_bf16 NS=" + std::to_string(pl.ns) +
                                 " BC=" + std::to_string(pl.bc)
                     : pl.mfma ? (pl.split == 3 ? "k_screen_m hi-x hi-q bf16 v_mfma_f32_16x16x32_bf16"
@@ -3019,7 +3044,11 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     a.bpc_near = groups == 2 ? pl.bpc_near : pl.bpc;
     a.nch_max = pl.nch_max;
     a.stats = idx->stats_on ? (unsigned long long *)idx->stats : nullptr;
-    hipError_t e = pl.wide ? launch_wscreen(idx, q, cnt, qoff, qlist, itab, head, QN, QE, partial, pE, qbound,
+    hipError_t e = pl.wide == 2 ? launch_vscreen(idx, q, cnt, qoff, qlist, itab, head, QN, QE, partial, pE, qbound,
+                                                 (int)nprobe, (int)k, pl.bpc, a.bpc_near, pl.nch_max, nvirt, tri ? 1 : 0,
+                                                 pl.grid, (int4 *)(w + pl.off_wrec),
+                                                 (int64_t)(pl.max_qblk + 1) * pl.nch_max, st)
+                   : pl.wide ? launch_wscreen(idx, q, cnt, qoff, qlist, itab, head, QN, QE, partial, pE, qbound,
                                             (int)nprobe, (int)k, pl.bpc, a.bpc_near, pl.nch_max, nvirt, tri ? 1 : 0,
                                             pl.grid, (int4 *)(w + pl.off_wrec),
                                             (int64_t)(pl.max_qblk + 1) * pl.nch_max, st)
@@ -3061,6 +3090,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     m.per_partition = per_part ? 1 : 0;
     m.stats = a.stats;
     m.split = pl.split;
+    m.unsorted = pl.wide == 2 ? 1 : 0;
     if (idx->metric == LIRA_METRIC_L2)
         launch_smerge<LIRA_METRIC_L2>(Rm, m, st);
     else

@@ -154,7 +154,11 @@ class PartitionedIndex:
         return max(1, int(distinct.sum(1).max())) if rows.numel() else 1
 
     def list_ids(self, b: int) -> np.ndarray:
-        """Row ids of bucket b in list order (search.cpp's sorted bucket_ids[b])."""
+        """Row ids of bucket b in STORAGE order (the set of search.cpp's bucket_ids[b]).
+
+        With option order=1 (the L2 default) a list's rows are stored by ascending
+        distance to its pivot, so this is a permutation of search.cpp's sorted list;
+        compare as sets.  Search results never depend on the storage order."""
         out = np.empty(int(self.list_sizes[b]), dtype=np.int32)
         with torch.cuda.device(self.device):
             _lib.call("lira_index_list_ids", self._h, int(b), out.ctypes.data_as(ctypes.c_void_p),

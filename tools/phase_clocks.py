@@ -1,7 +1,10 @@
 """Per-phase cycle split of the screen kernel (LIRA_OPT_DEBUG bit 8: thread 0 of
 every workgroup adds clock64() deltas: item prologue -> stats[1], block loop ->
 stats[3], epilogue -> stats[6]).  Timing experiment only (debug bits 1/2/4 also
-switch off MFMA / selection / staging; results invalid).
+switch off MFMA / selection / staging; results invalid).  Needs a debug build
+(production libraries refuse LIRA_OPT_DEBUG != 0):
+  VARIANT_FLAGS=-DLIRA_PHASE_CLOCKS tools/build_variant.sh lira_screen.hip \
+      lira-ann-search_amd/csrc/lira_screen.hip clk && LIRA_HIP_LIB=variants/clk.so python tools/phase_clocks.py ...
 
 usage: python tools/phase_clocks.py <config> <data> <debug bits> [option=value ...]
 """
