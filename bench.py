@@ -36,6 +36,7 @@ import torch  # noqa: E402
 # peaks (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0          # HBM3E spec
 L2LDS_PEAK_GBS = 18800.0       # LDS-DMA gather into LDS from the XCD L2, chip-wide (upper end, measured)
+L2_PEAK_GBS = 34500.0          # L2 read bandwidth, chip-wide (MI355X_MICROARCH.md, L2 per XCD)
 MFMA_F32_PEAK_TFLOPS = 157.3   # v_mfma_f32_*_f32 dense = fp32 vector peak
 MFMA_BF16_PEAK_TFLOPS = 2516.6  # dense bf16 MFMA, 16 x the f32 rate
 VALU_F32_PEAK_TOPS = 78.64     # non-FMA fp32 lane ops/s (157.3 TFLOP/s counts an FMA as 2)
@@ -67,6 +68,9 @@ def parse():
                     help="name=v1,v2,...: after the timed run, re-time the step with each value of an index "
                          "option (include/lira_hip.h LIRA_OPT_*) on the same index and batch (rank 0, N=1)")
     ap.add_argument("--no-exact", action="store_true", help="skip the all-exact kernel comparison")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="1 (default): the step's rank + search launches replayed as one captured HIP graph "
+                         "(hipGraph via torch.cuda.CUDAGraph; collectives stay outside); 0: launched one by one")
     ap.add_argument("--no-pipeline", action="store_true", help="skip the MLP-probed pipeline timing")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo only to rehearse N>1 on one GPU")
@@ -203,8 +207,24 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
         rank_nearest(q, centres, nprobe, out=probe, workspace=ws)
         index.search(q, probe, k, dedup=True, out=(D, I, ncand), fma=args.fma)
 
+    # the step's ~10 launches as one HIP graph: no per-launch host overhead or
+    # gaps between kernels (the library's calls are capture-safe: workspaces
+    # are allocated by the warm-up calls, no host syncs on the search path)
+    graph = None
+    if args.graph:
+        for _ in range(2):
+            local_step()
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            local_step()
+        torch.cuda.synchronize()
+
     def step():
-        local_step()
+        if graph is not None:
+            graph.replay()
+        else:
+            local_step()
         if world > 1:  # the per-rank top-k of the batch, to every rank (RCCL all-gather)
             if args.scaling == "strong":
                 all_gather_rows(D.to(gdev), nq_job, world)
@@ -217,7 +237,8 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
         step()
     torch.cuda.synchronize()
     index.check()
-    index.set_profiling(True)
+    if graph is None:
+        index.set_profiling(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -228,6 +249,11 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
+    if graph is not None:  # per-phase kernel times: the same step launched one by one, untimed
+        index.set_profiling(True)
+        for _ in range(args.steps):
+            local_step()
+        torch.cuda.synchronize()
     prof = index.profile_read()
     index.set_profiling(False)
     if world > 1:
@@ -239,6 +265,7 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
     nq_all = nq_job if args.scaling == "strong" else nq_job * world
     out = {"data": data, "value": nq_all * args.steps / elapsed, "unit": "queries/s",
            "ms_per_step": elapsed / args.steps * 1e3, "queries_per_rank": nq, "kernel": kernel,
+           "launch": "hip_graph" if graph is not None else "stream",
            "index_bytes": index.memory_bytes(), "n_mul": n_mul, "index_options": opts,
            "kernels_ms_per_step": {"plan": plan_ms, "scan": scan_ms, "merge": merge_ms}}
     if rank != 0:
@@ -275,7 +302,8 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
     hh = "hi-q" in kernel  # hi x hi: 1 product per dim (qh x xh), hi parts of x and q staged
     split = "split-bf16" in kernel or hh
     hix = "hi-x" in kernel  # hi-only x: 2 products per dim (qh, ql) x xh, half the X bytes
-    if kernel.startswith("k_screen_m"):
+    kname = kernel.split()[0]
+    if kname in ("k_screen_m", "k_screen_w", "k_screen_v"):
         # (row, cand) pairs x dpad x products x 2
         flops = work["chunks_computed"] * dpad * (2 if hh else 4 if hix else 8 if split else 2)
         mfma_peak = MFMA_BF16_PEAK_TFLOPS if split else MFMA_F32_PEAK_TFLOPS
@@ -283,8 +311,22 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
     else:
         flops = work["chunks_computed"] * dpad * 2
         mfma_peak, mfma_what = MFMA_F32_PEAK_TFLOPS, "fp32 VALU (v_pk_fma_f32)"
-    # L2 -> LDS bytes (LDS-DMA) per launch: X (256 candidates), Q (qr rows), xadj
-    staged = work["blocks"] * (256 * dpad * (2 if hix else 4) + qr * dpad * (2 if hh else 4) + 1024)
+    if kname == "k_screen_v":
+        # L2 -> VGPR bytes per launch: per tile (64 candidates) their hi parts + xadj
+        # (the work counter "blocks" counts tiles here)
+        staged = work["blocks"] * (64 * dpad * 2 + 256)
+        st_name, st_peak = "l2_regs", L2_PEAK_GBS
+        st_what = "bytes loaded L2/MALL -> VGPRs (x hi parts + xadj per tile; queries stay in registers)"
+    elif kname == "k_screen_w":
+        # per block (128 candidates): their hi parts + xadj; queries stay in registers
+        staged = work["blocks"] * (128 * dpad * 2 + 512)
+        st_name, st_peak = "l2_lds", L2LDS_PEAK_GBS
+        st_what = "bytes staged L2/MALL -> LDS by LDS-DMA (x hi parts + xadj per block)"
+    else:
+        # L2 -> LDS bytes (LDS-DMA) per launch: X (256 candidates), Q (qr rows), xadj
+        staged = work["blocks"] * (256 * dpad * (2 if hix else 4) + qr * dpad * (2 if hh else 4) + 1024)
+        st_name, st_peak = "l2_lds", L2LDS_PEAK_GBS
+        st_what = "bytes staged L2/MALL -> LDS by LDS-DMA (tiles + query chunk + xadj per computed block)"
     traffic, pmc_src = None, None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_scan_{args.config}_{data}.json")
     if os.path.exists(pmc_path):
@@ -299,9 +341,8 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
         "mfma": {"achieved": flops / sec / 1e12, "peak": mfma_peak, "unit": "TFLOP/s",
                  "what": f"executed {mfma_what} flops of the screen (work counters x dpad x products)",
                  "flops_per_launch": flops},
-        "l2_lds": {"achieved": staged / sec / 1e9, "peak": L2LDS_PEAK_GBS, "unit": "GB/s",
-                   "what": "bytes staged L2/MALL -> LDS by LDS-DMA (tiles + query chunk + xadj per computed block)",
-                   "bytes_per_launch": staged},
+        st_name: {"achieved": staged / sec / 1e9, "peak": st_peak, "unit": "GB/s", "what": st_what,
+                  "bytes_per_launch": staged},
     }
     if traffic:
         cands["hbm"] = {"achieved": traffic / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -98,4 +98,79 @@ __device__ __forceinline__ float row_h(double lim, double qn, double qnorm, doub
 }
 
 
+
+// ---- per-pair records + the partition filter (k_pairs, k_seed_t<..., PAIRS>) ----
+// 16 lanes per (query, slot) pair (sub = lane & 15; all 16 call it), double sums:
+// qn = fl(||q'||^2), qnorm >= ||q'||, q' = fl(q - c) of the pair's list pivot c
+// (centred) or q; dq = fl(||q - c||) (triangle skip); qres >= ||q' - hi(q')||
+// (hi x hi bound); QH (optional): hi(q') as bf16, dpad dims, zero past d (the
+// rows' A fragments of k_screen_m / k_screen_v, gathered per pair).
+// Filter (lstat, qb = f2ord of the query's seed bound T): a pair whose list
+// lies wholly outside the query's triangle interval under T (k exact
+// candidates of its slot-0 list score <= T) cannot hold a top-k candidate, so
+// it gets probe_live = -1 and no work item (the test is k_screen_m's per-block
+// skip over the list's radius range).  Slot 0 (the seed's own list) stays.
+__device__ __forceinline__ void pair_record(const float *Q, int64_t d, int64_t pair, bool valid, int praw,
+                                            int nprobe, int n_lists, const float *pivot, int centred,
+                                            const float2 *lstat, uint32_t qb, int32_t *probe_live, float4 *QN,
+                                            float *QE, float *pqn, uint16_t *QH, int64_t dpad) {
+    const int sub = threadIdx.x & 15;
+    const int p = praw < n_lists ? praw : -1;  // (an id >= n_lists passes through: k_count reports it)
+    const int64_t q = valid ? pair / nprobe : 0;
+    double s = 0.0, t = 0.0, e = 0.0;
+    if (p >= 0 && (QN || lstat)) {
+        const float *qr = Q + q * d, *pv = pivot ? pivot + (int64_t)p * d : nullptr;
+        uint16_t *qh = QH ? QH + pair * dpad : nullptr;
+        // (unrolled: 8 iterations' loads in flight together -- a dependent load per
+        // iteration made the fused seed + pairs kernel latency-bound)
+#pragma unroll 8
+        for (int64_t j = sub; j < d; j += 16) {
+            const float x = qr[j], cv = pv ? pv[j] : 0.0f;
+            const float sv = centred && pv ? x - cv : x;
+            if (qh) qh[j] = (uint16_t)bf16_rne_sat(sv);
+            const double xc = (double)sv;
+            s = __builtin_fma(xc, xc, s);
+            if (QE) {
+                const double rr = (double)(sv - __uint_as_float(bf16_rne_sat(sv) << 16));
+                e = __builtin_fma(rr, rr, e);
+            }
+            if (pv) {
+                const double df = (double)x - (double)cv;
+                t = __builtin_fma(df, df, t);
+            }
+        }
+        if (qh)
+            for (int64_t j = d + sub; j < dpad; j += 16) qh[j] = 0;
+    }
+#pragma unroll
+    for (int m = 8; m >= 1; m >>= 1) {  // within the 16-lane DPP row
+        s += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, s), m));
+        t += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, t), m));
+        e += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, e), m));
+    }
+    if (sub != 0 || !valid) return;
+    int live = p;
+    const float dq = (float)__builtin_sqrt(t);
+    if (p >= 0 && lstat && (int)(pair % nprobe) >= 1) {
+        const double dd = (double)d, F = 1.0 - (dd + 4.0) * kU;
+        if (qb != ~0u && F > 0.5) {
+            const double T = (double)ord2f(qb);
+            if (T < 1e300) {
+                const double rad = __builtin_sqrt((fmax(T, 0.0) + dd * 0x1p-140) / F) * (1.0 + 0x1p-40);
+                double A = (double)dq * (1.0 - 0x1p-22) - rad, B = (double)dq * (1.0 + 0x1p-22) + rad;
+                A -= __builtin_fabs(A) * 0x1p-50;
+                B += __builtin_fabs(B) * 0x1p-50;
+                const float2 ls = lstat[p];
+                if (ls.y < __double2float_rd(A) || ls.x > __double2float_ru(B)) live = -1;
+            }
+        }
+    }
+    probe_live[pair] = praw >= n_lists ? praw : live;
+    if (live < 0) return;
+    const float qnu = __double2float_ru(__builtin_sqrt(s) * (1.0 + 0x1p-40));
+    if (QN) QN[pair] = make_float4((float)s, qnu, __int_as_float((int)pair), dq);
+    if (QE) QE[pair] = __double2float_ru(__builtin_sqrt(e) * (1.0 + 0x1p-40));
+    if (pqn) pqn[pair] = qnu;
+}
+
 }  // namespace lira

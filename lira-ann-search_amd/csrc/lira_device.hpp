@@ -278,6 +278,21 @@ __device__ __forceinline__ uint32_t bf16_split_part(float v, int hl) {
     return hl ? bf16_rne_sat(v - __uint_as_float(hi << 16)) : hi;
 }
 
+// 64 u32 values, one per lane: ascending bitonic sort.
+__device__ __forceinline__ uint32_t wave_sort64_u32(uint32_t v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            const uint32_t o = xor_u32(v, stride);
+            const bool lower = (lane & stride) == 0, asc = (lane & size) == 0;
+            v = (lower == asc) ? min(v, o) : max(v, o);
+        }
+    }
+    return v;
+}
+
 __device__ __forceinline__ int popc64(u64 m) { return __popcll(m); }
 // number of set bits of m in lanes below this lane
 __device__ __forceinline__ int mbcnt64(u64 m) {

@@ -172,11 +172,6 @@ __global__ __launch_bounds__(256) void k_centroid_gemm(const float *__restrict__
     const float ebound = 8.0f * (float)(d + 8) * 5.9604645e-08f;
     const int col = lane & 31;
     const int cb = c0 + wc * 32 + col;
-    // the bound grows with ||c||^2: one atomic per query row with the wave's
-    // largest in-range column norm (not one per element)
-    float mx = cb < nb ? nrm[64 + wc * 32 + col] : 0.0f;
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
@@ -184,8 +179,20 @@ __global__ __launch_bounds__(256) void k_centroid_gemm(const float *__restrict__
         float nq_ = nrm[wr * 32 + row], nc_ = nrm[64 + wc * 32 + col];
         float v = (nq_ + nc_) - 2.0f * acc[r];
         if (qr < nq && cb < nb) out_sq[qr * nb + cb] = v;
-        if (out_err && col == 0 && qr < nq)
-            atomicMax((unsigned int *)&out_err[qr], __float_as_uint(ebound * (nq_ + mx) + 1e-30f));
+    }
+    // the bound grows with ||c||^2: per query row, with the block's largest
+    // in-range centroid norm; one column block (nb <= 64) stores it, several
+    // take the max over blocks (the caller zeroed out_err)
+    if (out_err && w == 0) {
+        float mx = c0 + lane < nb ? nrm[64 + lane] : 0.0f;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+        const int64_t qr = q0 + lane;
+        if (qr < nq) {
+            const float e = ebound * (nrm[lane] + mx) + 1e-30f;
+            if (gridDim.y == 1) out_err[qr] = e;
+            else atomicMax((unsigned int *)&out_err[qr], __float_as_uint(e));
+        }
     }
 }
 
@@ -265,6 +272,71 @@ __global__ __launch_bounds__(256) void k_rank_select(const float *__restrict__ A
         int e = r * 64 + lane;
         if (e < nprobe) out[qi * nprobe + e] = fin[r] == kEmptyKey ? -1 : key_gid(fin[r]);
     }
+}
+
+// nb <= 64 (one centroid per lane): the threshold from a 32-bit sort of the
+// approximate values (no index tie-break is needed for a value), and the exact
+// top-nprobe by counting ranks over the few re-checked lanes (the u64 bitonic
+// sorts of k_rank_select were most of its time: SIFT1M 26 us per 10 k queries)
+__global__ __launch_bounds__(256) void k_rank_select64(const float *__restrict__ A, const float *__restrict__ err,
+                                                       const float *__restrict__ q, int64_t nq,
+                                                       const float *__restrict__ cent, int nb, int64_t d,
+                                                       int nprobe, int32_t *out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t qi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (qi >= nq) return;
+    const bool ok = lane < nb;
+    const float av = ok ? A[qi * nb + lane] : __builtin_inff();
+    const uint32_t sorted = wave_sort64_u32(ok ? f2ord(av) : ~0u);
+    const uint32_t tk = (uint32_t)__shfl((int)sorted, min(nprobe, nb) - 1, 64);
+    const float lim = ord2f(tk) + 2.0f * err[qi] * 1.0001f;
+    const bool cand = ok && av <= lim;
+    u64 key = kEmptyKey;
+    if (cand) {  // search.cpp:220-235's sequential sum
+        const float *qr = q + qi * d, *cr = cent + (int64_t)lane * d;
+        float acc = 0.0f;
+        int64_t j = 0;
+        if ((((uintptr_t)cr | (uintptr_t)qr) & 15) == 0) {
+            for (; j + 16 <= d; j += 16) {
+                float4 cv[4], qv[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    cv[e] = *(const float4 *)(cr + j + 4 * e);
+                    qv[e] = *(const float4 *)(qr + j + 4 * e);
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float df = qv[e].x - cv[e].x;
+                    acc = acc + df * df;
+                    df = qv[e].y - cv[e].y;
+                    acc = acc + df * df;
+                    df = qv[e].z - cv[e].z;
+                    acc = acc + df * df;
+                    df = qv[e].w - cv[e].w;
+                    acc = acc + df * df;
+                }
+            }
+        }
+        for (; j < d; ++j) {
+            const float df = qr[j] - cr[j];
+            acc = acc + df * df;
+        }
+        key = make_key(__fsqrt_rn(acc), lane);
+    }
+    // rank of my key among the candidates' (keys are distinct: the index breaks ties)
+    u64 cm = __ballot(cand);
+    const int ncand = __popcll(cm);
+    int rank = 0;
+    while (cm) {
+        const int j = __builtin_ctzll(cm);
+        cm &= cm - 1;
+        const u64 kj = ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(key >> 32), j) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key, j);
+        rank += kj < key;
+    }
+    int32_t *o = out + qi * nprobe;
+    if (cand && rank < nprobe) o[rank] = lane;
+    for (int e = ncand + lane; e < nprobe; e += 64) o[e] = -1;
 }
 
 // -------------------------------------------------------------- probe select
@@ -431,7 +503,7 @@ int lira_centroid_gemm(const float *q, int64_t nq, const float *centroids, int64
     if (nq == 0) return LIRA_OK;
     if (!q || !centroids || !out_sq) return fail(LIRA_EINVAL, "NULL buffer");
     hipStream_t st = (hipStream_t)stream;
-    if (out_err) LIRA_HIP_TRY(hipMemsetAsync(out_err, 0, nq * 4, st));
+    if (out_err && n_centroids > 64) LIRA_HIP_TRY(hipMemsetAsync(out_err, 0, nq * 4, st));  // (max over column blocks)
     dim3 grid((unsigned)((nq + 63) / 64), (unsigned)((n_centroids + 63) / 64));
     if (d % 4 == 0 && ((uintptr_t)q & 15) == 0 && ((uintptr_t)centroids & 15) == 0)
         hipLaunchKernelGGL(k_centroid_gemm<true>, grid, dim3(256), 0, st, q, nq, centroids,
@@ -473,7 +545,10 @@ int lira_rank_nearest(const float *q, int64_t nq, const float *centroids, int64_
     int rc = lira_centroid_gemm(q, nq, centroids, n_centroids, d, A, err, stream);
     if (rc == LIRA_OK) {
         dim3 g((unsigned)((nq + 3) / 4));
-        if (R == 1)
+        if (n_centroids <= 64)
+            hipLaunchKernelGGL(k_rank_select64, g, dim3(256), 0, st, A, err, q, nq, centroids, (int)n_centroids, d,
+                               (int)nprobe, out_probe);
+        else if (R == 1)
             hipLaunchKernelGGL(k_rank_select<1>, g, dim3(256), 0, st, A, err, q, nq, centroids,
                                (int)n_centroids, d, (int)nprobe, out_probe);
         else if (R == 2)

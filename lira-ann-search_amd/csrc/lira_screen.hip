@@ -58,7 +58,8 @@ bool wscreen_shape_ok(int64_t dpad);
 int wscreen_smem();
 hipError_t launch_pairs(const float *Q, int64_t d, const int32_t *probe, int64_t npairs, int nprobe, int n_lists,
                         const float *pivot, int centred, const float2 *lstat, const uint32_t *qbound,
-                        int32_t *probe_live, float4 *QN, float *QE, float *pqn, hipStream_t st);
+                        int32_t *probe_live, float4 *QN, float *QE, float *pqn, uint16_t *QH, int64_t dpad,
+                        hipStream_t st);
 hipError_t launch_wscreen(const lira_index *idx, const float *q, const int32_t *cnt, const int32_t *qoff,
                           const int32_t *qlist, const int4 *itab, int32_t *head, const float4 *QN, const float *QE,
                           u64 *partial, float *pE, uint32_t *qbound, int nprobe, int k, int bpc, int bpc_near,
@@ -68,10 +69,13 @@ hipError_t launch_wscreen(const lira_index *idx, const float *q, const int32_t *
 bool vscreen_shape_ok(int64_t dpad);
 int vscreen_smem();
 int vscreen_max_tiles();
+int vscreen_rows();
+int vscreen_workers_per_cu();
 hipError_t launch_vscreen(const lira_index *idx, const float *q, const int32_t *cnt, const int32_t *qoff,
                           const int32_t *qlist, const int4 *itab, int32_t *head, const float4 *QN, const float *QE,
-                          u64 *partial, float *pE, uint32_t *qbound, int nprobe, int k, int bpc, int bpc_near,
-                          int nch_max, int n_virt, int tri, int grid, int4 *vrec, int64_t max_items, hipStream_t st);
+                          const uint16_t *QH, u64 *partial, float *pE, uint32_t *qbound, int nprobe, int k, int bpc,
+                          int bpc_near, int nch_max, int n_virt, int tri, int grid, int4 *vrec, int64_t max_items,
+                          hipStream_t st);
 
 hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npairs, int nprobe, int bpc,
                        int bpc_near,
@@ -93,6 +97,12 @@ struct ScreenArgs {
     const float *rmax;     // [n_lists]
     const int32_t *tile_off, *cnt, *item_off, *qblk_off;
     const int4 *itab;  // item -> (virtual partition, query block, chunk, global query block)
+    // per-pair query records (k_screen_m<..., 3>, qpair = 1): a row's pair is
+    // qlist[qoff[vp] + qb QR + row], its QN / QE are indexed by pair, and its hi
+    // parts are gathered from QH[pair][dpad] (no k_qstage copy)
+    const int32_t *qoff, *qlist;
+    const uint16_t *QH;
+    int qpair;
     int32_t *head;
     const float *QT;       // [qblk][dpad][QR]
     const float4 *QN;      // [qblk*QR]: qn, |q| (up), pair (int bits), 0
@@ -395,20 +405,6 @@ __device__ __forceinline__ float from_row_lane(float v, int reg, int g) {
     return g == 0 ? a0 : g == 1 ? a1 : g == 2 ? a2 : a3;
 }
 
-// 64 u32 values, one per lane: ascending bitonic sort.
-__device__ __forceinline__ uint32_t wave_sort64_u32(uint32_t v) {
-    const int lane = lane_id();
-#pragma unroll
-    for (int size = 2; size <= 64; size <<= 1) {
-#pragma unroll
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            const uint32_t o = xor_u32(v, stride);
-            const bool lower = (lane & stride) == 0, asc = (lane & size) == 0;
-            v = (lower == asc) ? min(v, o) : max(v, o);
-        }
-    }
-    return v;
-}
 
 // Merge a row's survivor buffer (n keys) into its sorted K2-list.  Both halves
 // run the half-wave network on the same row; half 0 stores.
@@ -920,8 +916,15 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
         const int p = vp >= a.n_lists ? vp - a.n_lists : vp;
         const int ch = __builtin_amdgcn_readfirstlane(meta[3]);
         const int gqb = __builtin_amdgcn_readfirstlane(meta[4]);
+        const bool QP = SPLIT == 3 && a.qpair;  // per-pair records (uniform)
         if (tid < QR) {
-            m_pair[tid] = __float_as_int(a.QN[(int64_t)gqb * QR + tid].z);
+            if (QP) {
+                const int qb = __builtin_amdgcn_readfirstlane(meta[2]);
+                const int nval = a.cnt[vp] - qb * QR;
+                m_pair[tid] = tid < nval ? a.qlist[a.qoff[vp] + qb * QR + tid] : -1;
+            } else {
+                m_pair[tid] = __float_as_int(a.QN[(int64_t)gqb * QR + tid].z);
+            }
             m_bufc[tid] = 0;
         }
         for (int i = tid; i < QR * K2; i += NT) lists[i] = kEmptyKey;
@@ -936,11 +939,17 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
 
         // lanes 0..15 of wave w hold row 16w + lane's threshold state
         const int my_row = wave * 16 + cj;
-        const float4 qrec = a.QN[(int64_t)gqb * QR + my_row];
+        const int qp_row = QP ? m_pair[my_row] : -1;
+        const float4 qrec = QP ? (qp_row >= 0 ? a.QN[qp_row] : make_float4(0.0f, 0.0f, __int_as_float(-1), 0.0f))
+                               : a.QN[(int64_t)gqb * QR + my_row];
         const int my_pair = __float_as_int(qrec.z);
         const int my_q = my_pair >= 0 ? my_pair / a.nprobe : -1;
         const double my_qn = (double)qrec.x, my_qnorm = (double)qrec.y;
-        const double my_qres = SPLIT == 3 ? (double)a.QE[(int64_t)gqb * QR + my_row] : 0.0;
+        const double my_qres = SPLIT == 3 ? (double)(QP ? (qp_row >= 0 ? a.QE[qp_row] : 0.0f)
+                                                        : a.QE[(int64_t)gqb * QR + my_row])
+                                          : 0.0;
+        // (QP) this lane's row (lane = row of the staged Q piece): its pair's hi parts in QH
+        const int qh_row = QP ? max(m_pair[lane], 0) * (int)a.dpad : 0;
         const double my_E = err_E<METRIC>(my_qnorm, R, dd, ESPLIT, (double)a.dpad, a.centred, -1.0, my_qres);
         u64 *my_list = lists + my_row * K2;
         // this lane's 4 output rows 4g + reg: qn for the screened scores
@@ -969,9 +978,15 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
             }
             // Q: QR/16 pieces of 1 KiB, one per wave (SPLIT 3: the hi parts,
             // chunk half wave >> 1, quarter wave & 1; QR = 64)
+            // (QP: gathered per row from QH -- dims jc + 16 (wave >> 1) + 8 (wave & 1) .. + 7
+            // of row lane -- into the same LDS image)
             const int qsrc = SPLIT == 3 ? (wave >> 1) * (kSDK * QR / 4) + (wave & 1) * 64 : wave * 64;
-            LIRA_SGLDS(qtg + (int64_t)jc * (QR / 4) + qsrc + lane,
-                    __builtin_amdgcn_readfirstlane(base + (uint32_t)S::kXS + (uint32_t)wave * 1024u));
+            if (QP)
+                LIRA_SGLDS(a.QH + qh_row + jc + 16 * (wave >> 1) + 8 * (wave & 1),
+                           __builtin_amdgcn_readfirstlane(base + (uint32_t)S::kXS + (uint32_t)wave * 1024u));
+            else
+                LIRA_SGLDS(qtg + (int64_t)jc * (QR / 4) + qsrc + lane,
+                           __builtin_amdgcn_readfirstlane(base + (uint32_t)S::kXS + (uint32_t)wave * 1024u));
             if (jc == 0 && wave == 0) {  // the block's xadj rides along (tiles past its end: masked on read)
                 LIRA_SGLDS(a.xadj + (int64_t)(tile0 + tb + min(lane >> 4, ntv - 1)) * kTile + (lane & 15) * 4,
                            __builtin_amdgcn_readfirstlane(xs_lds + (uint32_t)(NSL * S::kStage + xpar * 1024)));
@@ -2196,17 +2211,17 @@ __global__ __launch_bounds__(256) void k_seed_b(const float *Q, int64_t d, int n
 // query, lane = candidate: each dim of a tile is one coalesced 256-B row).
 // NT tiles: 2 for k <= 32 (measured SIFT1M mixture: plan 0.217 -> 0.164 ms,
 // scan +0.02 ms), else NT.
-template <int METRIC, int NT = kSeedTiles>
-__global__ __launch_bounds__(256) void k_seed_t(const float *Q, const int32_t *probe, int nprobe, int n_lists,
-                                                const int32_t *tile_off, const int32_t *ids, const float *X,
-                                                int64_t d, int64_t dpad, int64_t nq, int k, uint32_t *qbound) {
+// the seed bound of query q (wave-uniform; +inf: none): k exact candidates of
+// its slot-0 list, the first NT tiles, score <= the returned value
+template <int METRIC, int NT>
+__device__ __forceinline__ float seed_bound(const float *Q, const int32_t *probe, int nprobe, int n_lists,
+                                           const int32_t *tile_off, const int32_t *ids, const float *X, int64_t d,
+                                           int64_t dpad, int64_t q, int k) {
     const int lane = threadIdx.x & 63;
-    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (q >= nq) return;
     const int p = probe[q * nprobe];
-    if (p < 0 || p >= n_lists) return;
+    if (p < 0 || p >= n_lists) return __builtin_inff();
     const int tile0 = tile_off[p], nt = min(NT, tile_off[p + 1] - tile0);
-    if (nt <= 0) return;
+    if (nt <= 0) return __builtin_inff();
     const float *qrow = Q + q * d;
     const float *xt[NT];
 #pragma unroll
@@ -2271,12 +2286,50 @@ __global__ __launch_bounds__(256) void k_seed_t(const float *Q, const int32_t *p
         }
     }
     const int t = (k + 63) / 64;
-    if (t > 4) return;
+    if (t > 4) return __builtin_inff();
     const float mine = t == 1 ? m[0] : t == 2 ? m[1] : t == 3 ? m[2] : m[3];
     const uint32_t sorted = wave_sort64_u32(f2ord(mine));
     const int j = (k + t - 1) / t;
-    const float B = ord2f((uint32_t)__shfl((int)sorted, j - 1, 64));
-    if (lane == 0 && B < __builtin_inff()) qbound[q] = f2ord(B);
+    return ord2f((uint32_t)__shfl((int)sorted, j - 1, 64));
+}
+
+// PAIRS: the query's per-pair records and partition filter (pair_record, as
+// k_pairs) right after its seed, with the seed bound from registers -- one
+// launch and one read of the query row fewer; qbound is then written for
+// every query (~0: no bound), so the caller needs no fill.
+struct SeedPairs {
+    const float *pivot;
+    int centred;
+    const float2 *lstat;
+    int32_t *probe_live;
+    float4 *QN;
+    float *QE;
+    float *pqn;
+    uint16_t *QH;
+};
+template <int METRIC, int NT = kSeedTiles, bool PAIRS = false>
+__global__ __launch_bounds__(256) void k_seed_t(const float *Q, const int32_t *probe, int nprobe, int n_lists,
+                                                const int32_t *tile_off, const int32_t *ids, const float *X,
+                                                int64_t d, int64_t dpad, int64_t nq, int k, uint32_t *qbound,
+                                                SeedPairs sp) {
+    const int lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    const float B = seed_bound<METRIC, NT>(Q, probe, nprobe, n_lists, tile_off, ids, X, d, dpad, q, k);
+    const uint32_t qb = B < __builtin_inff() ? f2ord(B) : ~0u;
+    if (PAIRS) {
+        if (lane == 0) qbound[q] = qb;
+        for (int s0 = 0; s0 < nprobe; s0 += 4) {
+            const int slot = s0 + (lane >> 4);
+            const bool valid = slot < nprobe;
+            const int64_t pair = q * nprobe + (valid ? slot : 0);
+            const int praw = valid ? probe[pair] : -1;
+            pair_record(Q, d, pair, valid, praw, nprobe, n_lists, sp.pivot, sp.centred, sp.lstat, qb, sp.probe_live,
+                        sp.QN, sp.QE, sp.pqn, sp.QH, dpad);
+        }
+    } else if (lane == 0 && qb != ~0u) {
+        qbound[q] = qb;
+    }
 }
 
 // One workgroup per query, wave w = tile w of its first probed partition.  The
@@ -2577,6 +2630,8 @@ static int screen_smem(int qr, int rl) {
 struct SPlan {
     int rl = 1, qr = 64, K2 = 32, bpc = 1, bpc_near = 1, nch_max = 1, grid = 1, smem = 0, mfma = 1, split = 0;
     int v2 = 0, ns = 2, bc = 32;  // the pipelined split screen (k_screen_s): ring slots, buffer keys per row
+    int pp = 0;                   // per-pair query records (QN / QE / QH per pair, k_pairs or k_seed_t<.., PAIRS>)
+                                  // instead of k_qstage's per-block copy: the hi x hi k_screen_m and the wide screens
     int wide = 0;                 // 1: the wide screen (lira_wscreen.hip k_screen_w), 256 rows per item;
                                   // 2: the wave-resident screen (lira_vscreen.hip k_screen_v), 64 rows per wave
     int64_t max_qblk = 0;
@@ -2650,7 +2705,8 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     pl.wide = op.wide && pl.split == 3 && !pl.v2 && pl.rl == 1 && idx->xadjc && idx->tstat && idx->lstat &&
               (op.wide == 2 ? vscreen_shape_ok(idx->dpad) : wscreen_shape_ok(idx->dpad)) && op.seed &&
               !(flags & LIRA_SCAN_PER_PARTITION) ? op.wide : 0;
-    if (pl.wide) pl.qr = pl.wide == 2 ? 64 : 256;
+    if (pl.wide) pl.qr = pl.wide == 2 ? vscreen_rows() : 256;
+    pl.pp = pl.wide || (pl.split == 3 && !pl.v2);
     pl.smem = pl.wide == 2 ? vscreen_smem() : pl.wide ? wscreen_smem() : pl.v2 ? (pl.qr == 128 ? (pl.ns == 4 ? SSmem2<128, 1, 4, 16>::total : SSmem2<128, 1, 3, 32>::total)
                                      : pl.rl == 1 ? (pl.ns == 4 ? SSmem2<64, 1, 4, 32>::total : SSmem2<64, 1, 2, 32>::total)
                                      : pl.rl == 2 ? SSmem2<64, 2, 4, 32>::total : SSmem2<64, 4, 3, 32>::total)
@@ -2670,9 +2726,10 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // ~8 items per workgroup: fewer item prologues/epilogues and row lists to
     // merge than k_scan's 16 (measured: SIFT1M scan + merge 1.47 -> 1.22 ms on
     // the mixture, 4.80 -> 4.66 ms on latent data; 4 and 32 slower overall)
-    // (k_screen_v: a workgroup is 4 independent waves, each its own item)
-    const int rounds = op.rounds > 0 ? op.rounds : pl.wide == 2 ? 16 : pl.wide ? 4 : 8;
-    const int64_t target = (int64_t)rounds * pl.grid;
+    // (k_screen_v: every wave is its own worker: CUs x waves per CU of them)
+    const int workers = pl.wide == 2 ? cu_count_s(idx->device) * vscreen_workers_per_cu() : pl.grid;
+    const int rounds = op.rounds > 0 ? op.rounds : pl.wide == 2 ? 4 : pl.wide ? 4 : 8;
+    const int64_t target = (int64_t)rounds * workers;
     // (LIRA_OPT_PROBES_HINT: the probe lists are mostly -1 padding, e.g. a
     // threshold selection padded to B; size the chunking for the expected pairs)
     const int64_t npairs_est = op.probes_hint > 0 ? std::min<int64_t>(npairs, nq * op.probes_hint) : npairs;
@@ -2692,7 +2749,7 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     const int near_rounds = op.near_rounds > 0 ? op.near_rounds : 2;
     {
         const int64_t est0 = std::min<int64_t>(nq, (nq + pl.qr - 1) / pl.qr + idx->n_lists);
-        const int64_t split0 = std::max<int64_t>(1, ((int64_t)near_rounds * pl.grid + est0 - 1) / std::max<int64_t>(1, est0));
+        const int64_t split0 = std::max<int64_t>(1, ((int64_t)near_rounds * workers + est0 - 1) / std::max<int64_t>(1, est0));
         pl.bpc_near = (int)std::min<int64_t>(pl.bpc, std::max<int64_t>(1, (max_blocks + split0 - 1) / split0));
     }
     // k_screen_m stages the radius ranges of an item's first kBR blocks in LDS; a
@@ -2731,9 +2788,10 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     pl.off_wrec = take(pl.wide ? (size_t)(pl.max_qblk + 1) * pl.nch_max * 32 : 0);  // (wide) per-item records
     pl.off_qlist = take((size_t)npairs * 4);
     // (wide: no transposed query copy; QN / QE per pair, from k_pairs)
-    pl.off_qt = take(pl.wide ? 0 : (size_t)pl.max_qblk * pl.qr * idx->dpad * 4);
-    pl.off_qn = take(pl.wide ? (size_t)npairs * 16 : (size_t)pl.max_qblk * pl.qr * 16);
-    pl.off_qe = take(pl.wide ? (size_t)npairs * 4 : (size_t)pl.max_qblk * pl.qr * 4);
+    // (per-pair records: QH, the rows' hi(q - c) per pair, in the QT slot; k_screen_w reads Q itself)
+    pl.off_qt = take(pl.wide == 1 ? 0 : pl.pp ? (size_t)npairs * idx->dpad * 2 : (size_t)pl.max_qblk * pl.qr * idx->dpad * 4);
+    pl.off_qn = take(pl.pp ? (size_t)npairs * 16 : (size_t)pl.max_qblk * pl.qr * 16);
+    pl.off_qe = take(pl.pp ? (size_t)npairs * 4 : (size_t)pl.max_qblk * pl.qr * 4);
     pl.off_live = take((size_t)npairs * 4);
     pl.off_partial = take((size_t)npairs * pl.nch_max * pl.K2 * 8);
     pl.off_qbound = take((size_t)nq * 4);
@@ -2898,7 +2956,6 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
 
     if (ev[0]) LIRA_HIP_TRY(hipEventRecord(ev[0], st));
     LIRA_HIP_TRY(hipMemsetAsync(w, 0, pl.off_qoff, st));  // cnt, cursor, head
-    if (qbound) LIRA_HIP_TRY(hipMemsetAsync(qbound, 0xff, (size_t)nq * 4, st));
     // Two groups (every query's first probe slot -- its nearest partition, where
     // most of its top-k lives -- queued ahead of the rest) when the bound is
     // shared across a query's items: later items then start from tight bounds.
@@ -2926,20 +2983,40 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     // blocks and runs after it, without the filter
     const bool seed_b = qbound && (o.seed == 2 || o.seed == 3) && groups == 2 && k <= 32 && pl.qr == 64 &&
                         idx->d <= 256;
-    if (!seed_b && qbound && o.seed && idx->X) {  // from the fp32 tiles (coalesced)
+    const bool filter = qbound && tri && !seed_b && o.seed && idx->lstat != nullptr;
+    int32_t *plive = filter || pl.pp ? (int32_t *)(w + pl.off_live) : nullptr;
+    uint16_t *QH = pl.pp && pl.wide != 1 ? (uint16_t *)QT : nullptr;
+    // the per-pair records inside the seed kernel where it is k_seed_t (L2, k <= 32)
+    const bool fused = plive && !seed_b && qbound && o.seed && idx->X && idx->metric == LIRA_METRIC_L2 && k <= 32;
+    if (qbound && !fused) LIRA_HIP_TRY(hipMemsetAsync(qbound, 0xff, (size_t)nq * 4, st));
+    if (fused) {
+        SeedPairs sp;
+        sp.pivot = idx->pivot;
+        sp.centred = centred ? 1 : 0;
+        sp.lstat = filter ? idx->lstat : nullptr;
+        sp.probe_live = plive;
+        sp.QN = pl.pp ? QN : nullptr;
+        sp.QE = pl.pp ? QE : nullptr;
+        sp.pqn = pl.pp ? pqn : nullptr;
+        sp.QH = QH;
+        hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2, 2, true>), dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, q,
+                           probe, (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad,
+                           nq, (int)k, qbound, sp);
+        LIRA_HIP_TRY(hipGetLastError());
+    } else if (!seed_b && qbound && o.seed && idx->X) {  // from the fp32 tiles (coalesced)
         const dim3 g((unsigned)((nq + 3) / 4));
         if (idx->metric == LIRA_METRIC_L2 && k <= 32)
             hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2, 2>), g, dim3(256), 0, st, q, probe, (int)nprobe,
-                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound);
+                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound, SeedPairs());
         else if (idx->metric == LIRA_METRIC_L2)
             hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2>), g, dim3(256), 0, st, q, probe, (int)nprobe,
-                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound);
+                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound, SeedPairs());
         else if (k <= 32)
             hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_IP, 2>), g, dim3(256), 0, st, q, probe, (int)nprobe,
-                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound);
+                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound, SeedPairs());
         else
             hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_IP>), g, dim3(256), 0, st, q, probe, (int)nprobe,
-                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound);
+                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound, SeedPairs());
         LIRA_HIP_TRY(hipGetLastError());
     } else if (!seed_b && qbound && o.seed) {  // compact index: from the row-major copy
         if (idx->metric == LIRA_METRIC_L2)
@@ -2952,17 +3029,16 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
                                (int)k, qbound);
         LIRA_HIP_TRY(hipGetLastError());
     }
-    const bool filter = qbound && tri && !seed_b && o.seed && idx->lstat != nullptr;
-    int32_t *plive = filter || pl.wide ? (int32_t *)(w + pl.off_live) : nullptr;
-    if (plive)
+    if (plive && !fused)
         LIRA_HIP_TRY(launch_pairs(q, idx->d, probe, npairs, (int)nprobe, (int)idx->n_lists, idx->pivot,
                                   centred ? 1 : 0, filter ? idx->lstat : nullptr, filter ? qbound : nullptr, plive,
-                                  pl.wide ? QN : nullptr, pl.wide ? QE : nullptr, pl.wide ? pqn : nullptr, st));
+                                  pl.pp ? QN : nullptr, pl.pp ? QE : nullptr, pl.pp ? pqn : nullptr, QH, idx->dpad,
+                                  st));
     const int32_t *pprobe = plive ? plive : probe;  // the pairs that become work
     const int nvirt = groups * (int)idx->n_lists;
     LIRA_HIP_TRY(launch_plan(idx, pprobe, npairs, (int)nprobe, pl.bpc, groups == 2 ? pl.bpc_near : pl.bpc, pl.qr, groups, cnt, cursor, qoff, item_off,
                              nch, head, qlist, qblk, itab, st));
-    if (!pl.wide) {
+    if (!pl.pp) {
     const dim3 qgrid((unsigned)pl.max_qblk, (unsigned)((idx->dpad + 64 * kQSlabs - 1) / (64 * kQSlabs)));
     if (pl.qr == 128 && pl.split)
         hipLaunchKernelGGL((k_qstage<128, true>), qgrid, dim3(256), 0, st, q, idx->d, idx->dpad,
@@ -3029,6 +3105,10 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     a.QT = QT;
     a.QN = QN;
     a.QE = QE;
+    a.qoff = qoff;
+    a.qlist = qlist;
+    a.QH = QH;
+    a.qpair = pl.pp && !pl.wide ? 1 : 0;
     a.partial = partial;
     // the lists' own error bounds (k_screen_m only; the merge otherwise takes the list-wide one)
     float *pE = pl.mfma && !pl.v2 ? (float *)(w + pl.off_pe) : nullptr;
@@ -3044,7 +3124,8 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     a.bpc_near = groups == 2 ? pl.bpc_near : pl.bpc;
     a.nch_max = pl.nch_max;
     a.stats = idx->stats_on ? (unsigned long long *)idx->stats : nullptr;
-    hipError_t e = pl.wide == 2 ? launch_vscreen(idx, q, cnt, qoff, qlist, itab, head, QN, QE, partial, pE, qbound,
+    hipError_t e = pl.wide == 2 ? launch_vscreen(idx, q, cnt, qoff, qlist, itab, head, QN, QE, (const uint16_t *)QT,
+                                                 partial, pE, qbound,
                                                  (int)nprobe, (int)k, pl.bpc, a.bpc_near, pl.nch_max, nvirt, tri ? 1 : 0,
                                                  pl.grid, (int4 *)(w + pl.off_wrec),
                                                  (int64_t)(pl.max_qblk + 1) * pl.nch_max, st)

@@ -40,23 +40,27 @@ namespace lira {
 typedef __bf16 vbf16x8 __attribute__((ext_vector_type(8)));
 typedef float vf4 __attribute__((ext_vector_type(4)));
 
-static constexpr int kVQR = 64;     // query rows per item (one wave)
-static constexpr int kVW = 4;       // independent waves per workgroup (one per SIMD)
+static constexpr int kVRT = 2;      // row tiles of 16 per wave
+static constexpr int kVQR = 16 * kVRT;  // query rows per item (one wave): 32
+static constexpr int kVW = 4;       // independent waves per workgroup
+static constexpr int kVOcc = 2;     // workgroups per CU (2 waves per SIMD: <= 256 registers per wave)
 static constexpr int kVK2 = 32;     // row list keys (k <= 24)
 static constexpr int kVBC = 32;     // survivor buffer keys per row
 static constexpr int kVMaxT = 128;  // tiles per item (their radius ranges: 2 registers per lane)
 
 struct VSmem {  // per wave
-    static constexpr int lists = 0;                            // [64][K2] u64
-    static constexpr int bufs = lists + kVQR * kVK2 * 8;       // [64][BC] u64
-    static constexpr int kth = bufs + kVQR * kVBC * 8;         // [64] u64: list key k - 1
-    static constexpr int hs = kth + kVQR * 8;                  // [64] f32: the rows' dot thresholds
-    static constexpr int qns = hs + kVQR * 4;                  // [64] f32: the rows' fl(||q'||^2)
-    static constexpr int bcs = qns + kVQR * 4;                 // [64] int: buffer fills
-    static constexpr int per_wave = bcs + kVQR * 4;
+    static constexpr int lists = 0;                            // [QR][K2] u64
+    static constexpr int bufs = lists + kVQR * kVK2 * 8;       // [QR][BC] u64
+    static constexpr int kth = bufs + kVQR * kVBC * 8;         // [QR] u64: list key k - 1
+    static constexpr int hs = kth + kVQR * 8;                  // [QR] f32: the rows' dot thresholds
+    static constexpr int qns = hs + kVQR * 4;                  // [QR] f32: the rows' fl(||q'||^2)
+    static constexpr int bcs = qns + kVQR * 4;                 // [QR] int: buffer fills
+    static constexpr int rq = bcs + kVQR * 4;                  // [QR] float4: qn, qnorm, dq, qres of the row
+    static constexpr int tr = rq + kVQR * 16;                  // [kVMaxT] float4: tile lo, hi, hi residual
+    static constexpr int per_wave = tr + kVMaxT * 16;
     static constexpr int total = kVW * per_wave;
 };
-static_assert(VSmem::total <= 160 * 1024, "k_screen_v LDS");
+static_assert(VSmem::total * kVOcc <= 160 * 1024, "k_screen_v LDS");
 
 struct VArgs {
     const uint16_t *Xb;
@@ -67,6 +71,7 @@ struct VArgs {
     const float *Q, *pivot;
     const float4 *QN;    // per pair: qn, qnorm (up), -, ||q - c|| (k_pairs)
     const float *QE;     // per pair: ||q' - hi(q')|| (up)
+    const uint16_t *QH;  // per pair: hi(fl(q - c)) bf16, dpad dims (k_pairs; zero past d)
     const float2 *tstat;
     const float *tres;
     u64 *partial;
@@ -135,7 +140,8 @@ static constexpr bool kVClk = false;
 #endif
 
 template <int NKS>
-__global__ __launch_bounds__(256, 1) void k_screen_v(VArgs a) {
+__global__ __launch_bounds__(64 * kVW, kVOcc) void k_screen_v(VArgs a) {
+    constexpr int RT = kVRT, QR = kVQR;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
@@ -147,6 +153,8 @@ __global__ __launch_bounds__(256, 1) void k_screen_v(VArgs a) {
     float *const h_s = (float *)(wsm + VSmem::hs);
     float *const qn_s = (float *)(wsm + VSmem::qns);
     int *const bc_s = (int *)(wsm + VSmem::bcs);
+    float4 *const tr_s = (float4 *)(wsm + VSmem::tr);
+    float4 *const rq_s = (float4 *)(wsm + VSmem::rq);
     const int k = a.k;
     const double dd = (double)a.d;
     unsigned long long *const cnt = kVClk ? nullptr : a.stats;
@@ -218,6 +226,7 @@ __global__ __launch_bounds__(256, 1) void k_screen_v(VArgs a) {
 #pragma unroll 1
     for (;;) {
         const int it = claim_resolve(raw_next);
+        tick(7);
         if (it < 0) break;
         raw_next = claim_issue();
         const int4 r0 = a.vrec[2 * it], r1 = a.vrec[2 * it + 1];
@@ -227,7 +236,7 @@ __global__ __launch_bounds__(256, 1) void k_screen_v(VArgs a) {
         const float R = __int_as_float(__builtin_amdgcn_readfirstlane(r1.z));
 
         // ---- rows: lane = row
-        const int my_pair = lane < nval ? a.qlist[pbase + lane] : -1;
+        const int my_pair = lane < nval && lane < QR ? a.qlist[pbase + lane] : -1;
         const int my_q = my_pair >= 0 ? my_pair / a.nprobe : -1;
         float4 qr = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         float my_qres = 0.0f;
@@ -237,64 +246,35 @@ __global__ __launch_bounds__(256, 1) void k_screen_v(VArgs a) {
             my_qres = a.QE[my_pair];
             if (a.qbound) pub = __hip_atomic_load(a.qbound + my_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        const float my_qn = qr.x, my_qnorm = qr.y, my_dq = qr.w;
-        qn_s[lane] = my_qn;
-        bc_s[lane] = 0;
-        kth_s[lane] = kEmptyKey;
+        // (the row's constants live in LDS between refreshes: registers are short at
+        // 2 waves per SIMD, and a spill reload in the tile loop would drain vmcnt)
+        if (lane < QR) {
+            rq_s[lane] = make_float4(qr.x, qr.y, qr.w, my_qres);
+            qn_s[lane] = qr.x;
+            bc_s[lane] = 0;
+            kth_s[lane] = kEmptyKey;
+        }
         {
             uint4 *L4 = (uint4 *)lists;
 #pragma unroll
-            for (int i = 0; i < kVQR * kVK2 / 2 / 64; ++i) L4[i * 64 + lane] = make_uint4(~0u, ~0u, ~0u, ~0u);
+            for (int i = 0; i < QR * kVK2 / 2 / 64; ++i) L4[i * 64 + lane] = make_uint4(~0u, ~0u, ~0u, ~0u);
         }
         // ---- the rows' hi parts of fl(q - c): A fragments (lane (g, cj): row 16 rt + cj,
         // dims 32 s + 8 g .. + 7)
-        vbf16x8 Aq[4][NKS];
-        {
-            // (branch-free loads from clamped addresses, then selects: a divergent
-            // branch around a load makes hipcc wait for it at the join)
-            const float *pv = a.pivot + (int64_t)p * a.d;
-            const bool d8 = (a.d & 7) == 0;  // (uniform) whole 8-dim groups: two float4 per group
+        vbf16x8 Aq[RT][NKS];
 #pragma unroll
-            for (int rt = 0; rt < 4; ++rt) {
-                const int pr = __shfl(my_pair, rt * 16 + cj, 64);
-                const float *qrow = a.Q + (int64_t)(pr >= 0 ? pr / a.nprobe : 0) * a.d;
+        for (int rt = 0; rt < RT; ++rt) {
+            const int pr = __shfl(my_pair, rt * 16 + cj, 64);
+            const vbf16x8 *qh = (const vbf16x8 *)(a.QH + (int64_t)(pr >= 0 ? pr : 0) * a.dpad + 8 * g);
 #pragma unroll
-                for (int s = 0; s < NKS; ++s) {
-                    const int j0 = 32 * s + 8 * g;
-                    uint32_t w4[4];
-                    if (d8) {
-                        const bool ok = pr >= 0 && j0 < a.d;
-                        const int jj = ok ? j0 : 0;
-                        const float4 x0 = *(const float4 *)(qrow + jj), x1 = *(const float4 *)(qrow + jj + 4);
-                        const float4 c0 = *(const float4 *)(pv + jj), c1 = *(const float4 *)(pv + jj + 4);
-                        w4[0] = bf16_rne_sat(x0.x - c0.x) | (bf16_rne_sat(x0.y - c0.y) << 16);
-                        w4[1] = bf16_rne_sat(x0.z - c0.z) | (bf16_rne_sat(x0.w - c0.w) << 16);
-                        w4[2] = bf16_rne_sat(x1.x - c1.x) | (bf16_rne_sat(x1.y - c1.y) << 16);
-                        w4[3] = bf16_rne_sat(x1.z - c1.z) | (bf16_rne_sat(x1.w - c1.w) << 16);
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) w4[e] = ok ? w4[e] : 0u;
-                    } else {
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            uint32_t pr2[2];
-#pragma unroll
-                            for (int f = 0; f < 2; ++f) {
-                                const int jj = j0 + 2 * e + f;
-                                const bool ok = pr >= 0 && jj < a.d;
-                                const uint32_t v = bf16_rne_sat(qrow[ok ? jj : 0] - pv[ok ? jj : 0]);
-                                pr2[f] = ok ? v : 0u;
-                            }
-                            w4[e] = pr2[0] | (pr2[1] << 16);
-                        }
-                    }
-                    Aq[rt][s] = __builtin_bit_cast(vbf16x8, make_uint4(w4[0], w4[1], w4[2], w4[3]));
-                }
+            for (int s = 0; s < NKS; ++s) {
+                const vbf16x8 v = qh[4 * s];  // (branch-free: row 0's, then zeroed for an empty row)
+                Aq[rt][s] = pr >= 0 ? v : (vbf16x8)(__bf16)0.0f;
             }
         }
-        // ---- the item's tile radius ranges / hi residuals: lane t & 63 of register t >> 6
-        float bl_lo[2], bl_hi[2], bl_re[2];
+        // ---- the item's tile radius ranges / hi residuals into LDS (tr_s[t])
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < kVMaxT / 64; ++u) {
             const int t = lane + 64 * u;
             float lo = -__builtin_inff(), hi = __builtin_inff(), re = -1.0f;
             if (t < ntiles) {
@@ -305,15 +285,14 @@ __global__ __launch_bounds__(256, 1) void k_screen_v(VArgs a) {
                 }
                 if (a.tres) re = a.tres[tfirst + t];
             }
-            bl_lo[u] = lo;
-            bl_hi[u] = hi;
-            bl_re[u] = re;
+            tr_s[t] = make_float4(lo, hi, re, 0.0f);
         }
+        __builtin_amdgcn_wave_barrier();
         // ---- row threshold state (lane = row)
         float E_run = 0.0f, T_c = -1.0f, A_c = 0.0f, h_l = 0.0f;
         uint32_t own_pub = ~0u;
         float2 ab_c;
-        auto interval = [&](float T) {  // the row's skip interval for ||x - c|| under bound T (+ A_c)
+        auto interval = [&](float T, float my_dq) {  // the row's skip interval for ||x - c|| under bound T (+ A_c)
             float2 ab = make_float2(-__builtin_inff(), __builtin_inff());
             A_c = vup(vup(fmaxf(T, 0.0f) + 0x1p-126f) * iF);
             if (my_pair < 0) {
@@ -324,14 +303,14 @@ __global__ __launch_bounds__(256, 1) void k_screen_v(VArgs a) {
             }
             return ab;
         };
-        ab_c = interval(pub != ~0u ? ord2f(pub) : __builtin_inff());
+        ab_c = interval(pub != ~0u ? ord2f(pub) : __builtin_inff(), qr.w);
         const bool any_row = __any(my_pair >= 0);
         // first tile >= t that some row may need (current intervals; stale ones are wider: safe)
         auto next_live = [&](int t) {
             if (!a.tri) return t;
             while (t < ntiles) {
-                const float lo = vlane(t < 64 ? bl_lo[0] : bl_lo[1], t & 63);
-                const float hi = vlane(t < 64 ? bl_hi[0] : bl_hi[1], t & 63);
+                const float4 tv = tr_s[t];  // (uniform address: one broadcast read)
+                const float lo = tv.x, hi = tv.y;
                 if (!__all(hi < ab_c.x || lo > ab_c.y)) break;
                 ++t;
             }
@@ -343,14 +322,20 @@ __global__ __launch_bounds__(256, 1) void k_screen_v(VArgs a) {
         // candidate 4 cj + ct, Xb piece (2 s + (g >> 1), hi part g & 1), p = 16 ct + cj)
         vbf16x8 B0[NKS][4], B1[NKS][4];
         vf4 xa0, xa1;
+        // buffer loads off one per-item resource: a single VGPR offset per lane and
+        // scalar offsets per piece (flat addresses needed a 64-bit VGPR pair per 4 KiB
+        // of immediate-offset reach, which spilled at 2 waves per SIMD)
+        const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(a.Xb + (int64_t)tfirst * nkc * 2048), (short)0, ntiles * nkc * 4096, 0x00020000);
+        const int voff = (g >> 1) * 4096 + (g & 1) * 1024 + cj * 16;
         auto issue = [&](vbf16x8 (&B)[NKS][4], vf4 &xa, int t) {
             const int tc = min(t, ntiles - 1);  // (past the end: a valid tile, not used)
-            const uint16_t *tb = a.Xb + (int64_t)(tfirst + tc) * nkc * 2048 + (g & 1) * 512 + cj * 8;
 #pragma unroll
             for (int s = 0; s < NKS; ++s)
 #pragma unroll
                 for (int ct = 0; ct < 4; ++ct)
-                    B[s][ct] = *(const vbf16x8 *)(tb + (2 * s + (g >> 1)) * 2048 + ct * 128);
+                    B[s][ct] = __builtin_bit_cast(
+                        vbf16x8, __builtin_amdgcn_raw_buffer_load_b128(xrs, voff, tc * nkc * 4096 + s * 8192 + ct * 256, 0));
             xa = *(const vf4 *)(a.xadj + (int64_t)(tfirst + tc) * kTile + 4 * cj);
         };
 
@@ -359,10 +344,9 @@ __global__ __launch_bounds__(256, 1) void k_screen_v(VArgs a) {
         // ---- one tile: refresh the rows' thresholds, MFMAs, selection
         auto process = [&](const vbf16x8 (&B)[NKS][4], const vf4 &xa, int t) {
             // refresh (lane = row)
-            const float b_lo = vlane(t < 64 ? bl_lo[0] : bl_lo[1], t & 63);
-            const float b_hi = vlane(t < 64 ? bl_hi[0] : bl_hi[1], t & 63);
-            const float b_re = vlane(t < 64 ? bl_re[0] : bl_re[1], t & 63);
-            const u64 kk = kth_s[lane];
+            const float4 tv = tr_s[t];
+            const float b_lo = tv.x, b_hi = tv.y, b_re = tv.z;
+            const u64 kk = lane < QR ? kth_s[lane] : kEmptyKey;
             float T = kk == kEmptyKey ? __builtin_inff() : bndP(key_score(kk), E_run);
             if (a.share) {
                 if (my_pair >= 0 && kk != kEmptyKey) {
@@ -378,9 +362,11 @@ __global__ __launch_bounds__(256, 1) void k_screen_v(VArgs a) {
                 pub_next = __hip_atomic_load(a.qbound + my_qs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             if (pub != ~0u) T = fminf(T, ord2f(pub));
+            const float4 rq = lane < QR ? rq_s[lane] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            const float my_qn = rq.x, my_qnorm = rq.y, my_qres = rq.w;
             if (T != T_c) {
                 T_c = T;
-                ab_c = interval(T);
+                ab_c = interval(T, rq.z);
             }
             const float Rb = a.tri ? fminf(R, vup(b_hi * (1.0f + 0x1p-19f))) : R;
             const float Eb = verr_E(my_qnorm, Rb, dpf, b_re, my_qres);
@@ -397,35 +383,49 @@ __global__ __launch_bounds__(256, 1) void k_screen_v(VArgs a) {
             tick(2);
             if (wdead) return;
             E_run = fmaxf(E_run, Eb);  // (this tile's keys may join the lists)
-            h_s[lane] = h_l;
+            if (lane < QR) h_s[lane] = h_l;
             __builtin_amdgcn_wave_barrier();
-            vf4 hp[4];
+            vf4 hp[RT];
 #pragma unroll
-            for (int rt = 0; rt < 4; ++rt) {
+            for (int rt = 0; rt < RT; ++rt) {
                 const vf4 h4 = *(const vf4 *)(h_s + rt * 16 + 4 * g);
                 // (padding: xadj = +inf gives -inf, which never passes a finite threshold)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) hp[rt][r] = fmaxf(h4[r], -3.40282347e38f);
             }
             // MFMAs: 4 row tiles x 4 candidate groups x NKS k-steps
-            vf4 acc[4][4];
+            vf4 acc[RT][4];
 #pragma unroll
-            for (int rt = 0; rt < 4; ++rt)
+            for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                 for (int ct = 0; ct < 4; ++ct) acc[rt][ct] = (vf4)(0.0f);
+#ifdef LIRA_VDBG
+            if (!(LIRA_VDBG & 2))
+#endif
 #pragma unroll
             for (int s = 0; s < NKS; ++s)
 #pragma unroll
-                for (int rt = 0; rt < 4; ++rt)
+                for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                     for (int ct = 0; ct < 4; ++ct)
                         acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Aq[rt][s], B[s][ct], acc[rt][ct], 0, 0, 0);
             tick(3);
+#ifdef LIRA_VDBG  // timing experiments (results invalid): 1 = no selection, 2 = no MFMA either
+            if (LIRA_VDBG & 1) {
+                float z = 0.0f;
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                    for (int ct = 0; ct < 4; ++ct) z += (LIRA_VDBG & 2) ? (float)B[0][ct][rt] : acc[rt][ct][0];
+                if (z == 1234.5f) bufs[lane] = 1;
+                return;
+            }
+#endif
             // selection: lane (g, cj) holds rows 16 rt + 4 g + r, candidates 4 cj + ct
-            float m[4][4];
+            float m[RT][4];
             bool anyp = false;
 #pragma unroll
-            for (int rt = 0; rt < 4; ++rt)
+            for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const float w0 = acc[rt][0][r] - xa[0], w1 = acc[rt][1][r] - xa[1];
@@ -439,7 +439,7 @@ __global__ __launch_bounds__(256, 1) void k_screen_v(VArgs a) {
             }
             const uint32_t tid0 = (uint32_t)(tfirst + t) * kTile + 4 * cj;
 #pragma unroll
-            for (int rt = 0; rt < 4; ++rt)
+            for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     if (!__any(m[rt][r] >= hp[rt][r])) continue;
@@ -508,8 +508,8 @@ __global__ __launch_bounds__(256, 1) void k_screen_v(VArgs a) {
         }
 
         // ---- epilogue: merge the rows whose lists filled; lists out (two rows per round)
-        const int bcl = bc_s[lane];
-        const bool srt = kth_s[lane] != kEmptyKey || lists[lane * kVK2] != kEmptyKey || bcl == kVBC;
+        const int bcl = lane < QR ? bc_s[lane] : 0;
+        const bool srt = lane < QR && (kth_s[lane] != kEmptyKey || lists[lane * kVK2] != kEmptyKey || bcl == kVBC);
         {
             u64 mrg = __ballot(bcl > 0 && srt);
             while (mrg) {
@@ -528,7 +528,7 @@ __global__ __launch_bounds__(256, 1) void k_screen_v(VArgs a) {
         const u64 srt_m = __ballot(srt);
         const int hl = lane & 31;
 #pragma unroll 1
-        for (int r2 = 0; r2 < kVQR; r2 += 2) {
+        for (int r2 = 0; r2 < QR; r2 += 2) {
             const int row = r2 + (lane >> 5);
             const int pr = __shfl(my_pair, row, 64);
             const int nb = __shfl(bcl, row, 64);
@@ -546,8 +546,9 @@ __global__ __launch_bounds__(256, 1) void k_screen_v(VArgs a) {
         tick(6);
     }
     if (kVClk && a.stats && lane == 0 && wave == 0) {
-        // [1] item prologue, [2] refresh, [3] MFMA issue, [4] selection, [5] issue + skip, [6] epilogue
-        for (int i = 1; i < 7; ++i) atomicAdd(a.stats + i, (unsigned long long)ck[i]);
+        // [1] item prologue, [2] refresh, [3] MFMA issue, [4] selection, [5] issue + skip, [6] epilogue,
+        // [7] claims
+        for (int i = 1; i < 8; ++i) atomicAdd(a.stats + i, (unsigned long long)ck[i]);
     }
 }
 
@@ -557,18 +558,21 @@ static hipError_t launch_v(const VArgs &a, int grid, hipStream_t st) {
     static std::atomic<uint64_t> attr{0};
     hipError_t e = set_smem_attr_once(attr, (const void *)k_screen_v<NKS>, VSmem::total);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_screen_v<NKS>), dim3(grid), dim3(64 * kVW), VSmem::total, st, a);
+    hipLaunchKernelGGL((k_screen_v<NKS>), dim3(grid * kVOcc), dim3(64 * kVW), VSmem::total, st, a);
     return hipGetLastError();
 }
 
 bool vscreen_shape_ok(int64_t dpad) { return dpad == 64 || dpad == 96 || dpad == 128; }
 int vscreen_smem() { return VSmem::total; }
 int vscreen_max_tiles() { return kVMaxT; }
+int vscreen_rows() { return kVQR; }
+int vscreen_workers_per_cu() { return kVW * kVOcc; }
 
 hipError_t launch_vscreen(const lira_index *idx, const float *q, const int32_t *cnt, const int32_t *qoff,
                           const int32_t *qlist, const int4 *itab, int32_t *head, const float4 *QN, const float *QE,
-                          u64 *partial, float *pE, uint32_t *qbound, int nprobe, int k, int bpc, int bpc_near,
-                          int nch_max, int n_virt, int tri, int grid, int4 *vrec, int64_t max_items, hipStream_t st) {
+                          const uint16_t *QH, u64 *partial, float *pE, uint32_t *qbound, int nprobe, int k, int bpc,
+                          int bpc_near, int nch_max, int n_virt, int tri, int grid, int4 *vrec, int64_t max_items,
+                          hipStream_t st) {
     hipLaunchKernelGGL(k_vrec, dim3((unsigned)((max_items + 255) / 256)), dim3(256), 0, st, itab, head, idx->tile_off,
                        qoff, cnt, idx->rmaxc, (int)idx->n_lists, n_virt, bpc, bpc_near, vrec);
     VArgs a;
@@ -581,6 +585,7 @@ hipError_t launch_vscreen(const lira_index *idx, const float *q, const int32_t *
     a.pivot = idx->pivot;
     a.QN = QN;
     a.QE = QE;
+    a.QH = QH;
     a.tstat = idx->tstat;
     a.tres = idx->tres;
     a.partial = partial;

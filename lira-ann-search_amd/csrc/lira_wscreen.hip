@@ -86,74 +86,19 @@ struct WArgs {
     unsigned long long *stats;
 };
 
-// ---- per-pair records + the partition filter --------------------------------
-// 16 lanes per (query, slot) pair, double sums as k_qstage: qn = fl(||q'||^2),
-// qnorm >= ||q'||, q' = fl(q - c) of the pair's list pivot c (centred) or q;
-// dq = fl(||q - c||) (triangle skip); qres >= ||q' - hi(q')|| (hi x hi bound).
-// Filter (lstat, qbound): a pair whose list lies wholly outside the query's
-// triangle interval under the seed bound T (k_seed_t: k exact candidates of
-// its slot-0 list score <= T) cannot hold a top-k candidate -- no candidate of
-// it can score <= T -- so it gets probe_live = -1 and no work item (the test
-// is k_screen_m's per-block skip over the list's radius range).  Slot 0 (the
-// seed's own list) always stays.
+// ---- per-pair records + the partition filter (lira_bounds.hpp pair_record) ----
+// One pair per 16 lanes, the filter bound from qbound (k_seed_t's seed); the
+// default L2 screen runs the same records inside k_seed_t<..., PAIRS> instead.
 __global__ __launch_bounds__(256) void k_pairs(const float *Q, int64_t d, const int32_t *probe, int64_t npairs,
                                                int nprobe, int n_lists, const float *pivot, int centred,
                                                const float2 *lstat, const uint32_t *qbound, int32_t *probe_live,
-                                               float4 *QN, float *QE, float *pqn) {
-    const int sub = threadIdx.x & 15;
+                                               float4 *QN, float *QE, float *pqn, uint16_t *QH, int64_t dpad) {
     const int64_t pair = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
     const bool valid = pair < npairs;
     const int praw = valid ? probe[pair] : -1;
-    const int p = praw < n_lists ? praw : -1;  // (an id >= n_lists passes through: k_count reports it)
-    const int64_t q = valid ? pair / nprobe : 0;
-    double s = 0.0, t = 0.0, e = 0.0;
-    if (p >= 0 && (QN || lstat)) {
-        const float *qr = Q + q * d, *pv = pivot ? pivot + (int64_t)p * d : nullptr;
-        for (int64_t j = sub; j < d; j += 16) {
-            const float x = qr[j], cv = pv ? pv[j] : 0.0f;
-            const float sv = centred && pv ? x - cv : x;
-            const double xc = (double)sv;
-            s = __builtin_fma(xc, xc, s);
-            if (QE) {
-                const double rr = (double)(sv - __uint_as_float(bf16_rne_sat(sv) << 16));
-                e = __builtin_fma(rr, rr, e);
-            }
-            if (pv) {
-                const double df = (double)x - (double)cv;
-                t = __builtin_fma(df, df, t);
-            }
-        }
-    }
-#pragma unroll
-    for (int m = 8; m >= 1; m >>= 1) {  // within the 16-lane DPP row
-        s += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, s), m));
-        t += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, t), m));
-        e += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, e), m));
-    }
-    if (sub != 0 || !valid) return;
-    int live = p;
-    const float dq = (float)__builtin_sqrt(t);
-    if (p >= 0 && lstat && qbound && (int)(pair % nprobe) >= 1) {
-        const uint32_t qb = qbound[q];
-        const double dd = (double)d, F = 1.0 - (dd + 4.0) * kU;
-        if (qb != ~0u && F > 0.5) {
-            const double T = (double)ord2f(qb);
-            if (T < 1e300) {
-                const double rad = __builtin_sqrt((fmax(T, 0.0) + dd * 0x1p-140) / F) * (1.0 + 0x1p-40);
-                double A = (double)dq * (1.0 - 0x1p-22) - rad, B = (double)dq * (1.0 + 0x1p-22) + rad;
-                A -= __builtin_fabs(A) * 0x1p-50;
-                B += __builtin_fabs(B) * 0x1p-50;
-                const float2 ls = lstat[p];
-                if (ls.y < __double2float_rd(A) || ls.x > __double2float_ru(B)) live = -1;
-            }
-        }
-    }
-    probe_live[pair] = praw >= n_lists ? praw : live;
-    if (live < 0) return;
-    const float qnu = __double2float_ru(__builtin_sqrt(s) * (1.0 + 0x1p-40));
-    if (QN) QN[pair] = make_float4((float)s, qnu, __int_as_float((int)pair), dq);
-    if (QE) QE[pair] = __double2float_ru(__builtin_sqrt(e) * (1.0 + 0x1p-40));
-    if (pqn) pqn[pair] = qnu;
+    const uint32_t qb = valid && lstat && qbound ? qbound[pair / nprobe] : ~0u;
+    pair_record(Q, d, pair, valid, praw, nprobe, n_lists, pivot, centred, lstat && qbound ? lstat : nullptr, qb,
+                probe_live, QN, QE, pqn, QH, dpad);
 }
 
 // ---- the wide screen ----------------------------------------------------------
@@ -735,11 +680,12 @@ int wscreen_smem() { return WSmem::total; }
 
 hipError_t launch_pairs(const float *Q, int64_t d, const int32_t *probe, int64_t npairs, int nprobe, int n_lists,
                         const float *pivot, int centred, const float2 *lstat, const uint32_t *qbound,
-                        int32_t *probe_live, float4 *QN, float *QE, float *pqn, hipStream_t st) {
+                        int32_t *probe_live, float4 *QN, float *QE, float *pqn, uint16_t *QH, int64_t dpad,
+                        hipStream_t st) {
     const unsigned g = (unsigned)((npairs * 16 + 255) / 256);
     if (g == 0) return hipSuccess;
     hipLaunchKernelGGL(k_pairs, dim3(g), dim3(256), 0, st, Q, d, probe, npairs, nprobe, n_lists, pivot, centred, lstat,
-                       qbound, probe_live, QN, QE, pqn);
+                       qbound, probe_live, QN, QE, pqn, QH, dpad);
     return hipGetLastError();
 }
 
