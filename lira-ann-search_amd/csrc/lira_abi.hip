@@ -121,57 +121,126 @@ __global__ __launch_bounds__(256) void k_pivot_partial_ids(const float *x, int64
     psum[(int64_t)s * d + j] = acc;
 }
 
+// Block of 64 threads: thread r walks row r (d floats at x + off, off < 0: a
+// row of zeros) in dim order, f(j, value).  Every row is read once and
+// coalesced: 32-dim slabs go through LDS (thread l loads dim j0 + (l & 31) of
+// rows 2i + (l >> 5)), so the per-row sequential sums below keep their order
+// (and bits) while HBM sees each byte once -- the lane-per-row walks they
+// replace read a tile's rows 4 B at a time, 64 rows apart (k_row_norms read
+// 13.3 GB for SIFT1M's 0.51 GB, profiles/r02_sift1m_mixture_pmc_summary.json).
+template <class F>
+__device__ __forceinline__ void walk_rows64(const float *x, int64_t d, int64_t off, F &&f) {
+    __shared__ float slab[64 * 33];
+    __shared__ int64_t roff[64];
+    const int l = threadIdx.x;
+    roff[l] = off;
+    __syncthreads();
+    for (int64_t j0 = 0; j0 < d; j0 += 32) {
+        const int nj = (int)min<int64_t>(32, d - j0), jj = l & 31;
+#pragma unroll 8
+        for (int i = 0; i < 32; ++i) {
+            const int r = 2 * i + (l >> 5);
+            const int64_t o = roff[r];
+            slab[r * 33 + jj] = o >= 0 && jj < nj ? x[o + j0 + jj] : 0.0f;
+        }
+        __syncthreads();
+        for (int u = 0; u < nj; ++u) f(j0 + u, slab[l * 33 + u]);
+        __syncthreads();
+    }
+}
+
 // Sort key of every list entry for the radius-ordered build: the bits of
-// fl(||x - pivot||) (non-negative floats order as their bits), one thread per
-// entry; its list by binary search over the offsets.
-__global__ __launch_bounds__(256) void k_entry_radius(const float *x, int64_t d, const int32_t *list_ids,
-                                                      const int64_t *list_off, int64_t n_lists, const float *pivot,
-                                                      int64_t total, uint32_t *key) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        int64_t lo = 0, hi = n_lists;  // list_off[lo] <= i < list_off[hi]
+// fl(||x - pivot||) (non-negative floats order as their bits), thread r of a
+// 64-thread block = entry 64 blockIdx + r (rows gathered through list_ids);
+// its list by binary search over the offsets.
+__global__ __launch_bounds__(64) void k_entry_radius(const float *x, int64_t d, const int32_t *list_ids,
+                                                     const int64_t *list_off, int64_t n_lists, const float *pivot,
+                                                     int64_t total, uint32_t *key) {
+    const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    int64_t lo = 0;
+    if (i < total) {
+        int64_t hi = n_lists;  // list_off[lo] <= i < list_off[hi]
         while (hi - lo > 1) {
             const int64_t m = (lo + hi) >> 1;
             if (list_off[m] <= i) lo = m; else hi = m;
         }
-        const float *row = x + (int64_t)list_ids[i] * d, *pv = pivot + lo * d;
-        double s = 0.0;
-        for (int64_t j = 0; j < d; ++j) {
-            const double df = (double)row[j] - (double)pv[j];
-            s = __builtin_fma(df, df, s);
-        }
-        key[i] = __float_as_uint((float)__builtin_sqrt(s));
     }
+    const float *pv = pivot + lo * d;
+    double s = 0.0;
+    walk_rows64(x, d, i < total ? (int64_t)list_ids[i] * d : -1, [&](int64_t j, float v) {
+        const double df = (double)v - (double)pv[j];
+        s = __builtin_fma(df, df, s);
+    });
+    if (i < total) key[i] = __float_as_uint((float)__builtin_sqrt(s));
 }
 
-// Radius bounds of every tile: lane r of a wave = row r of the tile.
-// ||x - pivot|| in double, rounded outward to fp32 with a 2^-40 relative
-// margin (the double sum's error is ~d * 2^-53), min/max over the tile's real
-// rows (NaN rows are ignored by fminf/fmaxf; they are never selected either).
-// A tile without real rows gets (+inf, -inf).
-__global__ __launch_bounds__(256) void k_tile_stats(const float *Xr, const int32_t *ids, int64_t d,
-                                                    const int32_t *tile_list, const float *pivot, int64_t n_tiles,
-                                                    float2 *tstat) {
-    const int lane = threadIdx.x & 63;
-    const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (t >= n_tiles) return;
-    const float *pv = pivot + (int64_t)tile_list[t] * d;
-    const float *x = Xr + (t * kTile + lane) * d;
-    double s = 0.0;
-    for (int64_t j = 0; j < d; ++j) {
-        const double df = (double)x[j] - (double)pv[j];
-        s = __builtin_fma(df, df, s);
-    }
-    const double R = __builtin_sqrt(s);
+// Every per-row statistic of the screen in ONE read of the row-major copy;
+// one 64-thread block per tile, thread r = row r (walk_rows64), sums in double
+// in dim order:
+//   xadj = fl(||x||^2) / 2 (L2; IP 0), +inf for padding, and the list's rmax
+//     >= max ||x|| (atomicMax on the bits of a non-negative float);
+//   (pivot, tstat) the tile's radius range lo <= ||x - c|| <= hi over its real
+//     rows, rounded outward with a 2^-40 margin ((+inf, -inf) without real rows);
+//   (pivot, xadjc) xadjc = fl(||fl(x - c)||^2) / 2 and the list's rmaxc >= max
+//     ||fl(x - c)||, fl(x - c) exactly the values k_split_rows splits;
+//   (tres) the tile's max over real rows of ||v - hi(v)||, v = fl(x - c) (or x
+//     without a pivot), hi(v) the bf16 part k_split_rows stores first.
+// sqrt rounded up with a 2^-40 relative margin (the double sums' error is ~d 2^-53).
+__global__ __launch_bounds__(64) void k_row_stats(const float *Xr, const int32_t *ids, int64_t d,
+                                                  const int32_t *tile_list, int metric, const float *pivot,
+                                                  float *xadj, float *rmax, float2 *tstat, float *xadjc, float *rmaxc,
+                                                  float *tres) {
+    const int lane = threadIdx.x;
+    const int64_t t = blockIdx.x;
+    const int b = tile_list[t];
+    const float *pv = pivot ? pivot + (int64_t)b * d : nullptr;
+    double s = 0.0, sr = 0.0, sc = 0.0, sh = 0.0;
+    walk_rows64(Xr, d, (t * kTile + lane) * d, [&](int64_t j, float v) {
+        const double dv = (double)v;
+        s = __builtin_fma(dv, dv, s);
+        float w = v;
+        if (pv) {
+            const float c = pv[j];
+            const double df = dv - (double)c;
+            sr = __builtin_fma(df, df, sr);
+            w = v - c;
+            const double dc = (double)w;
+            sc = __builtin_fma(dc, dc, sc);
+        }
+        if (tres) {
+            const double r = (double)w - (double)__uint_as_float(bf16_split_part(w, 0) << 16);
+            sh = __builtin_fma(r, r, sh);
+        }
+    });
     const bool real = ids[t * kTile + lane] >= 0;
-    float lo = real ? __double2float_rd(R * (1.0 - 0x1p-40)) : __builtin_inff();
-    float hi = real ? __double2float_ru(R * (1.0 + 0x1p-40)) : -__builtin_inff();
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-        lo = fminf(lo, __shfl_xor(lo, m, 64));
-        hi = fmaxf(hi, __shfl_xor(hi, m, 64));
+    const float xn = (float)s;  // round to nearest
+    xadj[t * kTile + lane] = !real ? __builtin_inff() : metric == LIRA_METRIC_L2 ? xn * 0.5f : 0.0f;
+    float r = real ? __double2float_ru(__builtin_sqrt(s) * (1.0 + 0x1p-40)) : 0.0f;
+    float lo = __builtin_inff(), hi = -__builtin_inff(), rc = 0.0f, m = 0.0f;
+    if (pv && tstat) {
+        const double R = __builtin_sqrt(sr);
+        lo = real ? __double2float_rd(R * (1.0 - 0x1p-40)) : __builtin_inff();
+        hi = real ? __double2float_ru(R * (1.0 + 0x1p-40)) : -__builtin_inff();
     }
-    if (lane == 0) tstat[t] = make_float2(lo, hi);
+    if (pv && xadjc) {
+        xadjc[t * kTile + lane] = real ? (float)sc * 0.5f : __builtin_inff();
+        rc = real ? __double2float_ru(__builtin_sqrt(sc) * (1.0 + 0x1p-40)) : 0.0f;
+    }
+    if (tres) m = real ? __double2float_ru(__builtin_sqrt(sh) * (1.0 + 0x1p-40)) : 0.0f;
+#pragma unroll
+    for (int k = 32; k >= 1; k >>= 1) {
+        r = fmaxf(r, __shfl_xor(r, k, 64));
+        lo = fminf(lo, __shfl_xor(lo, k, 64));
+        hi = fmaxf(hi, __shfl_xor(hi, k, 64));
+        rc = fmaxf(rc, __shfl_xor(rc, k, 64));
+        m = fmaxf(m, __shfl_xor(m, k, 64));
+    }
+    if (lane == 0) {
+        if (r > 0.0f) atomicMax((unsigned int *)&rmax[b], __float_as_uint(r));
+        if (pv && tstat) tstat[t] = make_float2(lo, hi);
+        if (pv && xadjc && rc > 0.0f) atomicMax((unsigned int *)&rmaxc[b], __float_as_uint(rc));
+        if (tres) tres[t] = m;
+    }
 }
 
 // Per list: the (min, max) of its tiles' radius ranges (+inf, -inf for an
@@ -190,54 +259,6 @@ __global__ __launch_bounds__(64) void k_list_stats(const float2 *tstat, const in
         hi = fmaxf(hi, __shfl_xor(hi, m, 64));
     }
     if (lane == 0) lstat[b] = make_float2(lo, hi);
-}
-
-// Screening constants of every storage row (lane = row of a tile): xadj and
-// the list's rmax (atomicMax on the bits of a non-negative float).  Norms in
-// double; sqrt rounded up with a 2^-40 relative margin.
-__global__ __launch_bounds__(256) void k_row_norms(const float *Xr, const int32_t *ids, int64_t d,
-                                                   const int32_t *tile_list, int64_t n_tiles, int metric,
-                                                   float *xadj, float *rmax) {
-    const int lane = threadIdx.x & 63;
-    const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (t >= n_tiles) return;
-    const float *x = Xr + (t * kTile + lane) * d;
-    double s = 0.0;
-    for (int64_t j = 0; j < d; ++j) {
-        const double v = (double)x[j];
-        s = __builtin_fma(v, v, s);
-    }
-    const bool real = ids[t * kTile + lane] >= 0;
-    const float xn = (float)s;  // round to nearest
-    xadj[t * kTile + lane] = !real ? __builtin_inff() : metric == LIRA_METRIC_L2 ? xn * 0.5f : 0.0f;
-    float r = real ? __double2float_ru(__builtin_sqrt(s) * (1.0 + 0x1p-40)) : 0.0f;
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) r = fmaxf(r, __shfl_xor(r, m, 64));
-    if (lane == 0 && r > 0.0f) atomicMax((unsigned int *)&rmax[tile_list[t]], __float_as_uint(r));
-}
-
-// Centred screening constants (L2, for the split-bf16 copy): per row
-// xadjc = fl(||fl(x - c)||^2) / 2 and the list's rmaxc >= max ||fl(x - c)||,
-// c = the list's pivot, fl(x - c) exactly the fp32 values k_split_rows splits.
-__global__ __launch_bounds__(256) void k_row_norms_c(const float *Xr, const int32_t *ids, int64_t d,
-                                                     const int32_t *tile_list, const float *pivot, int64_t n_tiles,
-                                                     float *xadjc, float *rmaxc) {
-    const int lane = threadIdx.x & 63;
-    const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (t >= n_tiles) return;
-    const float *x = Xr + (t * kTile + lane) * d;
-    const float *pv = pivot + (int64_t)tile_list[t] * d;
-    double s = 0.0;
-    for (int64_t j = 0; j < d; ++j) {
-        const double v = (double)(x[j] - pv[j]);
-        s = __builtin_fma(v, v, s);
-    }
-    const bool real = ids[t * kTile + lane] >= 0;
-    xadjc[t * kTile + lane] = real ? (float)s * 0.5f : __builtin_inff();
-    float r = real ? __double2float_ru(__builtin_sqrt(s) * (1.0 + 0x1p-40)) : 0.0f;
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) r = fmaxf(r, __shfl_xor(r, m, 64));
-    if (lane == 0 && r > 0.0f) atomicMax((unsigned int *)&rmaxc[tile_list[t]], __float_as_uint(r));
 }
 
 // X[tile][j][row] = Xr[tile*64 + row][j]: one workgroup per tile, LDS
@@ -287,29 +308,6 @@ __global__ __launch_bounds__(256) void k_split_rows(const float *Xr, int64_t d, 
         }
         Xb[tc * 256 + u] = make_uint4(w[0], w[1], w[2], w[3]);
     }
-}
-
-// Per tile: max over its real rows of ||v - hi(v)||, v the values k_split_rows
-// splits (x - pivot with a pivot), hi(v) the bf16 part it stores first; double
-// sum, rounded up with a 2^-40 margin.  Lane = row of the tile.
-__global__ __launch_bounds__(256) void k_tile_hires(const float *Xr, const int32_t *ids, int64_t d,
-                                                    const float *pivot, const int32_t *tile_list, int64_t n_tiles,
-                                                    float *tres) {
-    const int lane = threadIdx.x & 63;
-    const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (t >= n_tiles) return;
-    const float *x = Xr + (t * kTile + lane) * d;
-    const float *pv = pivot ? pivot + (int64_t)tile_list[t] * d : nullptr;
-    double s = 0.0;
-    for (int64_t j = 0; j < d; ++j) {
-        const float v = pv ? x[j] - pv[j] : x[j];
-        const double r = (double)v - (double)__uint_as_float(bf16_split_part(v, 0) << 16);
-        s = __builtin_fma(r, r, s);
-    }
-    float m = ids[t * kTile + lane] >= 0 ? __double2float_ru(__builtin_sqrt(s) * (1.0 + 0x1p-40)) : 0.0f;
-#pragma unroll
-    for (int k = 32; k >= 1; k >>= 1) m = fmaxf(m, __shfl_xor(m, k, 64));
-    if (lane == 0) tres[t] = m;
 }
 
 __global__ void k_check_ids(const int32_t *ids, int64_t n, int64_t n_rows, int32_t *bad) {
@@ -547,8 +545,8 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
                 rc = fail(LIRA_ENOMEM, "hipMalloc of the radius-order scratch failed (LIRA_OPT_ORDER = 0 skips it)");
                 break;
             }
-            hipLaunchKernelGGL(k_entry_radius, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 65536)),
-                               dim3(256), 0, st, x, d, list_ids, d_loff, n_lists, idx->pivot, total, d_key);
+            hipLaunchKernelGGL(k_entry_radius, dim3((unsigned)((total + 63) / 64)), dim3(64), 0, st, x, d, list_ids,
+                               d_loff, n_lists, idx->pivot, total, d_key);
             e = hipGetLastError();
             if (e == hipSuccess)
                 e = hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb, d_key, d_key2, list_ids, d_sorted,
@@ -589,62 +587,55 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
             break;
         }
         e = hipMemsetAsync(idx->rmax, 0, (size_t)n_lists * 4, st);
+        if (e == hipSuccess && l2 && !order) {  // (radius order computed them from x already)
+            if (segs > 0)
+                hipLaunchKernelGGL(k_pivot_partial, dim3((unsigned)segs, dy), dim3(256), 0, st, idx->Xr, d, d_seg,
+                                   d_segf, idx->tile_off, d_loff, d_psum);
+            hipLaunchKernelGGL(k_pivot_final, dim3((unsigned)n_lists, dy), dim3(256), 0, st, d, d_segf, d_loff,
+                               d_psum, idx->pivot);
+            e = hipGetLastError();
+        }
+        // the split-bf16 screen copy: best effort (without it the screen runs on fp32
+        // MFMA / VALU); L2: of x - pivot, with its own (centred) norms; its hi-part
+        // residual bounds tres also best effort (without them the hi-only screens
+        // bound by 2^-8 R)
+        if (hipMalloc(&idx->Xb, (size_t)tiles * kTile * dpad * 4) != hipSuccess) {
+            (void)hipGetLastError();
+            idx->Xb = nullptr;
+        }
+        if (idx->Xb && idx->pivot) {
+            if (hipMalloc(&idx->xadjc, (size_t)tiles * kTile * 4) != hipSuccess ||
+                hipMalloc(&idx->rmaxc, (size_t)n_lists * 4) != hipSuccess) {
+                rc = fail(LIRA_ENOMEM, "hipMalloc of the centred row-norm arrays failed");
+                break;
+            }
+            if (e == hipSuccess) e = hipMemsetAsync(idx->rmaxc, 0, (size_t)n_lists * 4, st);
+        }
+        if (idx->Xb && hipMalloc(&idx->tres, (size_t)tiles * 4) != hipSuccess) {
+            (void)hipGetLastError();
+            idx->tres = nullptr;
+        }
+        // every per-row statistic in one coalesced pass over Xr
         if (e == hipSuccess) {
-            hipLaunchKernelGGL(k_row_norms, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, idx->Xr, idx->ids,
-                               d, d_tlist, tiles, idx->metric, idx->xadj, idx->rmax);
+            hipLaunchKernelGGL(k_row_stats, dim3((unsigned)tiles), dim3(64), 0, st, idx->Xr, idx->ids, d, d_tlist,
+                               idx->metric, l2 ? idx->pivot : nullptr, idx->xadj, idx->rmax, l2 ? idx->tstat : nullptr,
+                               idx->xadjc, idx->rmaxc, idx->tres);
             e = hipGetLastError();
         }
         if (e == hipSuccess && l2) {
-            if (!order && segs > 0)
-                hipLaunchKernelGGL(k_pivot_partial, dim3((unsigned)segs, dy), dim3(256), 0, st, idx->Xr, d, d_seg,
-                                   d_segf, idx->tile_off, d_loff, d_psum);
-            {
-                if (!order)
-                    hipLaunchKernelGGL(k_pivot_final, dim3((unsigned)n_lists, dy), dim3(256), 0, st, d, d_segf,
-                                       d_loff, d_psum, idx->pivot);
-                hipLaunchKernelGGL(k_tile_stats, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, idx->Xr,
-                                   idx->ids, d, d_tlist, idx->pivot, tiles, idx->tstat);
-                hipLaunchKernelGGL(k_list_stats, dim3((unsigned)n_lists), dim3(64), 0, st, idx->tstat, idx->tile_off,
-                                   idx->lstat);
-                e = hipGetLastError();
-            }
+            hipLaunchKernelGGL(k_list_stats, dim3((unsigned)n_lists), dim3(64), 0, st, idx->tstat, idx->tile_off,
+                               idx->lstat);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess && idx->Xb) {
+            hipLaunchKernelGGL(k_split_rows, dim3((unsigned)std::min<int64_t>(tiles * (dpad / 16), 1 << 20)),
+                               dim3(256), 0, st, idx->Xr, d, tiles, dpad, idx->pivot, d_tlist, (uint4 *)idx->Xb);
+            e = hipGetLastError();
         }
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) {
-            rc = fail(LIRA_EHIP, std::string("row norms / pivots failed: ") + hipGetErrorString(e));
+            rc = fail(LIRA_EHIP, std::string("row statistics / pivots / split copy failed: ") + hipGetErrorString(e));
             break;
-        }
-        // the split-bf16 screen copy: best effort (without it the screen runs on fp32 MFMA / VALU);
-        // L2: of x - pivot, with its own (centred) norms
-        if (hipMalloc(&idx->Xb, (size_t)tiles * kTile * dpad * 4) == hipSuccess) {
-            if (idx->pivot) {
-                if (hipMalloc(&idx->xadjc, (size_t)tiles * kTile * 4) != hipSuccess ||
-                    hipMalloc(&idx->rmaxc, (size_t)n_lists * 4) != hipSuccess) {
-                    rc = fail(LIRA_ENOMEM, "hipMalloc of the centred row-norm arrays failed");
-                    break;
-                }
-                e = hipMemsetAsync(idx->rmaxc, 0, (size_t)n_lists * 4, st);
-                if (e == hipSuccess)
-                    hipLaunchKernelGGL(k_row_norms_c, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, idx->Xr,
-                                       idx->ids, d, d_tlist, idx->pivot, tiles, idx->xadjc, idx->rmaxc);
-            }
-            if (e == hipSuccess)
-                hipLaunchKernelGGL(k_split_rows, dim3((unsigned)std::min<int64_t>(tiles * (dpad / 16), 1 << 20)),
-                                   dim3(256), 0, st, idx->Xr, d, tiles, dpad, idx->pivot, d_tlist, (uint4 *)idx->Xb);
-            if (e == hipSuccess) e = hipGetLastError();
-            if (e == hipSuccess) {  // (best effort: without it the hi-only screen bounds by 2^-8 R)
-                if (hipMalloc(&idx->tres, (size_t)tiles * 4) == hipSuccess) {
-                    hipLaunchKernelGGL(k_tile_hires, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, idx->Xr,
-                                       idx->ids, d, idx->pivot, d_tlist, tiles, idx->tres);
-                    e = hipGetLastError();
-                } else {
-                    (void)hipGetLastError();
-                    idx->tres = nullptr;
-                }
-            }
-        } else {
-            (void)hipGetLastError();
-            idx->Xb = nullptr;
         }
         // the fp32 tile copy for the all-exact / VALU kernels (LIRA_OPT_KEEP_TILES)
         if (e == hipSuccess && idx->opt.keep_tiles) {

@@ -47,7 +47,7 @@ __device__ __forceinline__ double err_E(double qnorm, double R, double d, int sp
         // split == 2 (hi-only x, k_screen_m<..., 2>): dot~ = sum (qh + ql) xh, x = xh + ex:
         // |dot~ - q.x| <= |q.ex| + |(q - qh - ql).xh| + rounding <= |q| ||ex|| +
         // (2^-16 + 2 dpad 2^-22) 1.02 |q| R, with ||ex|| <= 2^-8 R (|ex_i| <= 2^-8 |x_i|)
-        // or, tighter, hres >= ||ex|| of every candidate concerned (k_tile_hires)
+        // or, tighter, hres >= ||ex|| of every candidate concerned (lira_abi.hip k_row_stats)
         const double ex = hres >= 0.0 ? hres * 1.0001 : 0x1p-8 * 1.02 * R;
         const double ed = split == 2 ? ex * qnorm + (1.0001 * 0x1p-16 + 2.0 * dp * 0x1p-22) * 1.02 * qnorm * R +
                                            2.0 * dp * 0x1p-96 * (qnorm + R + 1.0)

@@ -339,6 +339,59 @@ __global__ __launch_bounds__(256) void k_rank_select64(const float *__restrict__
     for (int e = ncand + lane; e < nprobe; e += 64) o[e] = -1;
 }
 
+// nb <= 64, d % 4 == 0, d <= 256: the ranking in ONE exact pass, no GEMM and no
+// re-check -- lane b = centroid b, whose rows sit transposed in LDS as float4
+// [d/4][64] (lane b reads dims 4j..4j+3 of its own centroid, conflict-free);
+// the query row comes in by scalar loads (wave-uniform).  Every distance is
+// search.cpp:220-235's sequential fp32 sum of fl(q_j - c_j)^2 in j order, so
+// the (sqrt, index) keys are the ones k_rank_select64 re-checks, and one u64
+// sort of the wave's 64 keys gives the nearest nprobe.  64 distances x d dims
+// is less VALU work than the GEMM's launch plus the re-check's (SIFT1M, 10 k
+// queries: k_centroid_gemm 8 us + k_rank_select64 23 us before).
+// qpw queries per wave, one after the other (1 for small batches: the chain of a
+// wave's queries, not the VALU work, set the time -- 8 per wave ran 31 us at 10 k
+// queries and 28 us at 1.25 k)
+__global__ __launch_bounds__(256) void k_rank_exact64(const float *__restrict__ q, int64_t nq,
+                                                      const float *__restrict__ cent, int nb, int64_t d,
+                                                      int nprobe, int qpw, int32_t *out) {
+    extern __shared__ float4 Cs[];  // [d/4][64]
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nd4 = (int)(d >> 2);
+    // coalesced row reads (consecutive threads: consecutive float4 of one row)
+    for (int i = tid; i < 64 * nd4; i += 256) {
+        const int b = i / nd4, j4 = i - b * nd4;
+        Cs[j4 * 64 + b] = b < nb ? *(const float4 *)(cent + (int64_t)b * d + 4 * j4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __syncthreads();
+    const int64_t q0 = (int64_t)blockIdx.x * (4 * qpw) + w * qpw;
+    for (int r = 0; r < qpw; ++r) {
+        const int64_t qi = q0 + r;
+        if (qi >= nq) break;
+        const float4 *qr = (const float4 *)(q + qi * d);
+        float acc = 0.0f;
+#pragma unroll 8
+        for (int j4 = 0; j4 < nd4; ++j4) {
+            const float4 qv = qr[j4], cv = Cs[j4 * 64 + lane];
+            float df = qv.x - cv.x;
+            acc = acc + df * df;
+            df = qv.y - cv.y;
+            acc = acc + df * df;
+            df = qv.z - cv.z;
+            acc = acc + df * df;
+            df = qv.w - cv.w;
+            acc = acc + df * df;
+        }
+        const u64 key = wave_sort64(lane < nb ? make_key(__fsqrt_rn(acc), lane) : kEmptyKey);
+        int32_t *o = out + qi * nprobe;
+        if (lane < nprobe) o[lane] = key == kEmptyKey ? -1 : key_gid(key);
+        for (int e = 64 + lane; e < nprobe; e += 64) o[e] = -1;
+    }
+}
+static bool rank_exact64_ok(const float *q, const float *cent, int64_t nb, int64_t d) {
+    return nb <= 64 && d % 4 == 0 && d <= 256 && ((uintptr_t)q & 15) == 0 && ((uintptr_t)cent & 15) == 0;
+}
+
 // -------------------------------------------------------------- probe select
 template <int R>
 __global__ __launch_bounds__(256) void k_select_nearest(const float *__restrict__ s, int64_t n,
@@ -529,6 +582,14 @@ int lira_rank_nearest(const float *q, int64_t nq, const float *centroids, int64_
     if (nprobe <= 0 || R < 0) return fail(LIRA_EUNSUPPORTED, "nprobe must be in [1, 256]");
     if (nq == 0) return LIRA_OK;
     if (!q || !centroids || !out_probe) return fail(LIRA_EINVAL, "NULL buffer");
+    if (rank_exact64_ok(q, centroids, n_centroids, d)) {  // (no workspace needed)
+        const int qpw = nq >= 8192 ? 2 : 1;
+        const unsigned g = (unsigned)((nq + 4 * qpw - 1) / (4 * qpw));
+        hipLaunchKernelGGL(k_rank_exact64, dim3(g), dim3(256), (size_t)d * 64 * 4, (hipStream_t)stream, q, nq,
+                           centroids, (int)n_centroids, d, (int)nprobe, qpw, out_probe);
+        LIRA_HIP_TRY(hipGetLastError());
+        return LIRA_OK;
+    }
     size_t need = 0;
     lira_rank_workspace_size(nq, n_centroids, &need);
     hipStream_t st = (hipStream_t)stream;

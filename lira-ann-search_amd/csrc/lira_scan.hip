@@ -61,7 +61,7 @@ struct ScanArgs {
     uint32_t *qbound;     // [nq] f2ord(k-th score) published per query, ~0 = none; NULL = off
     int64_t d, dpad;
     int n_lists, n_virt, nprobe, k, bpc, nch_max;
-    int prune;            // L2 early abandon (off: LIRA_SCAN_NO_PRUNE, or env LIRA_SCAN_PRUNE=0)
+    int prune;            // L2 early abandon (off: LIRA_SCAN_NO_PRUNE, or LIRA_OPT_PRUNE = 0)
     unsigned long long *stats;  // NULL, or the work counters of lira_index_set_stats
     const float *pivot;   // L2: per-list pivot (n_lists x d) and per-tile radius bounds
     const float2 *tstat;  //     for the triangle-inequality block skip; NULL = off
@@ -410,7 +410,7 @@ __global__ __launch_bounds__(kScanThreads, OCC) void k_scan(ScanArgs a) {
 
         // Triangle-inequality block skip (L2).  For a candidate x of list p with
         // pivot c_p: ||q - x|| >= | ||q - c_p|| - ||x - c_p|| |.  The index keeps
-        // per tile bounds lo <= ||x - c_p|| <= hi (k_tile_stats), so a block whose
+        // per tile bounds lo <= ||x - c_p|| <= hi (k_row_stats), so a block whose
         // radius range [lo, hi] sits farther than rad_r from ||q_r - c_p|| on
         // either side cannot hold a pair scoring <= row r's threshold T_r, with
         // rad_r = sqrt((T_r + d 2^-140) / (1 - (d+4) 2^-24)): search.cpp's fp32

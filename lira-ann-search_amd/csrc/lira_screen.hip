@@ -115,7 +115,7 @@ struct ScreenArgs {
     int bpc_near;  // blocks per chunk of group 0 (each query's nearest partition) when n_virt > n_lists
     unsigned long long *stats;  // NULL or lira_index_set_stats counters
     // L2 triangle-inequality block skip (k_screen_m): queries, per-list pivot,
-    // per-tile radius bounds (lira_abi.hip k_list_pivot / k_tile_stats); NULL = off
+    // per-tile radius bounds (lira_abi.hip k_pivot_final / k_row_stats); NULL = off
     const float *Q;
     const float *pivot;
     const float2 *tstat;
@@ -358,14 +358,34 @@ __device__ __forceinline__ int xcd_id() {
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
     return (int)(v & 7u);
 }
+// Once the claimant's queue is empty it reads all 8 claim counters at once (one
+// round trip) and steals from the first queue that still has items: walking
+// the queues with one atomic each in turn cost every workgroup up to 8
+// serial atomic round trips at the end of the scan.  tries = 8: all empty.
 __device__ __forceinline__ int claim_item(int32_t *head, const int *xq, int &x, int &tries) {
-    while (tries < 8) {
+    if (tries >= 8) return -1;
+    {
         const int i = xq[x] + atomicAdd(&head[2 + x], 1);
         if (i < xq[x + 1]) return i;
-        x = (x + 1) & 7;
-        ++tries;
     }
-    return -1;
+    for (;;) {
+        int c[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) c[r] = __hip_atomic_load(&head[2 + r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int pick = -1;
+#pragma unroll
+        for (int s = 1; s <= 8; ++s) {
+            const int r = (x + s) & 7;
+            if (pick < 0 && xq[r] + c[r] < xq[r + 1]) pick = r;
+        }
+        if (pick < 0) {
+            tries = 8;
+            return -1;
+        }
+        x = pick;
+        const int i = xq[x] + atomicAdd(&head[2 + x], 1);
+        if (i < xq[x + 1]) return i;
+    }
 }
 
 // acc += x * splat(q.lo) / splat(q.hi) on packed fp32.  Inline asm: hipcc
@@ -887,22 +907,25 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
     unsigned long long *const cnt = kPhaseClocks && (a.dbg & 8) ? nullptr : a.stats;  // (off while timing)
     __shared__ int xq[9];  // the XCD queues' bounds (k_plan)
     int qx = 0, qtries = 0, nxt = -1;  // thread 0: its queue, the claimed next item
+    int4 e_nxt = make_int4(0, 0, 0, 0);  // thread 0: the next item's table entry (loaded one item ahead)
     if (tid == 0) {
         for (int r = 0; r < 9; ++r) xq[r] = a.head[10 + r];
         qx = xcd_id();
         nxt = claim_item(a.head, xq, qx, qtries);
+        if (nxt >= 0) e_nxt = a.itab[nxt];
     }  // thread 0: the claimed next item
     for (;;) {
         if (clk) t_0 = clock64();
         if (tid == 0) {
-            // the next item is claimed one item ahead (its atomic completes
-            // under this item's work); one table load decodes it
+            // the next item is claimed, and its table entry loaded, one item
+            // ahead (both complete under this item's work)
             const int item = nxt;
             const int ok = item >= 0;
             int4 e = make_int4(0, 0, 0, 0);
             if (ok) {
-                e = a.itab[item];
+                e = e_nxt;
                 nxt = claim_item(a.head, xq, qx, qtries);
+                if (nxt >= 0) e_nxt = a.itab[nxt];
             }
             meta[0] = ok;
             meta[1] = e.x;
@@ -2743,7 +2766,7 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     }
     // Group 0 (each query's nearest partition, where pruning leaves most of
     // the work) is cut finer: its items are the heavy ones, and ~1.5 of them
-    // per workgroup left the slowest workgroup with two (env LIRA_SCAN_NEAR_ROUNDS;
+    // per workgroup left the slowest workgroup with two (LIRA_OPT_NEAR_ROUNDS;
     // measured SIFT1M mixture scan 1.08 -> 1.04 ms at 2, slower at 4 and 8:
     // more lists, more survivors)
     const int near_rounds = op.near_rounds > 0 ? op.near_rounds : 2;

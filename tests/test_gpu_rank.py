@@ -27,7 +27,10 @@ def test_centroid_dist_golden(name):
 
 
 @pytest.mark.parametrize("nq,nb,d", [(1, 8, 16), (100, 64, 128), (257, 130, 96), (33, 1024, 128),
-                                     (16, 128, 960), (70, 5, 7)])
+                                     (16, 128, 960), (70, 5, 7),
+                                     # the one-pass exact kernel (nb <= 64, d % 4 == 0, d <= 256):
+                                     # several workgroups with a partial last one, the LDS maximum
+                                     (1000, 64, 256), (65, 33, 100), (300, 64, 132), (37, 64, 260)])
 def test_gemm_bound_and_rank_nearest(nq, nb, d):
     from lira_amd import centroid_dist, centroid_gemm, rank_nearest, select_probes
     rng = np.random.default_rng(nq * 7 + nb)
@@ -41,7 +44,7 @@ def test_gemm_bound_and_rank_nearest(nq, nb, d):
     assert (np.abs(A - exact) <= err[:, None] + 1e-6 * exact).all()
     # relative accuracy of the MFMA GEMM itself (fp32, ~1e-5 with cancellation)
     assert np.allclose(A, exact, rtol=1e-3, atol=1e-3 * exact.mean())
-    for nprobe in sorted({1, min(8, nb), min(32, nb), min(nb, 64)}):
+    for nprobe in sorted({1, min(8, nb), min(32, nb), min(nb, 64), min(nb + 3, 256)}):
         got = rank_nearest(qt, ct, nprobe).cpu().numpy()
         want = oracle.probe_nearest(oracle.centroid_dist(q, c), nprobe)
         assert np.array_equal(got, want)

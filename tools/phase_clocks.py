@@ -20,6 +20,7 @@ from lira_amd.synthetic import CONFIGS, workload  # noqa: E402
 cfg, data, dbg = sys.argv[1], sys.argv[2], int(sys.argv[3])
 opts = dict((a.split("=")[0], int(a.split("=")[1])) for a in sys.argv[4:])
 N, d, B, nprobe, k, metric, nq = CONFIGS[cfg]
+nq = int(os.environ.get("NQ", nq))  # (NQ=1250: the 8-GPU strong-scaling share)
 dev = torch.device("cuda", 0)
 x, c, assign, mq = workload(cfg, 1234, dev, data)
 idx = PartitionedIndex(d, metric, 0, **opts).build(assign[:, None] if assign.dim() == 1 else assign, x, B)
