@@ -19,6 +19,10 @@ namespace lira {
 
 typedef unsigned long long u64;
 static constexpr u64 kEmptyKey = ~0ull;
+// last slot of a screen row list whose keys are NOT sorted (compact, then empty
+// keys): never a real key (its row field would be 2^32 - 2), and its score
+// field is a NaN, so no bound test takes it
+static constexpr u64 kUnsortedMark = ~0ull - 1;
 static constexpr int kWave = 64;
 
 __device__ __forceinline__ uint32_t f2ord(float s) {

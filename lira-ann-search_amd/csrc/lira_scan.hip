@@ -110,11 +110,10 @@ __global__ __launch_bounds__(256) void k_count(const int32_t *probe, int64_t npa
 // One workgroup of 1024 threads: exclusive scans over the buckets.
 // qr = queries per work item; qblk_off (optional) = exclusive scan of the
 // query blocks ceil(cnt / qr) per virtual partition.
-__global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t *tile_off,
-                                               int n_lists, int n_virt, int bpc, int bpc_near, int qr,
-                                               int32_t *qoff,
-                                               int32_t *item_off, int32_t *nch, int32_t *head,
-                                               int32_t *qblk_off, int4 *itab) {
+// (blockDim.x == 1024; plan_body is also block 0's share of k_plan_fill)
+__device__ __forceinline__ void plan_body(const int32_t *cnt, const int32_t *tile_off, int n_lists, int n_virt,
+                                          int bpc, int bpc_near, int qr, int32_t *qoff, int32_t *item_off,
+                                          int32_t *nch, int32_t *head, int32_t *qblk_off, int4 *itab) {
     __shared__ int32_t s_a[1024], s_b[1024], s_c[1024];
     __shared__ int32_t carry_a, carry_b, carry_c;
     if (threadIdx.x == 0) carry_a = carry_b = carry_c = 0;
@@ -224,6 +223,13 @@ __global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t
     }
     if (threadIdx.x == 0) head[18] = carry_b;
 }
+__global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t *tile_off,
+                                               int n_lists, int n_virt, int bpc, int bpc_near, int qr,
+                                               int32_t *qoff,
+                                               int32_t *item_off, int32_t *nch, int32_t *head,
+                                               int32_t *qblk_off, int4 *itab) {
+    plan_body(cnt, tile_off, n_lists, n_virt, bpc, bpc_near, qr, qoff, item_off, nch, head, qblk_off, itab);
+}
 
 // bucket -> pair ids.  Each block reserves its slice of every bucket once
 // (global atomic), then places its pairs by LDS-atomic rank.  The order inside
@@ -262,6 +268,63 @@ __global__ __launch_bounds__(256) void k_fill(const int32_t *probe, int64_t npai
         int p = probe[i];
         if (p < 0 || p >= n_lists) continue;
         const int v = virt_of(i, p, nprobe, split, groups, n_lists);
+        qlist[base[v] + atomicAdd(&hist[v], 1)] = (int32_t)i;
+    }
+}
+
+// k_plan and k_fill in one launch (n_virt <= kFuseMax): the fill needs only the
+// buckets' exclusive prefix sums, which every block recomputes from cnt in LDS
+// (a few scan passes over <= 2048 counts) instead of waiting on a separate
+// one-block plan kernel; block 0 also runs the plan itself (item table, queue
+// bounds, chunk counts) for the screen.  One launch and one dependency fewer
+// on the scan's critical path.
+static constexpr int kFuseMax = 2048;
+__global__ __launch_bounds__(1024) void k_plan_fill(const int32_t *probe, int64_t npairs, int n_lists, int nprobe,
+                                                    int groups, const int32_t *cnt, const int32_t *tile_off, int bpc,
+                                                    int bpc_near, int qr, int32_t *qoff, int32_t *item_off,
+                                                    int32_t *nch, int32_t *head, int32_t *qblk_off, int4 *itab,
+                                                    int32_t *cursor, int32_t *qlist) {
+    __shared__ int32_t sq[kFuseMax], hist[kFuseMax], base[kFuseMax], scan[1024];
+    __shared__ int32_t carry;
+    const int n_virt = groups * n_lists, tid = threadIdx.x;
+    if (blockIdx.x == 0)
+        plan_body(cnt, tile_off, n_lists, n_virt, bpc, bpc_near, qr, qoff, item_off, nch, head, qblk_off, itab);
+    // exclusive prefix of cnt over the virtual partitions -> sq
+    if (tid == 0) carry = 0;
+    for (int b = tid; b < n_virt; b += 1024) hist[b] = 0;
+    __syncthreads();
+    for (int b0 = 0; b0 < n_virt; b0 += 1024) {
+        const int v = b0 + tid < n_virt ? cnt[b0 + tid] : 0;
+        scan[tid] = v;
+        __syncthreads();
+        for (int off = 1; off < 1024; off <<= 1) {
+            const int o = tid >= off ? scan[tid - off] : 0;
+            __syncthreads();
+            scan[tid] += o;
+            __syncthreads();
+        }
+        if (b0 + tid < n_virt) sq[b0 + tid] = carry + scan[tid] - v;
+        __syncthreads();
+        if (tid == 1023) carry += scan[1023];
+        __syncthreads();
+    }
+    // k_fill with the local offsets
+    const int64_t s = (int64_t)blockIdx.x * kPairsPerBlock;
+    const int64_t e = min<int64_t>(npairs, s + kPairsPerBlock);
+    for (int64_t i = s + tid; i < e; i += 1024) {
+        const int p = probe[i];
+        if (p >= 0 && p < n_lists) atomicAdd(&hist[virt_of(i, p, nprobe, 1, groups, n_lists)], 1);
+    }
+    __syncthreads();
+    for (int b = tid; b < n_virt; b += 1024) {
+        base[b] = hist[b] ? sq[b] + atomicAdd(&cursor[b], hist[b]) : 0;
+        hist[b] = 0;
+    }
+    __syncthreads();
+    for (int64_t i = s + tid; i < e; i += 1024) {
+        const int p = probe[i];
+        if (p < 0 || p >= n_lists) continue;
+        const int v = virt_of(i, p, nprobe, 1, groups, n_lists);
         qlist[base[v] + atomicAdd(&hist[v], 1)] = (int32_t)i;
     }
 }
@@ -1186,6 +1249,11 @@ hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npai
     const size_t hc = nv <= kHistMax ? (size_t)nv * 4 : 0;
     const size_t hf = nv <= kHistMax / 2 ? (size_t)nv * 8 : 0;
     hipLaunchKernelGGL(k_count, dim3(pg), dim3(256), hc, st, probe, npairs, nl, nprobe, 1, groups, cnt, idx->err);
+    if (nv <= kFuseMax && qblk_off) {
+        hipLaunchKernelGGL(k_plan_fill, dim3(std::max(pg, 1u)), dim3(1024), 0, st, probe, npairs, nl, nprobe, groups, cnt,
+                           idx->tile_off, bpc, bpc_near, qr, qoff, item_off, nch, head, qblk_off, itab, cursor, qlist);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, nv, bpc, bpc_near, qr, qoff,
                        item_off, nch, head, qblk_off, itab);
     hipLaunchKernelGGL(k_fill, dim3(pg), dim3(256), hf, st, probe, npairs, nl, nprobe, 1, groups, qoff, cursor,

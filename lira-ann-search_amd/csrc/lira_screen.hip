@@ -1500,9 +1500,15 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
         // ---- flush buffers, emit lists, publish bounds (wave-owned rows);
         // buffers flushed two rows per network pass (one row per half-wave:
         // the per-item epilogue was ~8 % of the screen's cycles on SIFT1M latent)
+        // A row whose list is still empty and whose buffer holds fewer than k keys
+        // is NOT merged: its keys go out unsorted, marked by kUnsortedMark in the
+        // list's last slot (k_smerge then walks the list to its first empty key).
+        // Merging could not give it a k-th key to publish either, so the bounds
+        // are unchanged; the merges were most of the item epilogue (SIFT1M
+        // mixture at 1.25 k queries: 16 % of the screen's cycles).
         {
             const int nb = lane < 16 ? m_bufc[wave * 16 + lane] : 0;
-            u64 pend = __ballot(lane < 16 && nb > 0);
+            u64 pend = __ballot(lane < 16 && nb > 0 && (nb >= k || lists[(wave * 16 + lane) * K2] != kEmptyKey));
             while (pend) {
                 const int ra = __builtin_ctzll(pend);
                 pend &= pend - 1;
@@ -1526,7 +1532,10 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
             const int pr = m_pair[row];
             if (pr >= 0) {
                 u64 *dst = a.partial + ((int64_t)pr * a.nch_max + ch) * K2;
-                for (int e = lane; e < K2; e += 64) dst[e] = lists[row * K2 + e];
+                const int nb = m_bufc[row];
+                const bool uns = nb > 0 && nb < k && lists[row * K2] == kEmptyKey;  // (not merged above)
+                for (int e = lane; e < K2; e += 64)
+                    dst[e] = !uns ? lists[row * K2 + e] : e < nb ? bufs[row * BC + e] : e == K2 - 1 ? kUnsortedMark : kEmptyKey;
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -2451,15 +2460,20 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
     const int k = a.k, K2 = a.K2;
     const double dd = (double)a.d;
     const float *qrow = a.Q + q * a.d;
-    double qs = 0.0;
-    for (int64_t j = lane; j < a.d; j += 64) {
-        const double x = (double)qrow[j];
-        qs = __builtin_fma(x, x, qs);
-    }
+    // ||q|| only where the lists' error bound is recomputed on uncentred vectors
+    // (centred: the per-pair norms pqn; a round trip off the merge's chain otherwise)
+    double qnorm = 0.0;
+    if (!a.centred) {
+        double qs = 0.0;
+        for (int64_t j = lane; j < a.d; j += 64) {
+            const double x = (double)qrow[j];
+            qs = __builtin_fma(x, x, qs);
+        }
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) qs += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, qs), m));
-    // rounded up by more than any summation-order difference to k_qstage's value
-    const double qnorm = __builtin_sqrt(qs) * (1.0 + 0x1p-30);
+        for (int m = 32; m >= 1; m >>= 1) qs += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, qs), m));
+        // rounded up by more than any summation-order difference to k_qstage's value
+        qnorm = __builtin_sqrt(qs) * (1.0 + 0x1p-30);
+    }
     const int32_t *prow = a.probe + q * a.nprobe;
     const int32_t *plv = a.plive ? a.plive + q * a.nprobe : prow;  // the pairs that have lists
     uint32_t *pend = s_pend[w];
@@ -2534,14 +2548,15 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
             }
             const u64 *src = a.partial + ((q * a.nprobe + (p >= 0 ? s : 0)) * (int64_t)NC + (p >= 0 ? c : 0)) * K2;
             double lim = 0.0;
-            bool over = false;
+            bool over = false, uns = a.unsorted != 0;
             if (p >= 0) {
                 const double qn_s = a.centred ? (double)a.pqn[q * a.nprobe + s] : qnorm;
                 const double E = a.pE ? (double)a.pE[(q * a.nprobe + s) * (int64_t)NC + c]
                                       : err_E<METRIC>(qn_s, (double)a.rmax[p], dd, a.split, (double)a.dpad, a.centred);
                 lim = s_lim<METRIC>((double)T, E, dd);
                 const u64 last = src[K2 - 1];
-                over = last != kEmptyKey && (double)key_score(last) <= lim;
+                over = last != kEmptyKey && (double)key_score(last) <= lim;  // (kUnsortedMark: a NaN score)
+                uns = uns || last == kUnsortedMark;  // an unmerged row buffer (k_screen_m): walk to its first empty key
             }
             bool active = p >= 0 && !over;
             // four keys per round (two 16-B loads; K2 % 4 == 0, lists 32-B aligned):
@@ -2560,7 +2575,7 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
                     bool take = false;
                     if (active) {
                         take = kv[u] != kEmptyKey && (double)key_score(kv[u]) <= lim;
-                        active = a.unsorted ? kv[u] != kEmptyKey : take;
+                        active = uns ? kv[u] != kEmptyKey : take;
                     }
                     add(take, (uint32_t)kv[u]);
                 }
