@@ -551,7 +551,8 @@ def sweep_options(args, index, local_step, D, I, nq, nprobe, k):
 def time_pipeline(args, oracle, index, x, centres, q, make_queries, k, nprobe, metric, host, rows, Igt, dev):
     """search.cpp:424-514 per batch: exact distances + standardise (one HIP
     kernel) -> MLP_2_Input (PyTorch-ROCm) -> score >= 0.5 with argmax fallback
-    (lira_select_probes) -> scan + top-k, eagerly and as one replayed HIP graph.
+    (lira_select_probes), nearest probed centroid first (lira_order_probes) ->
+    scan + top-k, eagerly and as one replayed HIP graph.
     The MLP is fitted (untimed) to score each query's nprobe nearest centroids,
     standing in for LIRA's kNN-label training (out of scope)."""
     from lira_amd import centroid_dist
@@ -605,8 +606,14 @@ def time_pipeline(args, oracle, index, x, centres, q, make_queries, k, nprobe, m
         from lira_amd import _lib
         _lib.call("lira_select_probes", _lib.ptr(pipe.scores), nq, B, pipe.mode, 0.5,
                   pipe.max_probe, _lib.ptr(pipe.probe), _lib.ptr(pipe.nprobe), _lib.stream_ptr())
+        torch.addcmul(pipe.mean, pipe.dist, pipe.scale, out=pipe.raw)  # (as ProbePipeline: nearest first)
+        _lib.call("lira_order_probes", _lib.ptr(pipe.probe), nq, pipe.max_probe, _lib.ptr(pipe.raw), B,
+                  _lib.stream_ptr())
         ev[3].record()
+        old_hint = index.get_option("probes_hint")
+        index.set_option("probes_hint", pipe.expect_probes)  # (the pipeline's own scan setting)
         index.search(pipe.q, pipe.probe, k, dedup=True, out=(pipe.D, pipe.I, pipe.ncand))
+        index.set_option("probes_hint", old_hint)
         ev[4].record()
         torch.cuda.synchronize()
         for i, name in enumerate(parts):
@@ -630,6 +637,7 @@ def time_pipeline(args, oracle, index, x, centres, q, make_queries, k, nprobe, m
     npb = pipe.nprobe.float().mean().item()
     return {"what": "search.cpp:424-514 on the batch: lira_centroid_dist (exact + standardise) -> MLP_2_Input "
                     "(torch) -> lira_select_probes (>= 0.5, argmax fallback) -> lira_scan_topk",
+            "probe_order": "lira_order_probes: the selected set by ascending raw centroid distance",
             "value_eager": nq / eager_s, "value_graph": nq / graph_s, "unit": "queries/s",
             "ms_eager": eager_s * 1e3, "ms_graph": graph_s * 1e3, "graph_same_output": same,
             "stage_ms": parts, "max_probe": pipe.max_probe,

@@ -241,6 +241,19 @@ int lira_rank_nearest(const float *q, int64_t nq, const float *centroids, int64_
 int lira_select_probes(const float *scores, int64_t n, int64_t n_centroids, int mode, float thr,
                        int64_t max_probe, int32_t *out_probe, int32_t *out_nprobe, void *stream);
 
+/*
+ * Reorder every row of a probe matrix (n, max_probe) int32, -1 padded, in place
+ * by ascending key[i * n_centroids + b] (ties -> smaller b; -1 entries last):
+ * the same probe SET, nearest partition first when key is the query ->
+ * centroid distance.  No result of lira_scan_topk depends on the slot order,
+ * but its speed does: slot 0 seeds the query's starting bound and forms the
+ * nearest-probe group (a threshold selection in score order put an arbitrary
+ * one of the probed partitions there; search.cpp:447-466 probes in bucket
+ * order).  max_probe <= 256.  Stream-ordered, graph-capturable.
+ */
+int lira_order_probes(int32_t *probe, int64_t n, int64_t max_probe, const float *key, int64_t n_centroids,
+                      void *stream);
+
 /* -------------------------------------------------------------- scan */
 /*
  * Batched candidate scan + exact top-k over the probed buckets.

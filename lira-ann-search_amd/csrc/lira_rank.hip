@@ -523,6 +523,30 @@ __global__ __launch_bounds__(256) void k_select_threshold_sorted(const float *__
     if (out_np && lane == 0) out_np[i] = mm;
 }
 
+// lira_order_probes: one wave per row; keys (f2ord(key[b]) << 32 | b), -1 slots
+// as empty keys (sorted last), one wave-wide sort of the row's R*64 keys
+template <int R>
+__global__ __launch_bounds__(256) void k_order_probes(int32_t *probe, int64_t n, int mp, const float *__restrict__ key,
+                                                      int nb) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n) return;
+    int32_t *row = probe + i * mp;
+    u64 v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = r * 64 + lane;
+        const int b = e < mp ? row[e] : -1;
+        v[r] = b >= 0 && b < nb ? ((u64)f2ord(key[i * nb + b]) << 32) | (uint32_t)b : kEmptyKey;
+    }
+    wave_sort<R>(v);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = r * 64 + lane;
+        if (e < mp) row[e] = v[r] == kEmptyKey ? -1 : (int32_t)(uint32_t)v[r];
+    }
+}
+
 static int sel_r(int64_t np) { return np <= 64 ? 1 : np <= 128 ? 2 : np <= 256 ? 4 : -1; }
 
 }  // namespace lira
@@ -623,6 +647,26 @@ int lira_rank_nearest(const float *q, int64_t nq, const float *centroids, int64_
     }
     if (own) hipFreeAsync(ws, st);
     return rc;
+}
+
+int lira_order_probes(int32_t *probe, int64_t n, int64_t max_probe, const float *key, int64_t n_centroids,
+                      void *stream) {
+    if (n < 0 || n_centroids <= 0 || max_probe <= 0) return fail(LIRA_EINVAL, "bad shape");
+    const int R = sel_r(max_probe);
+    if (R < 0) return fail(LIRA_EUNSUPPORTED, "lira_order_probes supports max_probe <= 256");
+    if (n_centroids > INT32_MAX) return fail(LIRA_EUNSUPPORTED, "too many centroids");
+    if (n == 0) return LIRA_OK;
+    if (!probe || !key) return fail(LIRA_EINVAL, "NULL buffer");
+    const dim3 g((unsigned)((n + 3) / 4));
+    hipStream_t st = (hipStream_t)stream;
+    if (R == 1)
+        hipLaunchKernelGGL(k_order_probes<1>, g, dim3(256), 0, st, probe, n, (int)max_probe, key, (int)n_centroids);
+    else if (R == 2)
+        hipLaunchKernelGGL(k_order_probes<2>, g, dim3(256), 0, st, probe, n, (int)max_probe, key, (int)n_centroids);
+    else
+        hipLaunchKernelGGL(k_order_probes<4>, g, dim3(256), 0, st, probe, n, (int)max_probe, key, (int)n_centroids);
+    LIRA_HIP_TRY(hipGetLastError());
+    return LIRA_OK;
 }
 
 int lira_select_probes(const float *scores, int64_t n, int64_t n_centroids, int mode, float thr,

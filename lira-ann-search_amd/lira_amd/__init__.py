@@ -13,11 +13,11 @@ liblira_hip.so), with the reference's Python-side interfaces on top:
 """
 from ._lib import LiraError, load as load_library  # noqa: F401
 from .index import (PartitionedIndex, build_csr, centroid_dist, centroid_gemm,  # noqa: F401
-                    normalize_metric, rank_nearest, select_probes, RankWorkspace)
+                    normalize_metric, order_probes, rank_nearest, select_probes, RankWorkspace)
 from .faiss_compat import IndexFlatIP, IndexFlatL2  # noqa: F401
 
 __all__ = [
     "LiraError", "PartitionedIndex", "build_csr", "centroid_dist", "centroid_gemm",
-    "rank_nearest", "select_probes", "normalize_metric", "IndexFlatL2", "IndexFlatIP",
+    "rank_nearest", "select_probes", "order_probes", "normalize_metric", "IndexFlatL2", "IndexFlatIP",
     "RankWorkspace", "load_library",
 ]

@@ -366,6 +366,23 @@ def rank_nearest(q: torch.Tensor, centroids: torch.Tensor, nprobe: int, out=None
     return out
 
 
+def order_probes(probe: torch.Tensor, key: torch.Tensor, stream=None) -> torch.Tensor:
+    """Reorder each row of an (n, max_probe) -1 padded probe matrix IN PLACE by
+    ascending key[i, b] (ties -> smaller b, -1 last): lira_order_probes.  Same
+    probe sets, so the same scan results; with key = query -> centroid distance
+    the scan sees each query's nearest probed partition first (its seed and
+    nearest-probe group).  Returns probe."""
+    if probe.dtype != torch.int32 or not probe.is_contiguous():
+        raise ValueError("probe must be a contiguous int32 tensor")
+    k = _dev(key, torch.float32, probe.device)
+    n, mp = probe.shape
+    if k.shape[0] != n:
+        raise ValueError("key rows != probe rows")
+    with torch.cuda.device(probe.device):
+        _lib.call("lira_order_probes", _lib.ptr(probe), n, mp, _lib.ptr(k), k.shape[1], _lib.stream_ptr(stream))
+    return probe
+
+
 def select_probes(scores: torch.Tensor, mode: str, max_probe: int, threshold: float = 0.0,
                   stream=None, by_score: bool = False):
     """Probe lists from an (n, B) score matrix.

@@ -231,3 +231,26 @@ def test_search_engine_results_do_not_alias():
         pr, cnt = oracle.probe_threshold(s, thr)
         assert np.array_equal(n.cpu().numpy(), cnt)
     assert eng.index.get_option("probes_hint") == 0
+
+
+@pytest.mark.parametrize("mp,nb", [(8, 16), (64, 64), (100, 130), (256, 300)])
+def test_order_probes_matches_numpy(mp, nb):
+    # lira_order_probes: each row's valid probes by ascending key (ties -> smaller
+    # bucket), -1 slots last; the probe set is unchanged
+    from lira_amd import order_probes
+    rng = np.random.default_rng(mp + nb)
+    n = 300
+    key = rng.integers(0, 50, (n, nb)).astype(np.float32)  # many exact ties
+    key[:, 3] = -0.0
+    key[:, 5] = 0.0
+    probe = np.full((n, mp), -1, np.int32)
+    for i in range(n):
+        m = int(rng.integers(0, min(mp, nb) + 1))
+        probe[i, :m] = rng.permutation(nb)[:m]
+        rng.shuffle(probe[i])  # -1 slots anywhere
+    got = order_probes(torch.from_numpy(probe).cuda(), torch.from_numpy(key).cuda()).cpu().numpy()
+    for i in range(n):
+        v = probe[i][probe[i] >= 0]
+        kk = key[i, v] + np.float32(0.0)  # (-0 orders as +0)
+        want = v[np.lexsort((v, kk))]
+        assert np.array_equal(got[i, :len(want)], want) and (got[i, len(want):] == -1).all()
