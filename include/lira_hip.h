@@ -145,7 +145,8 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *                        rows where it applies (k <= 32, d <= 256, two groups); 0 off
  *   LIRA_OPT_SHARE       per-block exchange of query bounds between work items (1)
  *   LIRA_OPT_ROUNDS      work items per workgroup target (0 = kernel default)
- *   LIRA_OPT_NEAR_ROUNDS the same for the nearest-probe group (default 2)
+ *   LIRA_OPT_NEAR_ROUNDS the same for the nearest-probe group: 0 (default) auto -- the plan
+ *                        picks 2..6 from the seed's estimate of the blocks the batch will screen; n fixed
  *   LIRA_OPT_MFMA        screen engine: 1 auto (default), 0 VALU, 2 MFMA wherever it fits
  *   LIRA_OPT_DEBUG       timing experiments only (results invalid): bit mask, see lira_screen.hip.
  *                        Production builds accept only 0 and return LIRA_EUNSUPPORTED otherwise;

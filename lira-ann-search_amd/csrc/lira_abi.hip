@@ -245,8 +245,14 @@ __global__ __launch_bounds__(64) void k_row_stats(const float *Xr, const int32_t
 
 // Per list: the (min, max) of its tiles' radius ranges (+inf, -inf for an
 // empty list) -- one wave per list.
-__global__ __launch_bounds__(64) void k_list_stats(const float2 *tstat, const int32_t *tile_off, float2 *lstat) {
+__global__ __launch_bounds__(64) void k_list_stats(const float2 *tstat, const int32_t *tile_off, float2 *lstat,
+                                                   float2 *lsamp) {
     const int b = blockIdx.x, lane = threadIdx.x;
+    if (lsamp && lane < 16) {  // tile (lane * tiles / 16)'s range ((+inf, -inf) for an empty list)
+        const int t0 = tile_off[b], nt = tile_off[b + 1] - t0;
+        lsamp[b * 16 + lane] = nt > 0 ? tstat[t0 + (int)(((int64_t)lane * nt) / 16)]
+                                      : make_float2(__builtin_inff(), -__builtin_inff());
+    }
     float lo = __builtin_inff(), hi = -__builtin_inff();
     for (int t = tile_off[b] + lane; t < tile_off[b + 1]; t += 64) {
         const float2 v = tstat[t];
@@ -338,6 +344,8 @@ static void free_storage(lira_index *idx) {
     if (idx->pivot) hipFree(idx->pivot);
     if (idx->tstat) hipFree(idx->tstat);
     if (idx->lstat) hipFree(idx->lstat);
+    if (idx->lsamp) hipFree(idx->lsamp);
+    idx->lsamp = nullptr;
     idx->pivot = nullptr;
     idx->tstat = nullptr;
     idx->lstat = nullptr;
@@ -515,6 +523,7 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
             if (hipMalloc(&idx->pivot, (size_t)n_lists * d * 4) != hipSuccess ||
                 hipMalloc(&idx->tstat, (size_t)tiles * sizeof(float2)) != hipSuccess ||
                 hipMalloc(&idx->lstat, (size_t)n_lists * sizeof(float2)) != hipSuccess ||
+                hipMalloc(&idx->lsamp, (size_t)n_lists * 16 * sizeof(float2)) != hipSuccess ||
                 hipMalloc(&d_seg, (size_t)std::max<int64_t>(segs, 1) * 4) != hipSuccess ||
                 hipMalloc(&d_segf, (size_t)(n_lists + 1) * 4) != hipSuccess ||
                 hipMalloc(&d_psum, (size_t)std::max<int64_t>(segs, 1) * d * 8) != hipSuccess) {
@@ -624,7 +633,7 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
         }
         if (e == hipSuccess && l2) {
             hipLaunchKernelGGL(k_list_stats, dim3((unsigned)n_lists), dim3(64), 0, st, idx->tstat, idx->tile_off,
-                               idx->lstat);
+                               idx->lstat, idx->lsamp);
             e = hipGetLastError();
         }
         if (e == hipSuccess && idx->Xb) {
@@ -728,7 +737,7 @@ int lira_index_set_option(lira_index *idx, int option, int64_t value) {
         case LIRA_OPT_SEED: if (!in(0, 3)) break; o.seed = v; return LIRA_OK;
         case LIRA_OPT_SHARE: if (!in(0, 1)) break; o.share = v; return LIRA_OK;
         case LIRA_OPT_ROUNDS: if (!in(0, 1024)) break; o.rounds = v; return LIRA_OK;
-        case LIRA_OPT_NEAR_ROUNDS: if (!in(1, 1024)) break; o.near_rounds = v; return LIRA_OK;
+        case LIRA_OPT_NEAR_ROUNDS: if (!in(0, 1024)) break; o.near_rounds = v; return LIRA_OK;
         case LIRA_OPT_MFMA: if (!in(0, 2)) break; o.mfma = v; return LIRA_OK;
         case LIRA_OPT_DEBUG:
             if (!in(0, 255)) break;

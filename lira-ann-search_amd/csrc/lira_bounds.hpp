@@ -110,13 +110,24 @@ __device__ __forceinline__ float row_h(double lim, double qn, double qnorm, doub
 // candidates of its slot-0 list score <= T) cannot hold a top-k candidate, so
 // it gets probe_live = -1 and no work item (the test is k_screen_m's per-block
 // skip over the list's radius range).  Slot 0 (the seed's own list) stays.
-__device__ __forceinline__ void pair_record(const float *Q, int64_t d, int64_t pair, bool valid, int praw,
-                                            int nprobe, int n_lists, const float *pivot, int centred,
-                                            const float2 *lstat, uint32_t qb, int32_t *probe_live, float4 *QN,
-                                            float *QE, float *pqn, uint16_t *QH, int64_t dpad) {
+// (est_size / est_samp set) returns, in every lane of the pair's 16, an
+// estimate of the screen blocks the pair will compute: its whole list for slot
+// 0, else the share of 16 evenly spaced tiles of its (radius-ordered) list whose
+// radius range meets the query's triangle interval under the seed bound -- the
+// plan sizes the nearest-probe group's items from the batch's total (0 for an
+// invalid or filtered pair)
+__device__ __forceinline__ int pair_record(const float *Q, int64_t d, int64_t pair, bool valid, int praw,
+                                           int nprobe, int n_lists, const float *pivot, int centred,
+                                           const float2 *lstat, uint32_t qb, int32_t *probe_live, float4 *QN,
+                                           float *QE, float *pqn, uint16_t *QH, int64_t dpad,
+                                           const int32_t *est_size = nullptr, const float2 *est_samp = nullptr) {
     const int sub = threadIdx.x & 15;
     const int p = praw < n_lists ? praw : -1;  // (an id >= n_lists passes through: k_count reports it)
     const int64_t q = valid ? pair / nprobe : 0;
+    // (estimate) this lane's sample tile of the list and the list's size, loaded ahead
+    const bool est_on = est_size && p >= 0;
+    const float2 ts = est_on ? est_samp[p * 16 + sub] : make_float2(0.0f, 0.0f);
+    const int lsz = est_on ? est_size[p] : 0;
     double s = 0.0, t = 0.0, e = 0.0;
     if (p >= 0 && (QN || lstat)) {
         const float *qr = Q + q * d, *pv = pivot ? pivot + (int64_t)p * d : nullptr;
@@ -148,9 +159,11 @@ __device__ __forceinline__ void pair_record(const float *Q, int64_t d, int64_t p
         t += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, t), m));
         e += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, e), m));
     }
-    if (sub != 0 || !valid) return;
+    // (the interval math runs in lane 0 of the pair only, unless the estimate needs it in all 16)
+    if (!est_size && (sub != 0 || !valid)) return 0;
     int live = p;
     const float dq = (float)__builtin_sqrt(t);
+    float fa = -__builtin_inff(), fb = __builtin_inff();  // the triangle interval
     if (p >= 0 && lstat && (int)(pair % nprobe) >= 1) {
         const double dd = (double)d, F = 1.0 - (dd + 4.0) * kU;
         if (qb != ~0u && F > 0.5) {
@@ -160,17 +173,28 @@ __device__ __forceinline__ void pair_record(const float *Q, int64_t d, int64_t p
                 double A = (double)dq * (1.0 - 0x1p-22) - rad, B = (double)dq * (1.0 + 0x1p-22) + rad;
                 A -= __builtin_fabs(A) * 0x1p-50;
                 B += __builtin_fabs(B) * 0x1p-50;
+                fa = __double2float_rd(A);
+                fb = __double2float_ru(B);
                 const float2 ls = lstat[p];
-                if (ls.y < __double2float_rd(A) || ls.x > __double2float_ru(B)) live = -1;
+                if (ls.y < fa || ls.x > fb) live = -1;
             }
         }
     }
+    int est = 0;
+    if (est_size) {
+        const bool hit = est_on && valid && live >= 0 && !(ts.y < fa || ts.x > fb);
+        const unsigned long long bal = __ballot(hit);
+        const int hits = __builtin_popcount((unsigned)((bal >> (threadIdx.x & 48)) & 0xffffu));  // (this pair's 16 lanes)
+        est = (int)(((int64_t)((lsz + 255) / 256) * hits) / 16);  // blocks of 4 tiles
+    }
+    if (sub != 0 || !valid) return est;
     probe_live[pair] = praw >= n_lists ? praw : live;
-    if (live < 0) return;
+    if (live < 0) return est;
     const float qnu = __double2float_ru(__builtin_sqrt(s) * (1.0 + 0x1p-40));
     if (QN) QN[pair] = make_float4((float)s, qnu, __int_as_float((int)pair), dq);
     if (QE) QE[pair] = __double2float_ru(__builtin_sqrt(e) * (1.0 + 0x1p-40));
     if (pqn) pqn[pair] = qnu;
+    return est;
 }
 
 }  // namespace lira

@@ -45,7 +45,7 @@ struct lira_opts {
     int seed = 1;
     int share = 1;
     int rounds = 0;
-    int near_rounds = 2;
+    int near_rounds = 0;  // 0: auto (the plan sizes group 0 from the seed's work estimate, between 2 and 6 rounds)
     int mfma = 1;
     int debug = 0;
     int pipeline = 0;
@@ -79,6 +79,7 @@ struct lira_index_impl {
     float2 *tstat = nullptr;
     // per list: (min, max) of its tiles' radius ranges (the scan's pair filter)
     float2 *lstat = nullptr;
+    float2 *lsamp = nullptr;  // [n_lists][16] radius ranges of 16 evenly spaced tiles (k_list_stats): the seed's work estimate
     // For the screened scan (lira_screen.hip): per storage row xadj = ||x||^2 / 2
     // (L2, the fp32 rounding of the double sum, halved) or 0 (IP), +inf for
     // padding rows; per list rmax >= max ||x|| over its rows (rounded up).

@@ -81,7 +81,7 @@ hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npai
                        int bpc_near,
                        int qr, int groups, int32_t *cnt, int32_t *cursor, int32_t *qoff, int32_t *item_off,
                        int32_t *nch, int32_t *head, int32_t *qlist, int32_t *qblk_off, int4 *itab,
-                       hipStream_t st);
+                       hipStream_t st, int bpc_near_min, int workers);
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -815,6 +815,7 @@ struct SMergeArgs {
     const float *pqn;
     unsigned long long *stats;
     int unsorted;  // a list may hold its keys unsorted (k_screen_v): walk it to its first empty key
+    const int32_t *head;  // head[19]: group 0's chunk size as the plan chose it
 };
 
 // exact score of the candidate at storage row pos (search.cpp:253-269 order)
@@ -906,6 +907,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
     const bool clk = kPhaseClocks && (a.dbg & 8) && tid == 0;
     unsigned long long *const cnt = kPhaseClocks && (a.dbg & 8) ? nullptr : a.stats;  // (off while timing)
     __shared__ int xq[9];  // the XCD queues' bounds (k_plan)
+    const int bpc_near_d = __builtin_amdgcn_readfirstlane(a.head[19]);  // group 0's chunk size (plan_body)
     int qx = 0, qtries = 0, nxt = -1;  // thread 0: its queue, the claimed next item
     int4 e_nxt = make_int4(0, 0, 0, 0);  // thread 0: the next item's table entry (loaded one item ahead)
     if (tid == 0) {
@@ -955,7 +957,7 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
 
         const int tile0 = __builtin_amdgcn_readfirstlane(a.tile_off[p]);
         const int ntl = __builtin_amdgcn_readfirstlane(a.tile_off[p + 1]) - tile0;
-        const int bpc = vp < a.n_lists && a.n_virt > a.n_lists ? a.bpc_near : a.bpc;
+        const int bpc = vp < a.n_lists && a.n_virt > a.n_lists ? bpc_near_d : a.bpc;
         const int tb_begin = ch * bpc * kSBT;
         const int tb_end = min(ntl, tb_begin + bpc * kSBT);
         const double R = (double)a.rmax[p];
@@ -2338,6 +2340,9 @@ struct SeedPairs {
     float *QE;
     float *pqn;
     uint16_t *QH;
+    const int32_t *list_size;  // (non-null) estimate the blocks each pair will screen (pair_record,
+    const float2 *lsamp;       //   from lira_index::lsamp) on every 8th query, summed into
+    unsigned int *work;        //   work[(q / 8) % 64] (the plan adds the 64 up and scales by 8)
 };
 template <int METRIC, int NT = kSeedTiles, bool PAIRS = false>
 __global__ __launch_bounds__(256) void k_seed_t(const float *Q, const int32_t *probe, int nprobe, int n_lists,
@@ -2351,13 +2356,22 @@ __global__ __launch_bounds__(256) void k_seed_t(const float *Q, const int32_t *p
     const uint32_t qb = B < __builtin_inff() ? f2ord(B) : ~0u;
     if (PAIRS) {
         if (lane == 0) qbound[q] = qb;
+        // the work estimate on every 8th query (a statistic: the plan scales it by 8)
+        const bool samp = sp.work && (q & 7) == 0;
+        int est = 0;
         for (int s0 = 0; s0 < nprobe; s0 += 4) {
             const int slot = s0 + (lane >> 4);
             const bool valid = slot < nprobe;
             const int64_t pair = q * nprobe + (valid ? slot : 0);
             const int praw = valid ? probe[pair] : -1;
-            pair_record(Q, d, pair, valid, praw, nprobe, n_lists, sp.pivot, sp.centred, sp.lstat, qb, sp.probe_live,
-                        sp.QN, sp.QE, sp.pqn, sp.QH, dpad);
+            est += pair_record(Q, d, pair, valid, praw, nprobe, n_lists, sp.pivot, sp.centred, sp.lstat, qb,
+                               sp.probe_live, sp.QN, sp.QE, sp.pqn, sp.QH, dpad, samp ? sp.list_size : nullptr,
+                               sp.lsamp);
+        }
+        if (samp) {  // lanes 0, 16, 32, 48 hold their pair groups' sums
+            const int tot = __builtin_amdgcn_readlane(est, 0) + __builtin_amdgcn_readlane(est, 16) +
+                            __builtin_amdgcn_readlane(est, 32) + __builtin_amdgcn_readlane(est, 48);
+            if (lane == 0 && tot) atomicAdd(sp.work + ((q >> 3) & 63), (unsigned)tot);
         }
     } else if (lane == 0 && qb != ~0u) {
         qbound[q] = qb;
@@ -2511,7 +2525,7 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
     auto rescan = [&](int s, int p, int c, float T) {
         ++n_rescans;
         flush_pending();
-        const int bpc = a.groups == 2 && s == 0 ? a.bpc_near : a.bpc;
+        const int bpc = a.groups == 2 && s == 0 ? a.head[19] : a.bpc;
         const int tile0 = a.tile_off[p], ntl = a.tile_off[p + 1] - tile0;
         const int t0 = c * bpc * kSBT, t1 = min(ntl, t0 + bpc * kSBT);
         for (int t = t0; t < t1; ++t) {
@@ -2538,9 +2552,12 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
     // key is within lim may have dropped a needed candidate and is re-scanned
     // exactly instead.
     auto take_lists = [&](int s_lo, int s_hi, float T) {
-        const int NC = a.nch_max, NL = (s_hi - s_lo) * NC;
+        // NC: the partial lists' chunk stride; NCe: the most chunks any bucket has
+        // in this batch (head[20], the plan's), so no lane walks a chunk slot that
+        // cannot exist
+        const int NC = a.nch_max, NCe = a.head ? max(1, min(NC, a.head[20])) : NC, NL = (s_hi - s_lo) * NCe;
         for (int l0 = 0; l0 < NL; l0 += 64) {
-            const int li = l0 + lane, s = s_lo + li / NC, c = li % NC;
+            const int li = l0 + lane, s = s_lo + li / NCe, c = li % NCe;
             int p = -1;
             if (li < NL) {
                 p = plv[s];
@@ -2585,7 +2602,7 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
                 const int ln = __builtin_ctzll(ov);
                 ov &= ov - 1;
                 const int li2 = l0 + ln;
-                rescan(s_lo + li2 / NC, plv[s_lo + li2 / NC], li2 % NC, T);
+                rescan(s_lo + li2 / NCe, plv[s_lo + li2 / NCe], li2 % NCe, T);
             }
         }
     };
@@ -2667,6 +2684,7 @@ static int screen_smem(int qr, int rl) {
 
 struct SPlan {
     int rl = 1, qr = 64, K2 = 32, bpc = 1, bpc_near = 1, nch_max = 1, grid = 1, smem = 0, mfma = 1, split = 0;
+    int bpc_near_min = 1, workers = 1;  // the plan picks group 0's chunk size in [bpc_near_min, bpc_near]
     int v2 = 0, ns = 2, bc = 32;  // the pipelined split screen (k_screen_s): ring slots, buffer keys per row
     int pp = 0;                   // per-pair query records (QN / QE / QH per pair, k_pairs or k_seed_t<.., PAIRS>)
                                   // instead of k_qstage's per-block copy: the hi x hi k_screen_m and the wide screens
@@ -2806,7 +2824,21 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
         pl.bpc = std::min(pl.bpc, SSmem2<64, 1, 4, 32>::kBR);
         pl.bpc_near = std::min(pl.bpc_near, pl.bpc);
     }
-    pl.nch_max = (int)((max_blocks + pl.bpc_near - 1) / pl.bpc_near);
+    // k_screen_m + k_smerge with the default near_rounds: the plan picks group 0's
+    // chunk size on the device (plan_body) from the seed's estimate of the blocks
+    // the batch will screen, down to 6 rounds' worth
+    pl.workers = (int)workers;
+    pl.bpc_near_min = pl.bpc_near;
+    // (screen_topk's two-group rule: group 0's chunks exist only then)
+    const bool two = !(flags & LIRA_SCAN_PER_PARTITION) && op.two_phase && nprobe >= 2 &&
+                     (op.two_phase == 2 || nq >= (int64_t)pl.qr * idx->n_lists ||
+                      nq * nprobe >= 4 * (int64_t)pl.qr * idx->n_lists);
+    if (two && op.near_rounds <= 0 && pl.mfma && !pl.v2 && !pl.wide) {
+        const int64_t est0 = std::min<int64_t>(nq, (nq + pl.qr - 1) / pl.qr + idx->n_lists);
+        const int64_t split6 = std::max<int64_t>(1, (6 * (int64_t)workers + est0 - 1) / std::max<int64_t>(1, est0));
+        pl.bpc_near_min = (int)std::min<int64_t>(pl.bpc_near, std::max<int64_t>(1, (max_blocks + split6 - 1) / split6));
+    }
+    pl.nch_max = (int)((max_blocks + pl.bpc_near_min - 1) / pl.bpc_near_min);
     pl.max_qblk = npairs / pl.qr + std::min<int64_t>(2 * idx->n_lists, npairs) + 1;
     size_t o = 0;
     auto take = [&](size_t bytes) {
@@ -2817,7 +2849,8 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     const size_t nl = 2 * (size_t)idx->n_lists;  // up to two groups of virtual partitions
     pl.off_cnt = take(nl * 4);
     pl.off_cursor = take(nl * 4);
-    pl.off_head = take(32 * 4);  // [0..1] totals, [2..9] XCD queue counters, [10..18] queue bounds
+    pl.off_head = take(128 * 4);  // [0..1] totals, [2..9] XCD queue counters, [10..18] queue bounds,
+                                  // [19] group 0's chunk size, [64..127] the seed's work estimates
     pl.off_qoff = take((nl + 1) * 4);
     pl.off_item = take((nl + 1) * 4);
     pl.off_nch = take(nl * 4);
@@ -3037,6 +3070,11 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
         sp.QE = pl.pp ? QE : nullptr;
         sp.pqn = pl.pp ? pqn : nullptr;
         sp.QH = QH;
+        // (the work estimate that sizes group 0's items: only where the plan may adapt them)
+        const bool adapt = groups == 2 && pl.bpc_near_min < pl.bpc_near && idx->lsamp;
+        sp.list_size = adapt ? idx->list_size : nullptr;
+        sp.lsamp = adapt ? idx->lsamp : nullptr;
+        sp.work = adapt ? (unsigned int *)head + 64 : nullptr;
         hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2, 2, true>), dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, q,
                            probe, (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad,
                            nq, (int)k, qbound, sp);
@@ -3075,7 +3113,9 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     const int32_t *pprobe = plive ? plive : probe;  // the pairs that become work
     const int nvirt = groups * (int)idx->n_lists;
     LIRA_HIP_TRY(launch_plan(idx, pprobe, npairs, (int)nprobe, pl.bpc, groups == 2 ? pl.bpc_near : pl.bpc, pl.qr, groups, cnt, cursor, qoff, item_off,
-                             nch, head, qlist, qblk, itab, st));
+                             nch, head, qlist, qblk, itab, st,
+                             groups == 2 && fused && idx->lsamp ? pl.bpc_near_min : (groups == 2 ? pl.bpc_near : pl.bpc),
+                             pl.workers));
     if (!pl.pp) {
     const dim3 qgrid((unsigned)pl.max_qblk, (unsigned)((idx->dpad + 64 * kQSlabs - 1) / (64 * kQSlabs)));
     if (pl.qr == 128 && pl.split)
@@ -3204,6 +3244,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     m.nch_max = pl.nch_max;
     m.bpc = pl.bpc;
     m.bpc_near = a.bpc_near;
+    m.head = head;
     m.groups = groups;
     m.dedup = dedup ? 1 : 0;
     m.per_partition = per_part ? 1 : 0;

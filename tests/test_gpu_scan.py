@@ -380,7 +380,7 @@ def test_options_do_not_change_results(metric):
     ref = run(idx, q, probe, 10)
     for name, vals in (("qr", (128,)), ("two_phase", (0, 2)), ("seed", (0, 2, 3)), ("share", (0,)),
                        ("prune", (0,)), ("split", (0,)), ("mfma", (0, 2)), ("rounds", (1, 64)),
-                       ("near_rounds", (8,)), ("screen", (0,)), ("ring", (2, 3, 4)), ("probes_hint", (1, 4)), ("xhi", (0, 1, 2)),
+                       ("near_rounds", (2, 8)), ("screen", (0,)), ("ring", (2, 3, 4)), ("probes_hint", (1, 4)), ("xhi", (0, 1, 2)),
                        ("wide", (1, 2))):
         old = idx.get_option(name)
         for v in vals:
