@@ -348,10 +348,11 @@ __global__ __launch_bounds__(256) void k_rank_select64(const float *__restrict__
 // sort of the wave's 64 keys gives the nearest nprobe.  64 distances x d dims
 // is less VALU work than the GEMM's launch plus the re-check's (SIFT1M, 10 k
 // queries: k_centroid_gemm 8 us + k_rank_select64 23 us before).
+// 8 waves per workgroup (the 32 KB LDS image staged once per 8 or 16 queries);
 // qpw queries per wave, one after the other (1 for small batches: the chain of a
 // wave's queries, not the VALU work, set the time -- 8 per wave ran 31 us at 10 k
 // queries and 28 us at 1.25 k)
-__global__ __launch_bounds__(256) void k_rank_exact64(const float *__restrict__ q, int64_t nq,
+__global__ __launch_bounds__(512) void k_rank_exact64(const float *__restrict__ q, int64_t nq,
                                                       const float *__restrict__ cent, int nb, int64_t d,
                                                       int nprobe, int qpw, int32_t *out) {
     extern __shared__ float4 Cs[];  // [d/4][64]
@@ -359,12 +360,12 @@ __global__ __launch_bounds__(256) void k_rank_exact64(const float *__restrict__ 
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nd4 = (int)(d >> 2);
     // coalesced row reads (consecutive threads: consecutive float4 of one row)
-    for (int i = tid; i < 64 * nd4; i += 256) {
+    for (int i = tid; i < 64 * nd4; i += 512) {
         const int b = i / nd4, j4 = i - b * nd4;
         Cs[j4 * 64 + b] = b < nb ? *(const float4 *)(cent + (int64_t)b * d + 4 * j4) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     __syncthreads();
-    const int64_t q0 = (int64_t)blockIdx.x * (4 * qpw) + w * qpw;
+    const int64_t q0 = (int64_t)blockIdx.x * (8 * qpw) + w * qpw;
     for (int r = 0; r < qpw; ++r) {
         const int64_t qi = q0 + r;
         if (qi >= nq) break;
@@ -608,8 +609,8 @@ int lira_rank_nearest(const float *q, int64_t nq, const float *centroids, int64_
     if (!q || !centroids || !out_probe) return fail(LIRA_EINVAL, "NULL buffer");
     if (rank_exact64_ok(q, centroids, n_centroids, d)) {  // (no workspace needed)
         const int qpw = nq >= 8192 ? 2 : 1;
-        const unsigned g = (unsigned)((nq + 4 * qpw - 1) / (4 * qpw));
-        hipLaunchKernelGGL(k_rank_exact64, dim3(g), dim3(256), (size_t)d * 64 * 4, (hipStream_t)stream, q, nq,
+        const unsigned g = (unsigned)((nq + 8 * qpw - 1) / (8 * qpw));
+        hipLaunchKernelGGL(k_rank_exact64, dim3(g), dim3(512), (size_t)d * 64 * 4, (hipStream_t)stream, q, nq,
                            centroids, (int)n_centroids, d, (int)nprobe, qpw, out_probe);
         LIRA_HIP_TRY(hipGetLastError());
         return LIRA_OK;
