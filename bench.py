@@ -15,8 +15,14 @@ Scaling: ``weak`` (default) gives every rank its own batch of --nq queries;
 .shard_bounds), so at N = 1 it is the same workload and at N = 8 each rank scans
 nq/8 queries.  value = queries of all ranks / max-over-ranks time.
 
-Multi-GPU: launched as `python -m torch.distributed.run --nproc-per-node N
-bench.py --gpus N ...`.
+Multi-GPU: `python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the
+environment starts N ranks itself (a child `python -m torch.distributed.run
+--nproc-per-node N ... bench.py` process; this parent never touches the GPU and
+exits with the child's status).  Under torch.distributed.run (the driver's
+form) it runs as one of the ranks.  Every N > 1 line carries both figures:
+`value` for --scaling (weak by default) and an `other_scaling` sub-record for
+the other mode on the same index, plus `ranks_seen` (the world size the
+process group reported and each rank's device).
 """
 from __future__ import annotations
 
@@ -36,7 +42,6 @@ import torch  # noqa: E402
 # peaks (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0          # HBM3E spec
 L2LDS_PEAK_GBS = 18800.0       # LDS-DMA gather into LDS from the XCD L2, chip-wide (upper end, measured)
-L2_PEAK_GBS = 34500.0          # L2 read bandwidth, chip-wide (MI355X_MICROARCH.md, L2 per XCD)
 MFMA_F32_PEAK_TFLOPS = 157.3   # v_mfma_f32_*_f32 dense = fp32 vector peak
 MFMA_BF16_PEAK_TFLOPS = 2516.6  # dense bf16 MFMA, 16 x the f32 rate
 VALU_F32_PEAK_TOPS = 78.64     # non-FMA fp32 lane ops/s (157.3 TFLOP/s counts an FMA as 2)
@@ -110,8 +115,10 @@ def blas_scan_topk(qs, off, ids, vecs, ps, k, ip):
     probed list, the queries that probe it in one block -> one sgemm
     (torch CPU, all threads), ||q||^2 - 2 q.x + ||x||^2 (norms computed per
     search, as faiss' exhaustive_L2sqr_blas does), top-k per (query, list), then
-    top-k over each query's nprobe x k candidates (replicas not de-duplicated).
-    Not bit-exact with search.cpp's sequential sum; a baseline, not the oracle."""
+    top-k over each query's nprobe x k candidates with replicas de-duplicated
+    (a row in two probed lists counts once, at its better score, as the GPU's
+    LIRA_SCAN_DEDUP output does).  Not bit-exact with search.cpp's sequential
+    sum; a baseline, not the oracle."""
     n, P = ps.shape
     worst = -np.inf if ip else np.inf
     cD = torch.full((n * P, k), worst, dtype=torch.float32)
@@ -138,8 +145,19 @@ def blas_scan_topk(qs, off, ids, vecs, ps, k, ip):
         rows = torch.from_numpy(grp)
         cD[rows, :v.shape[1]] = v
         cI[rows, :v.shape[1]] = torch.from_numpy(ids[lo:hi])[j.reshape(-1)].reshape(j.shape).long()
-    v, j = torch.topk(cD.view(n, P * k), k, dim=1, largest=ip)
-    return v.numpy(), torch.gather(cI.view(n, P * k), 1, j).numpy()
+    cD, cI = cD.view(n, P * k), cI.view(n, P * k)
+    # de-duplicate ids: group each row by id (stable sorts: by score, then by id),
+    # keep the best score of each id, push the others past every real score
+    o1 = torch.sort(cD, dim=1, descending=ip, stable=True).indices
+    cD, cI = torch.gather(cD, 1, o1), torch.gather(cI, 1, o1)
+    o2 = torch.sort(cI, dim=1, stable=True).indices
+    cD, cI = torch.gather(cD, 1, o2), torch.gather(cI, 1, o2)
+    dup = torch.zeros_like(cI, dtype=torch.bool)
+    dup[:, 1:] = (cI[:, 1:] == cI[:, :-1]) & (cI[:, 1:] >= 0)
+    cD = cD.masked_fill(dup, worst)
+    cI = cI.masked_fill(dup, -1)
+    v, j = torch.topk(cD, k, dim=1, largest=ip)
+    return v.numpy(), torch.gather(cI, 1, j).numpy()
 
 
 def time_blas(qs, ps, host, k, ip, threads, budget_s=10.0):
@@ -166,10 +184,101 @@ def parse_opts(items, config):
     return opts
 
 
+def time_batch(args, index, q, centres, nprobe, k, world, dist, gdev, nq_total, scaling):
+    """Time args.steps steps of the hot path on this rank's query slice q
+    (rank_nearest -> scan + top-k, as one HIP graph unless --graph 0, then for
+    N > 1 the all-gather of the per-rank top-k), barrier + synchronize on both
+    sides, max over ranks.  Returns (elapsed s, D, I, ncand, probe, local_step,
+    graph, verified): `verified` checks once, after the timed loop, that every
+    rank's gathered copy of this rank's rows equals its own result (None at N = 1)."""
+    from lira_amd import RankWorkspace, rank_nearest
+    from lira_amd.distributed import all_gather_rows, shard_bounds
+    dev = q.device
+    nq = q.shape[0]
+    B = centres.shape[0]
+    ws = RankWorkspace(max(1, nq), B, dev)
+    probe = torch.empty((nq, nprobe), dtype=torch.int32, device=dev)
+    D = torch.empty((nq, k), dtype=torch.float32, device=dev)
+    I = torch.empty((nq, k), dtype=torch.int64, device=dev)
+    ncand = torch.empty(nq, dtype=torch.int64, device=dev)
+
+    def local_step():
+        rank_nearest(q, centres, nprobe, out=probe, workspace=ws)
+        index.search(q, probe, k, dedup=True, out=(D, I, ncand), fma=args.fma)
+
+    # the step's ~10 launches as one HIP graph: no per-launch host overhead or
+    # gaps between kernels (the library's calls are capture-safe: workspaces
+    # are allocated by the warm-up calls, no host syncs on the search path)
+    graph = None
+    if args.graph:
+        for _ in range(2):
+            local_step()
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            local_step()
+        torch.cuda.synchronize()
+
+    def gather():
+        if scaling == "strong":
+            return all_gather_rows(D.to(gdev), nq_total, world), all_gather_rows(I.to(gdev), nq_total, world)
+        gd = [torch.empty_like(D, device=gdev) for _ in range(world)]
+        gi = [torch.empty_like(I, device=gdev) for _ in range(world)]
+        dist.all_gather(gd, D.to(gdev))
+        dist.all_gather(gi, I.to(gdev))
+        return gd, gi
+
+    def step():
+        if graph is not None:
+            graph.replay()
+        else:
+            local_step()
+        if world > 1:  # the per-rank top-k of the batch, to every rank (RCCL all-gather)
+            return gather()
+        return None
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    index.check()
+    if graph is None:
+        index.set_profiling(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    verified = None
+    if world > 1:
+        t = torch.tensor([elapsed], device=gdev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        # the gathered result: this rank's rows as every rank received them
+        gd, gi = step()
+        torch.cuda.synchronize()
+        rank = dist.get_rank()
+        if scaling == "strong":
+            s, e = shard_bounds(nq_total, rank, world)
+            mine_d, mine_i = gd[s:e], gi[s:e]
+        else:
+            mine_d, mine_i = gd[rank], gi[rank]
+        ok = torch.equal(mine_i.cpu(), I.cpu()) and torch.equal(mine_d.cpu().view(torch.int32),
+                                                                 D.cpu().view(torch.int32))
+        f = torch.tensor([1 if ok else 0], device=gdev, dtype=torch.int32)
+        dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        verified = bool(f.item())
+    return elapsed, D, I, ncand, probe, local_step, graph, verified
+
+
 def run_workload(args, data, rank, world, gpu, dev, dist, primary):
     """Build one config on one distribution, time the step, measure everything."""
-    from lira_amd import PartitionedIndex, RankWorkspace, centroid_gemm, rank_nearest
-    from lira_amd.distributed import all_gather_rows, shard_bounds
+    from lira_amd import PartitionedIndex, centroid_gemm, rank_nearest
+    from lira_amd.distributed import shard_bounds
     from lira_amd.synthetic import CONFIGS, LATENT_DIM, N_MUL, workload
 
     N, d, B, nprobe, k, metric, nq_default = CONFIGS[args.config]
@@ -195,60 +304,10 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
         f"{int(sizes.min())}..{int(sizes.max())} in {time.time() - t0:.1f}s, index "
         f"{index.memory_bytes() / 1e9:.1f} GB, {nq} queries/rank")
 
-    ws = RankWorkspace(max(1, nq), B, dev)
-    probe = torch.empty((nq, nprobe), dtype=torch.int32, device=dev)
-    D = torch.empty((nq, k), dtype=torch.float32, device=dev)
-    I = torch.empty((nq, k), dtype=torch.int64, device=dev)
-    ncand = torch.empty(nq, dtype=torch.int64, device=dev)
     gdev = dev if args.backend == "nccl" else torch.device("cpu")
     kernel = index.describe(nq, nprobe, k)
-
-    def local_step():
-        rank_nearest(q, centres, nprobe, out=probe, workspace=ws)
-        index.search(q, probe, k, dedup=True, out=(D, I, ncand), fma=args.fma)
-
-    # the step's ~10 launches as one HIP graph: no per-launch host overhead or
-    # gaps between kernels (the library's calls are capture-safe: workspaces
-    # are allocated by the warm-up calls, no host syncs on the search path)
-    graph = None
-    if args.graph:
-        for _ in range(2):
-            local_step()
-        torch.cuda.synchronize()
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            local_step()
-        torch.cuda.synchronize()
-
-    def step():
-        if graph is not None:
-            graph.replay()
-        else:
-            local_step()
-        if world > 1:  # the per-rank top-k of the batch, to every rank (RCCL all-gather)
-            if args.scaling == "strong":
-                all_gather_rows(D.to(gdev), nq_job, world)
-                all_gather_rows(I.to(gdev), nq_job, world)
-            else:
-                dist.all_gather([torch.empty_like(D, device=gdev) for _ in range(world)], D.to(gdev))
-                dist.all_gather([torch.empty_like(I, device=gdev) for _ in range(world)], I.to(gdev))
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    index.check()
-    if graph is None:
-        index.set_profiling(True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
+    elapsed, D, I, ncand, probe, local_step, graph, verified = time_batch(
+        args, index, q, centres, nprobe, k, world, dist, gdev, nq_job, args.scaling)
     if graph is not None:  # per-phase kernel times: the same step launched one by one, untimed
         index.set_profiling(True)
         for _ in range(args.steps):
@@ -256,14 +315,28 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
         torch.cuda.synchronize()
     prof = index.profile_read()
     index.set_profiling(False)
-    if world > 1:
-        t = torch.tensor([elapsed], device=gdev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    other = None
+    if world > 1:  # the other scaling mode on the same index: a fixed batch split over ranks, or a batch each
+        om = "strong" if args.scaling == "weak" else "weak"
+        if om == "strong":
+            q_all = make_queries(nq_job, args.seed + 101)
+            s0, e0 = shard_bounds(nq_job, rank, world)
+            qo = q_all[s0:e0].contiguous()
+            del q_all
+        else:
+            qo = make_queries(nq_job, args.seed + 101 + 7919 * rank)
+        el_o, *_, ver_o = time_batch(args, index, qo, centres, nprobe, k, world, dist, gdev, nq_job, om)
+        index.set_profiling(False)
+        n_o = nq_job if om == "strong" else nq_job * world
+        other = {"scaling": om, "value": n_o * args.steps / el_o, "unit": "queries/s",
+                 "ms_per_step": el_o / args.steps * 1e3, "queries_per_step": n_o,
+                 "queries_per_rank": int(qo.shape[0]), "allgather_verified": ver_o}
+        del qo
     calls = max(1, prof["calls"])
     scan_ms, merge_ms, plan_ms = prof["scan_ms"] / calls, prof["merge_ms"] / calls, prof["plan_ms"] / calls
     nq_all = nq_job if args.scaling == "strong" else nq_job * world
-    out = {"data": data, "value": nq_all * args.steps / elapsed, "unit": "queries/s",
+    out = {"data": data, "value": nq_all * args.steps / elapsed, "unit": "queries/s", "other_scaling": other,
+           "allgather_verified": verified,
            "ms_per_step": elapsed / args.steps * 1e3, "queries_per_rank": nq, "kernel": kernel,
            "launch": "hip_graph" if graph is not None else "stream",
            "index_bytes": index.memory_bytes(), "n_mul": n_mul, "index_options": opts,
@@ -303,7 +376,7 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
     split = "split-bf16" in kernel or hh
     hix = "hi-x" in kernel  # hi-only x: 2 products per dim (qh, ql) x xh, half the X bytes
     kname = kernel.split()[0]
-    if kname in ("k_screen_m", "k_screen_w", "k_screen_v"):
+    if kname == "k_screen_m":
         # (row, cand) pairs x dpad x products x 2
         flops = work["chunks_computed"] * dpad * (2 if hh else 4 if hix else 8 if split else 2)
         mfma_peak = MFMA_BF16_PEAK_TFLOPS if split else MFMA_F32_PEAK_TFLOPS
@@ -311,22 +384,10 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
     else:
         flops = work["chunks_computed"] * dpad * 2
         mfma_peak, mfma_what = MFMA_F32_PEAK_TFLOPS, "fp32 VALU (v_pk_fma_f32)"
-    if kname == "k_screen_v":
-        # L2 -> VGPR bytes per launch: per tile (64 candidates) their hi parts + xadj
-        # (the work counter "blocks" counts tiles here)
-        staged = work["blocks"] * (64 * dpad * 2 + 256)
-        st_name, st_peak = "l2_regs", L2_PEAK_GBS
-        st_what = "bytes loaded L2/MALL -> VGPRs (x hi parts + xadj per tile; queries stay in registers)"
-    elif kname == "k_screen_w":
-        # per block (128 candidates): their hi parts + xadj; queries stay in registers
-        staged = work["blocks"] * (128 * dpad * 2 + 512)
-        st_name, st_peak = "l2_lds", L2LDS_PEAK_GBS
-        st_what = "bytes staged L2/MALL -> LDS by LDS-DMA (x hi parts + xadj per block)"
-    else:
-        # L2 -> LDS bytes (LDS-DMA) per launch: X (256 candidates), Q (qr rows), xadj
-        staged = work["blocks"] * (256 * dpad * (2 if hix else 4) + qr * dpad * (2 if hh else 4) + 1024)
-        st_name, st_peak = "l2_lds", L2LDS_PEAK_GBS
-        st_what = "bytes staged L2/MALL -> LDS by LDS-DMA (tiles + query chunk + xadj per computed block)"
+    # L2 -> LDS bytes (LDS-DMA) per launch: X (256 candidates), Q (qr rows), xadj
+    staged = work["blocks"] * (256 * dpad * (2 if hix else 4) + qr * dpad * (2 if hh else 4) + 1024)
+    st_name, st_peak = "l2_lds", L2LDS_PEAK_GBS
+    st_what = "bytes staged L2/MALL -> LDS by LDS-DMA (tiles + query chunk + xadj per computed block)"
     traffic, pmc_src = None, None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_scan_{args.config}_{data}.json")
     if os.path.exists(pmc_path):
@@ -363,6 +424,12 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
                     "roofline -- the partition-major scan reads a candidate once per query block and "
                     "skips or screens most of them; reported for continuity only"},
         "work": {"blocks_computed": work["blocks"], "blocks_skipped": work["blocks_skipped"],
+                 "pairs_pruned_plan": work["pairs_pruned_plan"],
+                 "candidates_pruned_plan": work["candidates_pruned_plan"],
+                 "blocks_pruned_plan": work["candidates_pruned_plan"] / (qr * 256.0),
+                 "blocks_pruned_plan_note": "(query, candidate) pairs the plan's partition filter removed, in "
+                                            "units of one screen block (qr query rows x 256 candidates); "
+                                            "blocks_skipped = blocks the in-kernel triangle test skipped",
                  "pairs_screened": work["chunks_computed"], "survivors": work["survivors"],
                  "rechecked": work["rechecked"], "rescans": work["rescans"],
                  "rechecked_per_query": work["rechecked"] / max(1, nq)},
@@ -654,24 +721,58 @@ def time_pipeline(args, oracle, index, x, centres, q, make_queries, k, nprobe, m
                    f"indicator: synthetic stand-in for LIRA's kNN labels"}
 
 
+def launch_ranks(args) -> int:
+    """--gpus N > 1 without a launcher: start the N ranks as ONE child process
+    tree (torch.distributed.run, rendezvous on 127.0.0.1) and return its exit
+    status.  Nothing here touches the GPU (no torch.cuda call), so the
+    children own the devices."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL, tensor sharing)
+    log(f"[bench] --gpus {args.gpus}: starting {args.gpus} ranks: {' '.join(cmd)}")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world != 1:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     ndev = torch.cuda.device_count()
     gpu = local % max(1, ndev)  # gloo rehearsal: several ranks may share one GPU
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     dist = None
+    ranks_seen = {"world_size": 1, "devices": [torch.cuda.get_device_name(dev)]}
     if world > 1:
         import torch.distributed as dist
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+        got = dist.get_world_size()
+        if got != args.gpus:
+            log(f"error: --gpus {args.gpus} but the process group has {got} ranks")
+            dist.destroy_process_group()
+            sys.exit(3)
+        me = {"rank": dist.get_rank(), "local_rank": local, "device": gpu,
+              "name": torch.cuda.get_device_name(dev), "pci_bus": torch.cuda.get_device_properties(dev).pci_bus_id,
+              "host": platform.node()}
+        seen = [None] * got
+        dist.all_gather_object(seen, me)
+        ranks_seen = {"world_size": got, "backend": args.backend, "ranks": seen,
+                      "distinct_gpus": len({(r["host"], r["pci_bus"]) for r in seen})}
+    elif args.gpus != 1:
+        log(f"error: --gpus {args.gpus} under WORLD_SIZE={world}")
+        sys.exit(3)
     from lira_amd.synthetic import CONFIGS, LATENT_DIM
 
     N, d, B, nprobe, k, metric, nq_default = CONFIGS[args.config]
@@ -690,6 +791,7 @@ def main():
             "value": head["value"],
             "unit": "queries/s",
             "n_gpus": world,
+            "ranks_seen": ranks_seen,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": head["ms_per_step"],
@@ -708,6 +810,8 @@ def main():
                        "queries_per_step": nq_job * (world if args.scaling == "weak" else 1),
                        "queries_per_rank": head["queries_per_rank"],
                        "parallelism": f"query-shard x{world} (index replicated)"},
+            "other_scaling": head.get("other_scaling"),
+            "allgather_verified": head.get("allgather_verified"),
             "roofline": head.get("roofline"),
             "cpu_baseline": head.get("cpu_baseline"),
             **{key: head[key] for key in ("kernels_ms_per_step", "kernel", "index_bytes", "index_options", "pipeline",

@@ -140,9 +140,8 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *   LIRA_OPT_QR          queries per screen work item: 0 auto (default), 64, 128; 32 (k > 56)
  *   LIRA_OPT_TWO_PHASE   nearest-probe group first: 1 auto (default), 0 off, 2 always
  *   LIRA_OPT_PRUNE       L2 triangle-inequality block skip / exact early abandon (1)
- *   LIRA_OPT_SEED        exact starting bound per query before the screen: 1 (default) per
- *                        query; 2 / 3: per nearest-partition query block over 128 / 256
- *                        rows where it applies (k <= 32, d <= 256, two groups); 0 off
+ *   LIRA_OPT_SEED        exact starting bound per query before the screen: 1 (default), 0 off
+ *                        (2 / 3, the block-shared seed, were removed: LIRA_EUNSUPPORTED)
  *   LIRA_OPT_SHARE       per-block exchange of query bounds between work items (1)
  *   LIRA_OPT_ROUNDS      work items per workgroup target (0 = kernel default)
  *   LIRA_OPT_NEAR_ROUNDS the same for the nearest-probe group: 0 (default) auto -- the plan
@@ -151,8 +150,10 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *   LIRA_OPT_DEBUG       timing experiments only (results invalid): bit mask, see lira_screen.hip.
  *                        Production builds accept only 0 and return LIRA_EUNSUPPORTED otherwise;
  *                        a -DLIRA_DEBUG build (tools/build_variant.sh) accepts 0..255
- *   LIRA_OPT_PIPELINE    1: the pipelined split screen k_screen_s for k > 56; 0 (default): k_screen_m
- *   LIRA_OPT_RING        k_screen_s ring slots: 0 auto, 2..4
+ *   LIRA_OPT_PIPELINE, LIRA_OPT_RING, LIRA_OPT_WIDE
+ *                        selected screen variants that measured slower than k_screen_m on every
+ *                        config (k_screen_s, k_screen_w, k_screen_v) and were removed: 0 is
+ *                        accepted (and read back), any other value returns LIRA_EUNSUPPORTED
  *   LIRA_OPT_PROBES_HINT expected valid probes per query when the probe lists are mostly -1
  *                        padding (a threshold selection padded to B): sizes the work split (0 = nprobe_max)
  *   LIRA_OPT_XHI         1: the split screen multiplies the query's hi + lo parts by x's hi part only
@@ -164,10 +165,6 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *                        each list's rows by ascending distance to the list's pivot, so tile radius
  *                        ranges are narrow and the triangle-inequality skip drops more; 0: list order.
  *                        Results never depend on it.
- *   LIRA_OPT_WIDE        1: the wide screen k_screen_w (256 query rows per item, one
- *                        512-thread workgroup per CU, v_mfma_f32_32x32x16_bf16) where it applies
- *                        (L2 with the centred split copy, k <= 24, dpad 64 / 96 / 128, a seeded
- *                        bound); 0 (default): k_screen_m (measured faster on every config)
  */
 #define LIRA_OPT_KEEP_TILES 1
 #define LIRA_OPT_SCREEN 2
@@ -309,7 +306,10 @@ int lira_index_profile_read(lira_index *idx, double *plan_ms, double *scan_ms, d
  *       a needed candidate), [7] screened survivors appended to row lists.
  * The screened path (default) counts [0] as the (query row, candidate) pairs
  * it screened (padding rows included; x dpad = FMAs executed), and [2], [4],
- * [5], [6], [7]; the all-exact scan (LIRA_SCAN_EXACT) [0]..[4] as above.
+ * [5], [6], [7]; there [1] = (query, partition) pairs the plan's partition
+ * filter removed before any work item exists (the seed bound's triangle test
+ * over the whole list) and [3] = their (query, candidate) pairs (never
+ * screened).  The all-exact scan (LIRA_SCAN_EXACT) counts [0]..[4] as above.
  * lira_index_stats_read synchronises the device, copies the 8 sums to `out8`
  * (host) and resets them.  Costs a few atomics per block: keep it off when
  * timing.

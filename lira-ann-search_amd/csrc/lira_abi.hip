@@ -718,7 +718,8 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes) {
              (idx->xadj ? rows * 4 + idx->n_lists * 4 : 0) +                   // xadj, rmax
              (idx->xadjc ? rows * 4 + idx->n_lists * 4 : 0) +                  // centred xadj, rmax
              (idx->pivot ? idx->n_lists * idx->d * 4 + idx->n_tiles * 8 + idx->n_lists * 8 : 0) +  // pivots, radii
-             (idx->tres ? idx->n_tiles * 4 : 0);                                // tile hi residuals
+             (idx->tres ? idx->n_tiles * 4 : 0) +                               // tile hi residuals
+             (idx->lsamp ? idx->n_lists * 16 * (int64_t)sizeof(float2) : 0);   // sampled tile radius ranges
     return LIRA_OK;
 }
 
@@ -734,7 +735,12 @@ int lira_index_set_option(lira_index *idx, int option, int64_t value) {
         case LIRA_OPT_QR: if (value != 0 && value != 32 && value != 64 && value != 128) break; o.qr = v; return LIRA_OK;
         case LIRA_OPT_TWO_PHASE: if (!in(0, 2)) break; o.two_phase = v; return LIRA_OK;
         case LIRA_OPT_PRUNE: if (!in(0, 1)) break; o.prune = v; return LIRA_OK;
-        case LIRA_OPT_SEED: if (!in(0, 3)) break; o.seed = v; return LIRA_OK;
+        case LIRA_OPT_SEED:
+            if (value == 2 || value == 3)  // (k_seed_b, measured slower: removed in round 4)
+                return fail(LIRA_EUNSUPPORTED, "LIRA_OPT_SEED 2 / 3 (block-shared seed) was removed");
+            if (!in(0, 1)) break;
+            o.seed = v;
+            return LIRA_OK;
         case LIRA_OPT_SHARE: if (!in(0, 1)) break; o.share = v; return LIRA_OK;
         case LIRA_OPT_ROUNDS: if (!in(0, 1024)) break; o.rounds = v; return LIRA_OK;
         case LIRA_OPT_NEAR_ROUNDS: if (!in(0, 1024)) break; o.near_rounds = v; return LIRA_OK;
@@ -744,12 +750,14 @@ int lira_index_set_option(lira_index *idx, int option, int64_t value) {
             if (v && !debug_build())  // a production build never returns invalid results
                 return fail(LIRA_EUNSUPPORTED, "LIRA_OPT_DEBUG needs a library built with -DLIRA_DEBUG");
             o.debug = v; return LIRA_OK;
-        case LIRA_OPT_PIPELINE: if (!in(0, 1)) break; o.pipeline = v; return LIRA_OK;
-        case LIRA_OPT_RING: if (!in(0, 4)) break; o.ring = v; return LIRA_OK;
+        case LIRA_OPT_PIPELINE:  // (k_screen_s, k_screen_w, k_screen_v: measured slower, removed in round 4)
+        case LIRA_OPT_RING:
+        case LIRA_OPT_WIDE:
+            if (value == 0) return LIRA_OK;
+            return fail(LIRA_EUNSUPPORTED, "option " + std::to_string(option) + " selected a screen variant that was removed");
         case LIRA_OPT_PROBES_HINT: if (!in(0, 1 << 20)) break; o.probes_hint = v; return LIRA_OK;
         case LIRA_OPT_XHI: if (!in(-1, 2)) break; o.xhi = v; return LIRA_OK;
         case LIRA_OPT_ORDER: if (!in(0, 1)) break; o.order = v; return LIRA_OK;
-        case LIRA_OPT_WIDE: if (!in(0, 2)) break; o.wide = v; return LIRA_OK;
         default: return fail(LIRA_EINVAL, "unknown option " + std::to_string(option));
     }
     return fail(LIRA_EINVAL, "value " + std::to_string(value) + " out of range for option " + std::to_string(option));
@@ -771,12 +779,12 @@ int lira_index_get_option(const lira_index *idx, int option, int64_t *value) {
         case LIRA_OPT_NEAR_ROUNDS: *value = o.near_rounds; break;
         case LIRA_OPT_MFMA: *value = o.mfma; break;
         case LIRA_OPT_DEBUG: *value = o.debug; break;
-        case LIRA_OPT_PIPELINE: *value = o.pipeline; break;
-        case LIRA_OPT_RING: *value = o.ring; break;
+        case LIRA_OPT_PIPELINE:
+        case LIRA_OPT_RING:
+        case LIRA_OPT_WIDE: *value = 0; break;
         case LIRA_OPT_PROBES_HINT: *value = o.probes_hint; break;
         case LIRA_OPT_XHI: *value = o.xhi; break;
         case LIRA_OPT_ORDER: *value = o.order; break;
-        case LIRA_OPT_WIDE: *value = o.wide; break;
         default: return fail(LIRA_EINVAL, "unknown option " + std::to_string(option));
     }
     return LIRA_OK;

@@ -72,6 +72,12 @@ __device__ __forceinline__ u64 shfl64(u64 v, int src) {
     return ((u64)hi << 32) | lo;
 }
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+// sum over the wave (every lane gets it)
+__device__ __forceinline__ u64 wave_sum_u64(u64 v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += shfl_xor64(v, m);
+    return v;
+}
 // lane l <- lane (l & 32) | (31 - (l & 31)): reversal inside each 32-lane half,
 // one ds_swizzle (bit mode: and 0x1f, xor 0x1f) per dword
 __device__ __forceinline__ u64 rev32_u64(u64 v) {

@@ -48,12 +48,9 @@ struct lira_opts {
     int near_rounds = 0;  // 0: auto (the plan sizes group 0 from the seed's work estimate, between 2 and 6 rounds)
     int mfma = 1;
     int debug = 0;
-    int pipeline = 0;
-    int ring = 0;
     int probes_hint = 0;
     int xhi = -1;
     int order = 1;
-    int wide = 0;
 };
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device):

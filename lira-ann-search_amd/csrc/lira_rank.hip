@@ -525,7 +525,9 @@ __global__ __launch_bounds__(256) void k_select_threshold_sorted(const float *__
 }
 
 // lira_order_probes: one wave per row; keys (f2ord(key[b]) << 32 | b), -1 slots
-// as empty keys (sorted last), one wave-wide sort of the row's R*64 keys
+// as empty keys (sorted last), one wave-wide sort of the row's R*64 keys.  An
+// id >= n_centroids is kept (after the valid ones, before the padding), so the
+// scan still sees it and reports LIRA_ERANGE: ordering never changes the set.
 template <int R>
 __global__ __launch_bounds__(256) void k_order_probes(int32_t *probe, int64_t n, int mp, const float *__restrict__ key,
                                                       int nb) {
@@ -538,7 +540,8 @@ __global__ __launch_bounds__(256) void k_order_probes(int32_t *probe, int64_t n,
     for (int r = 0; r < R; ++r) {
         const int e = r * 64 + lane;
         const int b = e < mp ? row[e] : -1;
-        v[r] = b >= 0 && b < nb ? ((u64)f2ord(key[i * nb + b]) << 32) | (uint32_t)b : kEmptyKey;
+        v[r] = b < 0 ? kEmptyKey : b < nb ? ((u64)f2ord(key[i * nb + b]) << 32) | (uint32_t)b
+                                          : (0xffffffffull << 32) | (uint32_t)b;
     }
     wave_sort<R>(v);
 #pragma unroll

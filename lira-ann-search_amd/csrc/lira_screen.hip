@@ -53,30 +53,6 @@
 
 namespace lira {
 
-// lira_wscreen.hip
-bool wscreen_shape_ok(int64_t dpad);
-int wscreen_smem();
-hipError_t launch_pairs(const float *Q, int64_t d, const int32_t *probe, int64_t npairs, int nprobe, int n_lists,
-                        const float *pivot, int centred, const float2 *lstat, const uint32_t *qbound,
-                        int32_t *probe_live, float4 *QN, float *QE, float *pqn, uint16_t *QH, int64_t dpad,
-                        hipStream_t st);
-hipError_t launch_wscreen(const lira_index *idx, const float *q, const int32_t *cnt, const int32_t *qoff,
-                          const int32_t *qlist, const int4 *itab, int32_t *head, const float4 *QN, const float *QE,
-                          u64 *partial, float *pE, uint32_t *qbound, int nprobe, int k, int bpc, int bpc_near,
-                          int nch_max, int n_virt, int tri, int grid, int4 *wrec, int64_t max_items, hipStream_t st);
-
-// lira_vscreen.hip
-bool vscreen_shape_ok(int64_t dpad);
-int vscreen_smem();
-int vscreen_max_tiles();
-int vscreen_rows();
-int vscreen_workers_per_cu();
-hipError_t launch_vscreen(const lira_index *idx, const float *q, const int32_t *cnt, const int32_t *qoff,
-                          const int32_t *qlist, const int4 *itab, int32_t *head, const float4 *QN, const float *QE,
-                          const uint16_t *QH, u64 *partial, float *pE, uint32_t *qbound, int nprobe, int k, int bpc,
-                          int bpc_near, int nch_max, int n_virt, int tri, int grid, int4 *vrec, int64_t max_items,
-                          hipStream_t st);
-
 hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npairs, int nprobe, int bpc,
                        int bpc_near,
                        int qr, int groups, int32_t *cnt, int32_t *cursor, int32_t *qoff, int32_t *item_off,
@@ -1568,485 +1544,6 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_m(ScreenArgs a) {
     }
 }
 
-// ---- the pipelined split-bf16 screen (LIRA_OPT_PIPELINE; measured slower) ----
-// k_screen_s: k_screen_m<..., SPLIT>'s work (same items, error model, row
-// lists and outputs) around an NS-slot LDS-DMA ring:
-//  * a wave waits only for its OWN DMA of the chunk it consumes, by a counted
-//    s_waitcnt vmcnt(Y) (Y = the DMA instructions it issued since that chunk's),
-//    then one barrier; NS - 1 chunks stay in flight across block boundaries,
-//    so the streaming overlaps the MFMAs and the selection;
-//  * nothing the compiler sees as a global load is consumed inside the ring
-//    (its own waitcnts would drain it): the block's xadj rides with the
-//    block's first chunk, and the query bounds published by other items come
-//    back by DMA into LDS (pub_s) at a block's end, to be read at the next;
-//  * thresholds are refreshed at a block's end (the selection's h and the
-//    triangle-skip interval the issuer uses for the blocks after it).
-template <int QR, int RL, int NS, int BC>
-struct SSmem2 {
-    static constexpr int NW = QR / 16, K2 = 32 * RL;
-    static constexpr int kX = kSBT * kSDK * kTile * 4;  // X chunk: 16 KiB (split-bf16 = fp32 bytes)
-    static constexpr int kQ = kSDK * QR * 4;            // Q chunk
-    static constexpr int kXA = kSBT * kTile * 4;        // the block's xadj (rides with chunk 0)
-    static constexpr int kSlot = kX + kQ + kXA;
-    static constexpr int kRing = NS * kSlot;
-    static constexpr int kLists = QR * K2 * 8;
-    static constexpr int kBufs = QR * BC * 8;
-    static constexpr int kBR = 256;  // block radius ranges staged per item (the planner keeps items <= kBR blocks)
-    // dq_s [QR] double2, tri_s [2][QR] float2, br_s [kBR] float2, then ints:
-    // item [16], slot tb/jc [4 + 4], marks [NW][8], pair/bufc/pub [QR] each
-    static constexpr int kMeta = QR * 16 + 2 * QR * 8 + kBR * 8 + (24 + NW * 8 + 3 * QR) * 4;
-    static constexpr int total = kRing + kLists + kBufs + kMeta;
-};
-
-__device__ __forceinline__ void sglds4(const void *gsrc, uint32_t lds_addr) {
-    unsigned keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-        "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(gsrc), "s"(lds_addr)
-        : "memory");
-}
-
-// s_waitcnt vmcnt(n), n wave-uniform; n > 15 waits for 15 (more than needed: safe)
-__device__ __forceinline__ void wait_vmcnt(int n) {
-    switch (n) {
-        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-        case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-        case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-        case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
-        case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-        case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
-        case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-    }
-}
-
-template <int METRIC, int RL, int QR, int NS, int BC, int OCC>
-__global__ __launch_bounds__(QR * 4, OCC) void k_screen_s(ScreenArgs a) {
-    constexpr int NW = QR / 16, NT = QR * 4;
-    typedef SSmem2<QR, RL, NS, BC> S;
-    constexpr int K2 = S::K2;
-    constexpr int XPW = 16 / NW;  // 1-KiB X pieces per wave per chunk
-    static_assert(NS >= 2 && NS <= 4 && BC <= 32 && 16 % NW == 0, "ring / buffer shape");
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    char *ring = smem;
-    u64 *lists = (u64 *)(smem + S::kRing);
-    u64 *bufs = (u64 *)(smem + S::kRing + S::kLists);
-    double *dq_s = (double *)(smem + S::kRing + S::kLists + S::kBufs);  // [QR][2]
-    float2 *tri_s = (float2 *)(dq_s + 2 * QR);                          // [2][QR]
-    float2 *br_s = tri_s + 2 * QR;                                       // [kBR]
-    int *meta = (int *)(br_s + S::kBR);                                  // [16]
-    int *slot_tb = meta + 16, *slot_jc = slot_tb + 4;                    // [NS] each
-    int *marks = slot_jc + 4;                                            // [NW][8]
-    int *m_pair = marks + NW * 8, *m_bufc = m_pair + QR;
-    uint32_t *pub_s = (uint32_t *)(m_bufc + QR);
-    const bool TRI = METRIC == LIRA_METRIC_L2 && a.tstat != nullptr;
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int g = lane >> 4, cj = lane & 15;
-    const int k = a.k;
-    const double dd = (double)a.d;
-    const float4 *Xg = (const float4 *)a.X;
-    const uint32_t ring_lds = (uint32_t)(uintptr_t)(lds_void_t *)ring;
-    const uint32_t pub_lds = (uint32_t)(uintptr_t)(lds_void_t *)pub_s;
-    const int tstride = (int)a.dpad * (kTile / 4);
-    const int dpad = (int)a.dpad;
-
-    __shared__ int xq[9];  // the XCD queues' bounds (k_plan)
-    int qx = 0, qtries = 0, nxt = -1;  // thread 0: its queue, the claimed next item
-    if (tid == 0) {
-        for (int r = 0; r < 9; ++r) xq[r] = a.head[10 + r];
-        qx = xcd_id();
-        nxt = claim_item(a.head, xq, qx, qtries);
-    }  // thread 0: the claimed next item
-    for (;;) {
-        if (tid == 0) {
-            const int item = nxt;
-            const int ok = item >= 0;
-            int4 e = make_int4(0, 0, 0, 0);
-            if (ok) {
-                e = a.itab[item];
-                nxt = claim_item(a.head, xq, qx, qtries);
-            }
-            meta[0] = ok;
-            meta[1] = e.x;
-            meta[2] = e.y;
-            meta[3] = e.z;
-            meta[4] = e.w;
-        }
-        __syncthreads();
-        if (!meta[0]) break;
-        const int vp = __builtin_amdgcn_readfirstlane(meta[1]);  // virtual partition
-        const int p = vp >= a.n_lists ? vp - a.n_lists : vp;
-        const int ch = __builtin_amdgcn_readfirstlane(meta[3]);
-        const int gqb = __builtin_amdgcn_readfirstlane(meta[4]);
-        if (tid < QR) {
-            m_pair[tid] = __float_as_int(a.QN[(int64_t)gqb * QR + tid].z);
-            m_bufc[tid] = 0;
-        }
-        for (int i = tid; i < QR * K2; i += NT) lists[i] = kEmptyKey;
-
-        const int tile0 = __builtin_amdgcn_readfirstlane(a.tile_off[p]);
-        const int ntl = __builtin_amdgcn_readfirstlane(a.tile_off[p + 1]) - tile0;
-        const int bpc = vp < a.n_lists && a.n_virt > a.n_lists ? a.bpc_near : a.bpc;
-        const int tb_begin = ch * bpc * kSBT;
-        const int tb_end = min(ntl, tb_begin + bpc * kSBT);
-        const double R = (double)a.rmax[p];
-
-        // lanes 0..15 of wave w hold row 16w + lane's threshold state
-        const int my_row = wave * 16 + cj;
-        const float4 qrec = a.QN[(int64_t)gqb * QR + my_row];
-        const int my_pair = __float_as_int(qrec.z);
-        const int my_q = my_pair >= 0 ? my_pair / a.nprobe : -1;
-        // (kept as floats: the doubles of the bound arithmetic are formed where used)
-        const float my_qnf = qrec.x, my_qnormf = qrec.y;
-        u64 *my_list = lists + my_row * K2;
-        float qn_r[4];
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) qn_r[reg] = __shfl(my_qnf, 4 * g + reg, 64);
-        const float4 *qtg = (const float4 *)(a.QT + (int64_t)gqb * a.dpad * QR);
-        // the published bound of my row's query (plain load: nothing is in flight yet)
-        uint32_t pub = a.qbound && my_q >= 0
-            ? __hip_atomic_load(a.qbound + my_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
-        uint32_t own_pub = ~0u;
-
-        if (TRI && g == 0) {  // ||q_r - c_p|| from k_qstage (QN.w, within 1 ulp), widened by 2^-22
-            const double dq = (double)qrec.w;
-            dq_s[my_row * 2] = dq * (1.0 - 0x1p-22);
-            dq_s[my_row * 2 + 1] = dq * (1.0 + 0x1p-22);
-        }
-        if (TRI) __builtin_amdgcn_wave_barrier();
-        // the row's threshold h and (TRI) skip interval into tri_s[pr], from its
-        // list and the published bound `pub`
-        auto refresh = [&](int pr) {
-            const double my_E = err_E<METRIC>((double)my_qnormf, R, dd, 1, (double)a.dpad, a.centred);
-            const u64 kk = my_list[k - 1];
-            double T = kk == kEmptyKey ? __builtin_inf() : bound_P<METRIC>((double)key_score(kk), my_E, dd);
-            if (pub != ~0u) T = fmin(T, (double)ord2f(pub));
-            const float h = my_pair < 0 ? __builtin_inff()
-                                        : row_h<METRIC>(s_lim<METRIC>(T, my_E, dd), (double)my_qnf,
-                                                        (double)my_qnormf, R);
-            if (TRI && lane < 16) {
-                float2 ab = make_float2(-__builtin_inff(), __builtin_inff());  // never skip
-                const double F = 1.0 - (dd + 4.0) * kU;
-                if (my_pair < 0) {
-                    ab = make_float2(__builtin_inff(), -__builtin_inff());     // no query: always
-                } else if (T < 1e300 && F > 0.5) {
-                    const double rad = __builtin_sqrt((fmax(T, 0.0) + dd * 0x1p-140) / F) * (1.0 + 0x1p-40);
-                    double A = dq_s[my_row * 2] - rad, B = dq_s[my_row * 2 + 1] + rad;
-                    A -= __builtin_fabs(A) * 0x1p-50;
-                    B += __builtin_fabs(B) * 0x1p-50;
-                    ab = make_float2(__double2float_rd(A), __double2float_ru(B));
-                }
-                tri_s[pr * QR + my_row] = ab;
-            }
-            __builtin_amdgcn_wave_barrier();
-            return h;
-        };
-        const int nblk = (tb_end - tb_begin + kSBT - 1) / kSBT;  // <= kBR (planner)
-        if (TRI) {
-            for (int i = tid; i < nblk; i += NT) {
-                const int tb = tb_begin + i * kSBT, ntv = min(kSBT, tb_end - tb);
-                float lo = __builtin_inff(), hi = -__builtin_inff();
-                for (int u = 0; u < ntv; ++u) {
-                    const float2 st = a.tstat[tile0 + tb + u];
-                    lo = fminf(lo, st.x);
-                    hi = fmaxf(hi, st.y);
-                }
-                br_s[i] = make_float2(lo, hi);
-            }
-        }
-        int par = 0;
-        float h_l = refresh(par);
-        __syncthreads();  // lists, pair/bufc, br_s, tri_s[0] visible to every wave
-        // first block at or after t that some row may need (uniform across the
-        // workgroup: every wave tests all QR rows against the same LDS values)
-        auto skip_from = [&](int t, int pr) {
-            if (TRI) {
-                const float2 ab = tri_s[pr * QR + lane];
-                const float2 ab2 = QR > 64 ? tri_s[pr * QR + (QR > 64 ? 64 : 0) + lane]
-                                           : make_float2(__builtin_inff(), -__builtin_inff());
-                while (t < tb_end) {
-                    const float2 r = br_s[(t - tb_begin) / kSBT];
-                    if (!__all((r.y < ab.x || r.x > ab.y) && (r.y < ab2.x || r.x > ab2.y))) break;
-                    if (a.stats && tid == 0) atomicAdd(a.stats + 4, 1ull);
-                    t += kSBT;
-                }
-            }
-            return t;
-        };
-
-        // ---- the ring: issuer state (identical in every wave) -----------------
-        int i_tb = skip_from(tb_begin, par), i_jc = 0, n_iss = 0;
-        int vcount = 0;  // this wave's DMA instructions so far in this item
-        auto issue = [&]() {
-            if (i_tb >= tb_end) return;
-            const int slot = n_iss % NS;
-            const uint32_t base = ring_lds + (uint32_t)(slot * S::kSlot);
-            const int ntv = min(kSBT, tb_end - i_tb);
-#pragma unroll
-            for (int m = 0; m < XPW; ++m) {  // X: 16 pieces of 1 KiB (tile pc >> 2, quarter pc & 3)
-                const int pc = wave + NW * m, t = pc >> 2, qq = pc & 3;
-                sglds16(Xg + (int64_t)(tile0 + i_tb + min(t, ntv - 1)) * tstride + i_jc * (kTile / 4) + qq * 64 + lane,
-                        __builtin_amdgcn_readfirstlane(base + (uint32_t)(t * (kSDK * kTile * 4) + qq * 1024)));
-            }
-            sglds16(qtg + (int64_t)i_jc * (QR / 4) + wave * 64 + lane,  // Q: one 1-KiB piece per wave
-                    __builtin_amdgcn_readfirstlane(base + (uint32_t)S::kX + (uint32_t)wave * 1024u));
-            vcount += XPW + 1;
-            if (i_jc == 0 && wave == 0) {  // the block's xadj (tiles past its end: masked on read)
-                sglds16(a.xadj + (int64_t)(tile0 + i_tb + min(lane >> 4, ntv - 1)) * kTile + (lane & 15) * 4,
-                        __builtin_amdgcn_readfirstlane(base + (uint32_t)(S::kX + S::kQ)));
-                vcount += 1;
-            }
-            if (lane == 0) marks[wave * 8 + slot] = vcount;
-            if (tid == 0) {
-                slot_tb[slot] = i_tb;
-                slot_jc[slot] = i_jc;
-            }
-            ++n_iss;
-            i_jc += kSDK;
-            if (i_jc == dpad) {
-                i_jc = 0;
-                i_tb = skip_from(i_tb + kSBT, par);
-            }
-        };
-        for (int i = 0; i < NS - 1; ++i) issue();
-
-        f4v acc[16];
-        f4 xa[4];
-        bool wdead = true;
-        int c_tb = 0, pubmark = -1;
-#pragma unroll 1
-        for (int seq = 0; seq < n_iss; ++seq) {
-            const int slot = seq % NS;
-            // my DMA of this chunk has landed (uniform count: scalar branches only)
-            wait_vmcnt(__builtin_amdgcn_readfirstlane(vcount - marks[wave * 8 + slot]));
-            __syncthreads();  // everyone's has; the previous slot is free
-            const int tb = __builtin_amdgcn_readfirstlane(slot_tb[slot]);
-            const int jc = __builtin_amdgcn_readfirstlane(slot_jc[slot]);
-            issue();
-            const char *sb = ring + slot * S::kSlot;
-            if (jc == 0) {
-                c_tb = tb;
-                const int ntv = min(kSBT, tb_end - tb);
-                const float *xs = (const float *)(sb + S::kX + S::kQ);
-#pragma unroll
-                for (int t = 0; t < 4; ++t) xa[t] = t < ntv ? *(const f4 *)(xs + t * kTile + 4 * cj) : (f4)(__builtin_inff());
-#pragma unroll
-                for (int i = 0; i < 16; ++i) acc[i] = (f4v)(0.0f);
-                // a wave whose 16 rows all skip the block (or hold no query) computes nothing for it
-                wdead = !__any(lane < 16 && my_pair >= 0);
-                if (TRI && !wdead) {
-                    const float2 r = br_s[(tb - tb_begin) / kSBT];
-                    const float2 ab = tri_s[par * QR + wave * 16 + cj];
-                    wdead = __all(r.y < ab.x || r.x > ab.y);
-                }
-            }
-            if (!wdead && !(a.dbg & 1)) {
-                const bf16x8 a_hi = *(const bf16x8 *)(sb + S::kX + (((g & 1) * QR + wave * 16 + cj) << 4));
-                const bf16x8 a_lo = *(const bf16x8 *)(sb + S::kX + (((2 + (g & 1)) * QR + wave * 16 + cj) << 4));
-                bf16x8 bv[16];
-#pragma unroll
-                for (int t = 0; t < 4; ++t)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        bv[t * 4 + i] = *(const bf16x8 *)(sb + t * (kSDK * kTile * 4) + ((g * 64 + i * 16 + cj) << 4));
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        acc[t * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_hi, bv[t * 4 + i], acc[t * 4 + i], 0, 0, 0);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        acc[t * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_lo, bv[t * 4 + i], acc[t * 4 + i], 0, 0, 0);
-                }
-                // the next tile's B fragments in flight under this tile's 8 MFMAs (k_screen_m)
-                __builtin_amdgcn_sched_group_barrier(0x100, 10, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
-            }
-            if (jc + kSDK < dpad) continue;
-
-            // ---- the block's last chunk: thresholds, selection, bound exchange
-            if (a.stats && lane == 0) {
-                if (wave == 0) atomicAdd(a.stats + 2, 1ull);
-                if (!wdead) atomicAdd(a.stats + 0, 16ull * kSBT * kTile);
-            }
-            if (pubmark >= 0) {  // the bounds fetched at the previous block's end
-                wait_vmcnt(__builtin_amdgcn_readfirstlane(vcount - pubmark));
-                if (my_q >= 0) pub = min(pub, pub_s[wave * 16 + cj]);
-                pubmark = -1;
-            }
-            h_l = refresh(par ^ 1);  // also the skip interval for the blocks the issuer picks next
-            par ^= 1;
-            if (!wdead && !(a.dbg & 2)) {
-                const int tb = c_tb;
-                float h_r[4];
-#pragma unroll
-                for (int reg = 0; reg < 4; ++reg) h_r[reg] = from_row_lane(h_l, reg, g);
-#pragma unroll
-                for (int reg = 0; reg < 4; ++reg) {
-                    float h = h_r[reg];
-                    float wv[16];  // fl(dot - xadj) of my 16 candidates
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        const f2 w0 = (f2){acc[t * 4 + 0][reg], acc[t * 4 + 1][reg]} - xa[t].xy;
-                        const f2 w1 = (f2){acc[t * 4 + 2][reg], acc[t * 4 + 3][reg]} - xa[t].zw;
-                        wv[4 * t + 0] = w0.x;
-                        wv[4 * t + 1] = w0.y;
-                        wv[4 * t + 2] = w1.x;
-                        wv[4 * t + 3] = w1.y;
-                    }
-                    const float m01 = fmaxf(fmaxf(wv[0], wv[1]), wv[2]), m02 = fmaxf(fmaxf(wv[3], wv[4]), wv[5]);
-                    const float m03 = fmaxf(fmaxf(wv[6], wv[7]), wv[8]), m04 = fmaxf(fmaxf(wv[9], wv[10]), wv[11]);
-                    const float m05 = fmaxf(fmaxf(wv[12], wv[13]), wv[14]);
-                    const float mx = fmaxf(fmaxf(fmaxf(m01, m02), m03), fmaxf(fmaxf(m04, m05), wv[15]));
-                    if (!__any(mx >= h)) continue;  // wave-uniform: none of the four rows has a candidate
-                    int pm = 0;
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) pm |= (wv[i] >= h && xa[i >> 2][i & 3] != __builtin_inff()) << i;
-                    auto score = [&](int i) {
-                        const float av = xa[i >> 2][i & 3], dv = acc[i][reg];
-                        return METRIC == LIRA_METRIC_L2 ? __builtin_fmaf(-2.0f, dv, qn_r[reg] + 2.0f * av) : -dv;
-                    };
-                    if (__any(h == -__builtin_inff()) && k <= 64) {
-                        // a row without a bound yet: t = ceil(k/16) smallest of each
-                        // of its 16 lanes, j = ceil(k/t) <= 16 over those lanes
-                        float m4[4] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};
-#pragma unroll
-                        for (int i = 0; i < 16; ++i) {
-                            const float sv = score(i);
-                            float v = xa[i >> 2][i & 3] != __builtin_inff() && sv == sv ? sv : __builtin_inff();
-#pragma unroll
-                            for (int u = 0; u < 4; ++u) {
-                                const float lo = fminf(m4[u], v), hi = fmaxf(m4[u], v);
-                                m4[u] = lo;
-                                v = hi;
-                            }
-                        }
-                        const int t = (k + 15) / 16;
-                        uint32_t key16 = f2ord(t <= 1 ? m4[0] : t == 2 ? m4[1] : t == 3 ? m4[2] : m4[3]);
-#pragma unroll
-                        for (int size = 2; size <= 16; size <<= 1)
-#pragma unroll
-                            for (int stride = size >> 1; stride > 0; stride >>= 1) {
-                                const uint32_t o = xor_u32(key16, stride);
-                                const bool lower = (cj & stride) == 0, asc = (cj & size) == 0;
-                                key16 = (lower == asc) ? min(key16, o) : max(key16, o);
-                            }
-                        const int j = (k + t - 1) / t;
-                        const float B = ord2f((uint32_t)__shfl((int)key16, 16 * g + j - 1, 64));
-                        if (h == -__builtin_inff() && B < __builtin_inff()) {
-                            const double qnorm_r = (double)__shfl(my_qnormf, 4 * g + reg, 64);
-                            const double E_r = err_E<METRIC>(qnorm_r, R, dd, 1, (double)a.dpad, a.centred);
-                            h = row_h<METRIC>(s_lim<METRIC>(bound_P<METRIC>((double)B, E_r, dd), E_r, dd),
-                                              (double)qn_r[reg], qnorm_r, R);
-                            int pm2 = 0;
-#pragma unroll
-                            for (int i = 0; i < 16; ++i) pm2 |= (acc[i][reg] - xa[i >> 2][i & 3] >= h) << i;
-                            pm &= pm2;
-                        }
-                    }
-                    {
-                        const int row = wave * 16 + 4 * g + reg;
-                        const int bc0 = m_bufc[row];
-                        const int n_l = __builtin_popcount(pm);
-                        const int inc = row16_incl_scan(n_l);  // inclusive prefix over the group's 16 lanes
-                        const int rowtot = row16_total(inc);
-                        const bool pre = bc0 > 0 && bc0 + rowtot > BC;
-                        const int total = (pre ? 0 : bc0) + rowtot;
-                        const int base = (pre ? 0 : bc0) + inc - n_l;
-                        for (int r0 = 0;; r0 += BC) {
-                            u64 fl = __ballot((r0 == 0 ? pre : total > r0) && cj == 0);
-                            while (fl) {
-                                const int gg = __builtin_ctzll(fl) >> 4;
-                                fl &= fl - 1;
-                                const int r = wave * 16 + 4 * gg + reg;
-                                s_flush<RL>(lists + r * K2, bufs + r * BC, r0 == 0 ? __builtin_amdgcn_readlane(bc0, 16 * gg) : BC);
-                            }
-                            int rank = base;
-#pragma unroll
-                            for (int v = 0; v < 16; ++v) {
-                                if ((pm >> v) & 1) {
-                                    if (rank >= r0 && rank < r0 + BC)
-                                        bufs[row * BC + rank - r0] =
-                                            ((u64)f2ord(score(v)) << 32) |
-                                            (uint32_t)((tile0 + tb + (v >> 2)) * kTile + 4 * cj + (v & 3));
-                                    ++rank;
-                                }
-                            }
-                            __builtin_amdgcn_wave_barrier();
-                            if (!__any(total - r0 > BC)) break;
-                        }
-                        if (cj == 0) {
-                            m_bufc[row] = total <= BC ? total : total - BC * ((total - 1) / BC);
-                            if (a.stats && rowtot) atomicAdd(a.stats + 7, (unsigned long long)rowtot);
-                        }
-                        __builtin_amdgcn_wave_barrier();
-                    }
-                }
-            }
-            // publish my rows' bounds when they improved, and fetch the query's
-            // bounds by DMA for the next block's thresholds
-            if (a.share && a.qbound) {
-                if (lane < 16 && my_q >= 0) {
-                    const u64 kk = my_list[k - 1];
-                    if (kk != kEmptyKey) {
-                        const double my_E = err_E<METRIC>((double)my_qnormf, R, dd, 1, (double)a.dpad, a.centred);
-                        const uint32_t b = f2ord(__double2float_ru(bound_P<METRIC>((double)key_score(kk), my_E, dd)));
-                        if (b < own_pub) {
-                            atomicMin(a.qbound + my_q, b);
-                            own_pub = b;
-                        }
-                    }
-                }
-                if (lane < 16)
-                    sglds4(a.qbound + (my_q >= 0 ? my_q : 0),
-                           __builtin_amdgcn_readfirstlane(pub_lds + (uint32_t)(wave * 64)));
-                vcount += 1;
-                pubmark = vcount;
-            }
-        }
-
-        // ---- flush buffers, emit lists, publish bounds (wave-owned rows)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (a pending bound fetch into pub_s)
-#pragma unroll 1
-        for (int r = 0; r < 16; ++r) {
-            const int row = wave * 16 + r;
-            const int bc = m_bufc[row];
-            if (bc > 0) s_flush<RL>(lists + row * K2, bufs + row * BC, bc);
-            const int pr = m_pair[row];
-            if (pr >= 0) {
-                u64 *dst = a.partial + ((int64_t)pr * a.nch_max + ch) * K2;
-                for (int e = lane; e < K2; e += 64) dst[e] = lists[row * K2 + e];
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (lane < 16 && a.qbound && my_q >= 0) {
-            const u64 kk = my_list[k - 1];
-            if (kk != kEmptyKey) {
-                const double my_E = err_E<METRIC>((double)my_qnormf, R, dd, 1, (double)a.dpad, a.centred);
-                const double P = bound_P<METRIC>((double)key_score(kk), my_E, dd);
-                atomicMin(a.qbound + my_q, f2ord(__double2float_ru(P)));
-            }
-        }
-        __syncthreads();
-    }
-}
-
 // ---- seed: a finite starting bound for every query ----------------------
 // One wave per query: exact scores of the first kSeedTiles tiles (256 rows) of its first
 // probed partition; with t = ceil(k/64) smallest per lane and j = ceil(k/t),
@@ -2055,192 +1552,6 @@ __global__ __launch_bounds__(QR * 4, OCC) void k_screen_s(ScreenArgs a) {
 // before k_screen, so no item starts unbounded (which would push a whole
 // first block per row through the selection).
 static constexpr int kSeedTiles = 4;
-// The same bound per group-0 query block (k_plan's first group: the QB pairs
-// whose first probe slot is partition p), one workgroup each: the queries of
-// a block share the partition, so its first NR storage rows (row-major Xr; in
-// radius order its central rows) are staged in LDS once, 32 dims at a time,
-// for all QB queries (k_seed_t reads them once per query).  Lane = query,
-// wave w = rows w, w + 4, ...; each (query, row) score is one lane's
-// sequential sum in search.cpp's order, two rows per packed fp32 instruction
-// (v_pk_add_f32 / v_pk_mul_f32 round each half like the scalar ops).  Each
-// lane keeps its 8 smallest valid scores per wave; the k-th smallest of the
-// four waves' lists has >= k distinct rows at or below it, so it bounds the
-// final k-th exact score (k <= 32).
-template <int METRIC, int QB, int NR>
-__global__ __launch_bounds__(256) void k_seed_b(const float *Q, int64_t d, int nprobe, int n_lists,
-                                                const int32_t *cnt, const int32_t *qoff, const int32_t *qlist,
-                                                const int32_t *qblk_off, const int32_t *tile_off,
-                                                const int32_t *ids, const float *Xr, int k, uint32_t *qbound) {
-    static_assert(QB == 64 && NR % 4 == 0, "lane = query");
-    constexpr int RW = NR / 4, DS = 32;
-    __shared__ float4 xs[NR][DS / 4];
-    __shared__ float qs[DS][QB + 1];
-    __shared__ int s_v, s_q[QB], s_ok[NR];
-    __shared__ float s_m[4][8][QB];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int b = blockIdx.x;
-    if (b >= qblk_off[n_lists]) return;  // (group 0: v < n_lists)
-    if (w == 0) {
-        const int v = wave_find_owner(qblk_off, n_lists, b);
-        if (lane == 0) s_v = v;
-    }
-    __syncthreads();
-    const int p = s_v, qb = b - qblk_off[p];
-    const int nval = min(QB, cnt[p] - qb * QB);
-    const int tile0 = tile_off[p], nrow = min(NR, (tile_off[p + 1] - tile0) * kTile);
-    const int64_t row0 = (int64_t)tile0 * kTile;
-    if (tid < QB) s_q[tid] = tid < nval ? qlist[qoff[p] + qb * QB + tid] / nprobe : -1;
-    for (int r = tid; r < NR; r += 256) s_ok[r] = r < nrow && ids[row0 + r] >= 0;
-    __syncthreads();
-    f2 acc[RW / 2];  // rows 8r + w, 8r + 4 + w (wave w: rows w, w + 4, ... -- every wave
-                     // gets central and outer rows of the radius order alike)
-#pragma unroll
-    for (int r = 0; r < RW / 2; ++r) acc[r] = (f2)(0.0f);
-    // staging: thread tid moves the 16-B pieces e = tid + 256 i (row e / 8,
-    // dims 4 (e % 8) ..), all loads of a slab in flight together, the next
-    // slab's loaded into registers while this one is computed
-    constexpr int XP = NR * DS / 4 / 256, QP = QB * DS / 4 / 256;  // pieces per thread
-    const bool v4 = (d & 3) == 0;
-    float4 xr[XP], qr[QP];
-    auto load = [&](int64_t j0) {
-        const int nj = (int)min<int64_t>(DS, d - j0);
-#pragma unroll
-        for (int i = 0; i < XP; ++i) {
-            const int e = tid + 256 * i, r = e >> 3, c = 4 * (e & 7);
-            const float *src = Xr + (row0 + r) * d + j0 + c;
-            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (r < nrow && v4 && c + 4 <= nj) {
-                v = *(const float4 *)src;
-            } else if (r < nrow) {
-                if (c < nj) v.x = src[0];
-                if (c + 1 < nj) v.y = src[1];
-                if (c + 2 < nj) v.z = src[2];
-                if (c + 3 < nj) v.w = src[3];
-            }
-            xr[i] = v;
-        }
-#pragma unroll
-        for (int i = 0; i < QP; ++i) {
-            const int e = tid + 256 * i, qq = e >> 3, c = 4 * (e & 7), qi = s_q[qq];
-            const float *src = Q + (int64_t)qi * d + j0 + c;
-            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (qi >= 0 && v4 && c + 4 <= nj) {
-                v = *(const float4 *)src;
-            } else if (qi >= 0) {
-                if (c < nj) v.x = src[0];
-                if (c + 1 < nj) v.y = src[1];
-                if (c + 2 < nj) v.z = src[2];
-                if (c + 3 < nj) v.w = src[3];
-            }
-            qr[i] = v;
-        }
-    };
-    load(0);
-    for (int64_t j0 = 0; j0 < d; j0 += DS) {
-        const int nj = (int)min<int64_t>(DS, d - j0);
-#pragma unroll
-        for (int i = 0; i < XP; ++i) {
-            const int e = tid + 256 * i;
-            xs[e >> 3][e & 7] = xr[i];
-        }
-#pragma unroll
-        for (int i = 0; i < QP; ++i) {
-            const int e = tid + 256 * i, qq = e >> 3, c = 4 * (e & 7);
-            qs[c][qq] = qr[i].x;
-            qs[c + 1][qq] = qr[i].y;
-            qs[c + 2][qq] = qr[i].z;
-            qs[c + 3][qq] = qr[i].w;
-        }
-        __syncthreads();
-        if (j0 + DS < d) load(j0 + DS);
-        for (int c4 = 0; c4 < DS / 4 && 4 * c4 < nj; ++c4) {
-            const int nc = min(4, nj - 4 * c4);  // (workgroup-uniform)
-            const f2 q0 = (f2)(qs[4 * c4][lane]), q1 = (f2)(qs[4 * c4 + 1][lane]);
-            const f2 q2 = (f2)(qs[4 * c4 + 2][lane]), q3 = (f2)(qs[4 * c4 + 3][lane]);
-            if (nc == 4) {
-#pragma unroll
-                for (int r = 0; r < RW / 2; ++r) {  // rows 8r + w and 8r + 4 + w, packed
-                    const float4 xa = xs[8 * r + w][c4], xb = xs[8 * r + 4 + w][c4];
-                    const f2 x0 = {xa.x, xb.x}, x1 = {xa.y, xb.y}, x2 = {xa.z, xb.z}, x3 = {xa.w, xb.w};
-                    if (METRIC == LIRA_METRIC_L2) {
-                        f2 df = q0 - x0;
-                        acc[r] = acc[r] + df * df;
-                        df = q1 - x1;
-                        acc[r] = acc[r] + df * df;
-                        df = q2 - x2;
-                        acc[r] = acc[r] + df * df;
-                        df = q3 - x3;
-                        acc[r] = acc[r] + df * df;
-                    } else {
-                        acc[r] = acc[r] + q0 * x0;
-                        acc[r] = acc[r] + q1 * x1;
-                        acc[r] = acc[r] + q2 * x2;
-                        acc[r] = acc[r] + q3 * x3;
-                    }
-                }
-            } else {  // the last dims of d (d % 4 != 0)
-                const f2 qq[4] = {q0, q1, q2, q3};
-                for (int u = 0; u < nc; ++u) {
-#pragma unroll
-                    for (int r = 0; r < RW / 2; ++r) {
-                        const f2 xv = {((const float *)&xs[8 * r + w][c4])[u], ((const float *)&xs[8 * r + 4 + w][c4])[u]};
-                        if (METRIC == LIRA_METRIC_L2) {
-                            const f2 df = qq[u] - xv;
-                            acc[r] = acc[r] + df * df;
-                        } else {
-                            acc[r] = acc[r] + qq[u] * xv;
-                        }
-                    }
-                }
-            }
-        }
-        __syncthreads();
-    }
-    // this lane's 8 smallest valid scores of the wave's RW rows, sorted
-    float m[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) m[i] = __builtin_inff();
-#pragma unroll
-    for (int r = 0; r < RW; ++r) {
-        const int row = 8 * (r >> 1) + 4 * (r & 1) + w;
-        const float a = (r & 1) ? acc[r >> 1].y : acc[r >> 1].x;
-        const float sc = METRIC == LIRA_METRIC_L2 ? a : -a;
-        float v = s_ok[row] && sc == sc ? sc : __builtin_inff();
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const float lo = fminf(m[i], v), hi = fmaxf(m[i], v);
-            m[i] = lo;
-            v = hi;
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) s_m[w][i][lane] = m[i];
-    __syncthreads();
-    // the k-th smallest of the four lists' union: >= k rows at or below it
-    // (the exact k-th over all NR rows for k <= 8)
-    if (w == 0 && s_q[lane] >= 0) {
-        int h[4] = {0, 0, 0, 0};
-        float B = __builtin_inff();
-        for (int e = 0; e < k; ++e) {
-            float best = __builtin_inff();
-            int bw = -1;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const float v = h[u] < 8 ? s_m[u][h[u]][lane] : __builtin_inff();
-                if (v < best) {
-                    best = v;
-                    bw = u;
-                }
-            }
-            B = best;
-            if (bw < 0) break;  // fewer than k valid rows: no bound
-#pragma unroll
-            for (int u = 0; u < 4; ++u) h[u] += bw == u;
-        }
-        if (B < __builtin_inff()) qbound[s_q[lane]] = f2ord(B);
-    }
-}
-
 // The same bound from the fp32 tiles where the index keeps them (one wave per
 // query, lane = candidate: each dim of a tile is one coalesced 256-B row).
 // NT tiles: 2 for k <= 32 (measured SIFT1M mixture: plan 0.217 -> 0.164 ms,
@@ -2660,7 +1971,50 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
     }
 }
 
+// ---- per-pair records + the partition filter (lira_bounds.hpp pair_record) ----
+// One pair per 16 lanes, the filter bound from qbound (k_seed_t's seed); the
+// default L2 screen runs the same records inside k_seed_t<..., PAIRS> instead.
+__global__ __launch_bounds__(256) void k_pairs(const float *Q, int64_t d, const int32_t *probe, int64_t npairs,
+                                               int nprobe, int n_lists, const float *pivot, int centred,
+                                               const float2 *lstat, const uint32_t *qbound, int32_t *probe_live,
+                                               float4 *QN, float *QE, float *pqn, uint16_t *QH, int64_t dpad) {
+    const int64_t pair = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+    const bool valid = pair < npairs;
+    const int praw = valid ? probe[pair] : -1;
+    const uint32_t qb = valid && lstat && qbound ? qbound[pair / nprobe] : ~0u;
+    pair_record(Q, d, pair, valid, praw, nprobe, n_lists, pivot, centred, lstat && qbound ? lstat : nullptr, qb,
+                probe_live, QN, QE, pqn, QH, dpad);
+}
+
+// (stats on) what the plan's partition filter removed: pairs whose probe slot
+// is valid but probe_live = -1 -> stats[1], and their candidates (list sizes:
+// (query, candidate) pairs never screened) -> stats[3]
+__global__ __launch_bounds__(256) void k_prune_stats(const int32_t *probe, const int32_t *plive, int64_t npairs,
+                                                     int n_lists, const int32_t *list_size,
+                                                     unsigned long long *stats) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int p = i < npairs ? probe[i] : -1;
+    const bool cut = p >= 0 && p < n_lists && plive[i] < 0;
+    const unsigned long long c = cut ? 1ull : 0ull, n = cut ? (unsigned long long)list_size[p] : 0ull;
+    const unsigned long long cs = wave_sum_u64(c), ns = wave_sum_u64(n);
+    if ((threadIdx.x & 63) == 0 && cs) {
+        atomicAdd(stats + 1, cs);
+        atomicAdd(stats + 3, ns);
+    }
+}
+
 // ------------------------------------------------------------------ host side
+
+static hipError_t launch_pairs(const float *Q, int64_t d, const int32_t *probe, int64_t npairs, int nprobe,
+                               int n_lists, const float *pivot, int centred, const float2 *lstat,
+                               const uint32_t *qbound, int32_t *probe_live, float4 *QN, float *QE, float *pqn,
+                               uint16_t *QH, int64_t dpad, hipStream_t st) {
+    const unsigned g = (unsigned)((npairs * 16 + 255) / 256);
+    if (g == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pairs, dim3(g), dim3(256), 0, st, Q, d, probe, npairs, nprobe, n_lists, pivot, centred, lstat,
+                       qbound, probe_live, QN, QE, pqn, QH, dpad);
+    return hipGetLastError();
+}
 
 static int cu_count_s(int device) {
     static int cached[64] = {0};
@@ -2685,14 +2039,11 @@ static int screen_smem(int qr, int rl) {
 struct SPlan {
     int rl = 1, qr = 64, K2 = 32, bpc = 1, bpc_near = 1, nch_max = 1, grid = 1, smem = 0, mfma = 1, split = 0;
     int bpc_near_min = 1, workers = 1;  // the plan picks group 0's chunk size in [bpc_near_min, bpc_near]
-    int v2 = 0, ns = 2, bc = 32;  // the pipelined split screen (k_screen_s): ring slots, buffer keys per row
-    int pp = 0;                   // per-pair query records (QN / QE / QH per pair, k_pairs or k_seed_t<.., PAIRS>)
-                                  // instead of k_qstage's per-block copy: the hi x hi k_screen_m and the wide screens
-    int wide = 0;                 // 1: the wide screen (lira_wscreen.hip k_screen_w), 256 rows per item;
-                                  // 2: the wave-resident screen (lira_vscreen.hip k_screen_v), 64 rows per wave
+    int pp = 0;  // per-pair query records (QN / QE / QH per pair, k_pairs or k_seed_t<.., PAIRS>)
+                 // instead of k_qstage's per-block copy: the hi x hi k_screen_m
     int64_t max_qblk = 0;
     size_t off_cnt, off_cursor, off_head, off_qoff, off_item, off_nch, off_qblk, off_itab, off_qlist, off_qt, off_qn,
-        off_partial, off_qbound, off_pqn, off_pe, off_qe, off_live, off_wrec, total;
+        off_partial, off_qbound, off_pqn, off_pe, off_qe, off_live, total;
 };
 
 static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, unsigned flags) {
@@ -2735,38 +2086,15 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // 0.67 mixture (survivors +4 %: the bound's extra ||q - qh|| R is small
     // against the score spread)
     const int xhi = op.xhi >= 0 ? op.xhi : idx->metric == LIRA_METRIC_L2 && idx->pivot != nullptr ? 2 : 0;
-    if (pl.split && xhi && pl.qr != 32 && pl.rl <= (pl.qr == 64 ? 4 : 1) && !(op.pipeline && (pl.rl == 4 || op.ring > 0)))
-        pl.split = 2;
+    if (pl.split && xhi && pl.qr != 32 && pl.rl <= (pl.qr == 64 ? 4 : 1)) pl.split = 2;
     if (pl.split == 2 && xhi == 2 && pl.qr == 64 && pl.rl == 1) pl.split = 3;
-    // the pipelined split screen (LIRA_OPT_PIPELINE): RL 1 at 128 queries per item
-    // (8 waves, 4 ring slots, 16-key buffers), RL 2 at 64 (4 slots), RL 4 at 64 (3 slots)
-    // (measured, SIFT1M / GIST1M, k = 10: every ring / QR variant of k_screen_s
-    // slower than k_screen_m's ring at 2 workgroups per CU -- its LDS leaves 1
-    // workgroup per CU; DEEP10M k = 100: 28.1 ms, k_screen_m 24.1 ms since its
-    // fragment reads are pipelined), so only where LIRA_OPT_PIPELINE = 1 (RL 4)
-    // or LIRA_OPT_RING asks for it
-    pl.v2 = pl.split && pl.qr != 32 && op.pipeline && (pl.rl == 4 || op.ring > 0);
-    if (pl.v2) {
-        pl.qr = pl.rl == 1 && op.qr != 64 ? 128 : 64;
-        pl.ns = pl.rl == 4 ? 3 : 4;
-        if (op.ring >= 2 && op.ring <= 4 && pl.rl == 1) pl.ns = op.ring;  // (A/B: 64 x 2/4 and 128 x 3/4 built)
-        if (pl.qr == 64 && pl.rl == 1 && pl.ns == 3) pl.ns = 4;
-        if (pl.qr == 128 && pl.ns == 2) pl.ns = 3;
-        pl.bc = pl.qr == 128 && pl.ns == 4 ? 16 : 32;
-    }
+    // (round 3 measured a pipelined NS-slot ring screen, k_screen_s, slower on
+    // every config -- DEEP10M 28.1 vs 24.9 ms; removed in round 4, git history keeps it)
     pl.K2 = 32 * pl.rl;
-    // the wide screen (LIRA_OPT_WIDE): the hi x hi form at 256 rows per item where its
-    // shape applies; it needs the per-query seeded bound (not PER_PARTITION)
-    // (both need the per-query seeded bound: not PER_PARTITION, LIRA_OPT_SEED on)
-    pl.wide = op.wide && pl.split == 3 && !pl.v2 && pl.rl == 1 && idx->xadjc && idx->tstat && idx->lstat &&
-              (op.wide == 2 ? vscreen_shape_ok(idx->dpad) : wscreen_shape_ok(idx->dpad)) && op.seed &&
-              !(flags & LIRA_SCAN_PER_PARTITION) ? op.wide : 0;
-    if (pl.wide) pl.qr = pl.wide == 2 ? vscreen_rows() : 256;
-    pl.pp = pl.wide || (pl.split == 3 && !pl.v2);
-    pl.smem = pl.wide == 2 ? vscreen_smem() : pl.wide ? wscreen_smem() : pl.v2 ? (pl.qr == 128 ? (pl.ns == 4 ? SSmem2<128, 1, 4, 16>::total : SSmem2<128, 1, 3, 32>::total)
-                                     : pl.rl == 1 ? (pl.ns == 4 ? SSmem2<64, 1, 4, 32>::total : SSmem2<64, 1, 2, 32>::total)
-                                     : pl.rl == 2 ? SSmem2<64, 2, 4, 32>::total : SSmem2<64, 4, 3, 32>::total)
-              : !pl.mfma       ? screen_smem(pl.qr, pl.rl)
+    // (the wide k_screen_w and wave-resident k_screen_v screens measured 0.571 /
+    // 1.50 ms against 0.325 on SIFT1M: removed in round 4)
+    pl.pp = pl.split == 3;
+    pl.smem = !pl.mfma       ? screen_smem(pl.qr, pl.rl)
               : pl.qr == 128 ? (pl.split == 2 ? SSmem<128, 1, true, true>::total
                                 : pl.rl == 1 ? SSmem<128, 1, true>::total : SSmem<128, 2, true>::total)
               : pl.split == 3 ? SSmem<64, 1, true, false, true>::total
@@ -2777,14 +2105,13 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
               : pl.rl == 2   ? SSmem<64, 2, true>::total
                              : SSmem<64, 4, true>::total;
     const int64_t npairs = nq * nprobe;
-    pl.grid = pl.wide ? cu_count_s(idx->device) : cu_count_s(idx->device) * std::max(1, std::min(2, (160 * 1024) / pl.smem));
+    pl.grid = cu_count_s(idx->device) * std::max(1, std::min(2, (160 * 1024) / pl.smem));
     if (op.debug & 32) pl.grid = cu_count_s(idx->device);  // timing experiment: one workgroup per CU
     // ~8 items per workgroup: fewer item prologues/epilogues and row lists to
     // merge than k_scan's 16 (measured: SIFT1M scan + merge 1.47 -> 1.22 ms on
     // the mixture, 4.80 -> 4.66 ms on latent data; 4 and 32 slower overall)
-    // (k_screen_v: every wave is its own worker: CUs x waves per CU of them)
-    const int workers = pl.wide == 2 ? cu_count_s(idx->device) * vscreen_workers_per_cu() : pl.grid;
-    const int rounds = op.rounds > 0 ? op.rounds : pl.wide == 2 ? 4 : pl.wide ? 4 : 8;
+    const int workers = pl.grid;
+    const int rounds = op.rounds > 0 ? op.rounds : 8;
     const int64_t target = (int64_t)rounds * workers;
     // (LIRA_OPT_PROBES_HINT: the probe lists are mostly -1 padding, e.g. a
     // threshold selection padded to B; size the chunking for the expected pairs)
@@ -2811,17 +2138,8 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // k_screen_m stages the radius ranges of an item's first kBR blocks in LDS; a
     // longer item would read them from global memory inside the ring (whose
     // compiler-inserted waits drain it): cap the chunk at kBR blocks
-    if (!pl.v2 && pl.mfma && idx->metric == LIRA_METRIC_L2 && idx->pivot) {
+    if (pl.mfma && idx->metric == LIRA_METRIC_L2 && idx->pivot) {
         pl.bpc = std::min(pl.bpc, SSmem<64, 1, true>::kBR);
-        pl.bpc_near = std::min(pl.bpc_near, pl.bpc);
-    }
-    if (pl.wide) {  // k_screen_w holds <= 128 blocks of 128 candidates per item in registers,
-                    // k_screen_v <= 128 tiles
-        pl.bpc = std::min(pl.bpc, pl.wide == 2 ? vscreen_max_tiles() / kSBT : 64);
-        pl.bpc_near = std::min(pl.bpc_near, pl.bpc);
-    }
-    if (pl.v2 && idx->metric == LIRA_METRIC_L2 && idx->pivot) {  // k_screen_s stages <= kBR block ranges per item
-        pl.bpc = std::min(pl.bpc, SSmem2<64, 1, 4, 32>::kBR);
         pl.bpc_near = std::min(pl.bpc_near, pl.bpc);
     }
     // k_screen_m + k_smerge with the default near_rounds: the plan picks group 0's
@@ -2833,7 +2151,7 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     const bool two = !(flags & LIRA_SCAN_PER_PARTITION) && op.two_phase && nprobe >= 2 &&
                      (op.two_phase == 2 || nq >= (int64_t)pl.qr * idx->n_lists ||
                       nq * nprobe >= 4 * (int64_t)pl.qr * idx->n_lists);
-    if (two && op.near_rounds <= 0 && pl.mfma && !pl.v2 && !pl.wide) {
+    if (two && op.near_rounds <= 0 && pl.mfma) {
         const int64_t est0 = std::min<int64_t>(nq, (nq + pl.qr - 1) / pl.qr + idx->n_lists);
         const int64_t split6 = std::max<int64_t>(1, (6 * (int64_t)workers + est0 - 1) / std::max<int64_t>(1, est0));
         pl.bpc_near_min = (int)std::min<int64_t>(pl.bpc_near, std::max<int64_t>(1, (max_blocks + split6 - 1) / split6));
@@ -2856,11 +2174,9 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     pl.off_nch = take(nl * 4);
     pl.off_qblk = take((nl + 1) * 4);
     pl.off_itab = take((size_t)(pl.max_qblk + 1) * pl.nch_max * 16);  // items <= query blocks x chunks
-    pl.off_wrec = take(pl.wide ? (size_t)(pl.max_qblk + 1) * pl.nch_max * 32 : 0);  // (wide) per-item records
     pl.off_qlist = take((size_t)npairs * 4);
-    // (wide: no transposed query copy; QN / QE per pair, from k_pairs)
-    // (per-pair records: QH, the rows' hi(q - c) per pair, in the QT slot; k_screen_w reads Q itself)
-    pl.off_qt = take(pl.wide == 1 ? 0 : pl.pp ? (size_t)npairs * idx->dpad * 2 : (size_t)pl.max_qblk * pl.qr * idx->dpad * 4);
+    // (per-pair records: QH, the rows' hi(q - c) per pair, in the QT slot)
+    pl.off_qt = take(pl.pp ? (size_t)npairs * idx->dpad * 2 : (size_t)pl.max_qblk * pl.qr * idx->dpad * 4);
     pl.off_qn = take(pl.pp ? (size_t)npairs * 16 : (size_t)pl.max_qblk * pl.qr * 16);
     pl.off_qe = take(pl.pp ? (size_t)npairs * 4 : (size_t)pl.max_qblk * pl.qr * 4);
     pl.off_live = take((size_t)npairs * 4);
@@ -2886,11 +2202,7 @@ size_t screen_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, 
 // the kernel a screened scan of this shape runs (lira_scan_describe)
 std::string screen_describe(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, unsigned flags) {
     SPlan pl = make_splan(idx, nq, nprobe, k, flags);
-    std::string s = pl.wide == 2 ? "k_screen_v hi-x hi-q bf16 v_mfma_f32_16x16x32_bf16"
-                    : pl.wide ? "k_screen_w hi-x hi-q bf16 v_mfma_f32_32x32x16_bf16"
-                    : pl.v2 ? "k_screen_s split-bf16 v_mfma_f32_16x16x32_bf16 NS=" + std::to_string(pl.ns) +
-                                " BC=" + std::to_string(pl.bc)
-                    : pl.mfma ? (pl.split == 3 ? "k_screen_m hi-x hi-q bf16 v_mfma_f32_16x16x32_bf16"
+    std::string s = pl.mfma ? (pl.split == 3 ? "k_screen_m hi-x hi-q bf16 v_mfma_f32_16x16x32_bf16"
                                  : pl.split == 2 ? "k_screen_m hi-x split-bf16 v_mfma_f32_16x16x32_bf16"
                                  : pl.split ? "k_screen_m split-bf16 v_mfma_f32_16x16x32_bf16"
                                         : "k_screen_m fp32 v_mfma_f32_16x16x4_f32")
@@ -2923,29 +2235,8 @@ static hipError_t launch_screen_m(const ScreenArgs &a, const SPlan &pl, hipStrea
     return hipGetLastError();
 }
 
-template <int M, int RL, int QR, int NS, int BC>
-static hipError_t launch_screen_s(const ScreenArgs &a, const SPlan &pl, hipStream_t st) {
-    constexpr int smem = SSmem2<QR, RL, NS, BC>::total;
-    static_assert(smem <= 160 * 1024, "k_screen_s LDS");
-    constexpr int OCC = (160 * 1024) / smem >= 2 ? 2 : 1;
-    static std::atomic<uint64_t> attr{0};
-    hipError_t e = set_smem_attr_once(attr, (const void *)k_screen_s<M, RL, QR, NS, BC, OCC>, smem);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_screen_s<M, RL, QR, NS, BC, OCC>), dim3(pl.grid), dim3(QR * 4), smem, st, a);
-    return hipGetLastError();
-}
-
 template <int M>
 static hipError_t launch_screen_rl(const ScreenArgs &a, const SPlan &pl, hipStream_t st) {
-    if (pl.v2) {
-        if (pl.qr == 128)
-            return pl.ns == 4 ? launch_screen_s<M, 1, 128, 4, 16>(a, pl, st) : launch_screen_s<M, 1, 128, 3, 32>(a, pl, st);
-        switch (pl.rl) {
-            case 1: return pl.ns == 4 ? launch_screen_s<M, 1, 64, 4, 32>(a, pl, st) : launch_screen_s<M, 1, 64, 2, 32>(a, pl, st);
-            case 2: return launch_screen_s<M, 2, 64, 4, 32>(a, pl, st);
-            default: return launch_screen_s<M, 4, 64, 3, 32>(a, pl, st);
-        }
-    }
     if (pl.mfma) {
         if (pl.qr == 128 && pl.split == 2) return launch_screen_m<M, 1, 128, 2>(a, pl, st);
         if (pl.qr == 128 && pl.split)
@@ -3049,16 +2340,12 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     float *pqn = centred ? (float *)(w + pl.off_pqn) : nullptr;
     // seed bound per query (k_seed_t / k_seed) before the plan, so that
     // k_pairs can drop the pairs whose whole list lies outside the query's
-    // triangle interval under it (they get no work item and no lists); the
-    // block-shared seed k_seed_b (LIRA_OPT_SEED 2 / 3) needs the plan's query
-    // blocks and runs after it, without the filter
-    const bool seed_b = qbound && (o.seed == 2 || o.seed == 3) && groups == 2 && k <= 32 && pl.qr == 64 &&
-                        idx->d <= 256;
-    const bool filter = qbound && tri && !seed_b && o.seed && idx->lstat != nullptr;
+    // triangle interval under it (they get no work item and no lists)
+    const bool filter = qbound && tri && o.seed && idx->lstat != nullptr;
     int32_t *plive = filter || pl.pp ? (int32_t *)(w + pl.off_live) : nullptr;
-    uint16_t *QH = pl.pp && pl.wide != 1 ? (uint16_t *)QT : nullptr;
+    uint16_t *QH = pl.pp ? (uint16_t *)QT : nullptr;
     // the per-pair records inside the seed kernel where it is k_seed_t (L2, k <= 32)
-    const bool fused = plive && !seed_b && qbound && o.seed && idx->X && idx->metric == LIRA_METRIC_L2 && k <= 32;
+    const bool fused = plive && qbound && o.seed && idx->X && idx->metric == LIRA_METRIC_L2 && k <= 32;
     if (qbound && !fused) LIRA_HIP_TRY(hipMemsetAsync(qbound, 0xff, (size_t)nq * 4, st));
     if (fused) {
         SeedPairs sp;
@@ -3079,7 +2366,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
                            probe, (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad,
                            nq, (int)k, qbound, sp);
         LIRA_HIP_TRY(hipGetLastError());
-    } else if (!seed_b && qbound && o.seed && idx->X) {  // from the fp32 tiles (coalesced)
+    } else if (qbound && o.seed && idx->X) {  // from the fp32 tiles (coalesced)
         const dim3 g((unsigned)((nq + 3) / 4));
         if (idx->metric == LIRA_METRIC_L2 && k <= 32)
             hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2, 2>), g, dim3(256), 0, st, q, probe, (int)nprobe,
@@ -3094,7 +2381,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
             hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_IP>), g, dim3(256), 0, st, q, probe, (int)nprobe,
                                (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound, SeedPairs());
         LIRA_HIP_TRY(hipGetLastError());
-    } else if (!seed_b && qbound && o.seed) {  // compact index: from the row-major copy
+    } else if (qbound && o.seed) {  // compact index: from the row-major copy
         if (idx->metric == LIRA_METRIC_L2)
             hipLaunchKernelGGL(k_seed<LIRA_METRIC_L2>, dim3((unsigned)nq), dim3(256), 0, st, q, probe,
                                (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->Xr, idx->d, nq,
@@ -3139,27 +2426,6 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     LIRA_HIP_TRY(hipGetLastError());
     }
     // (measured: SIFT1M mixture 1.70 -> 1.44 ms, latent +1 %)
-    // LIRA_OPT_SEED 2 / 3: per nearest-partition query block (k_seed_b, 128 /
-    // 256 rows) where the plan has that group.  Measured SIFT1M: the same
-    // survivors as k_seed_t's 128 rows, plan 0.122 -> 0.143 ms (~220 workgroups
-    // of exact VALU work leave most of the chip idle); 256 rows: survivors
-    // -28 %, scan -0.02 ms, plan +0.06 ms.  So the per-query seed is the default.
-    if (seed_b) {
-        const dim3 g((unsigned)std::min<int64_t>(pl.max_qblk, (nq + 63) / 64 + idx->n_lists));
-        if (idx->metric == LIRA_METRIC_L2 && o.seed == 3)
-            hipLaunchKernelGGL((k_seed_b<LIRA_METRIC_L2, 64, 256>), g, dim3(256), 0, st, q, idx->d, (int)nprobe,
-                               (int)idx->n_lists, cnt, qoff, qlist, qblk, idx->tile_off, idx->ids, idx->Xr, (int)k, qbound);
-        else if (idx->metric == LIRA_METRIC_L2)
-            hipLaunchKernelGGL((k_seed_b<LIRA_METRIC_L2, 64, 128>), g, dim3(256), 0, st, q, idx->d, (int)nprobe,
-                               (int)idx->n_lists, cnt, qoff, qlist, qblk, idx->tile_off, idx->ids, idx->Xr, (int)k, qbound);
-        else if (o.seed == 3)
-            hipLaunchKernelGGL((k_seed_b<LIRA_METRIC_IP, 64, 256>), g, dim3(256), 0, st, q, idx->d, (int)nprobe,
-                               (int)idx->n_lists, cnt, qoff, qlist, qblk, idx->tile_off, idx->ids, idx->Xr, (int)k, qbound);
-        else
-            hipLaunchKernelGGL((k_seed_b<LIRA_METRIC_IP, 64, 128>), g, dim3(256), 0, st, q, idx->d, (int)nprobe,
-                               (int)idx->n_lists, cnt, qoff, qlist, qblk, idx->tile_off, idx->ids, idx->Xr, (int)k, qbound);
-        LIRA_HIP_TRY(hipGetLastError());
-    }
     if (ev[1]) LIRA_HIP_TRY(hipEventRecord(ev[1], st));
 
     ScreenArgs a;
@@ -3186,10 +2452,10 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     a.qoff = qoff;
     a.qlist = qlist;
     a.QH = QH;
-    a.qpair = pl.pp && !pl.wide ? 1 : 0;
+    a.qpair = pl.pp ? 1 : 0;
     a.partial = partial;
     // the lists' own error bounds (k_screen_m only; the merge otherwise takes the list-wide one)
-    float *pE = pl.mfma && !pl.v2 ? (float *)(w + pl.off_pe) : nullptr;
+    float *pE = pl.mfma ? (float *)(w + pl.off_pe) : nullptr;
     a.pE = pE;
     a.qbound = qbound;
     a.d = idx->d;
@@ -3202,19 +2468,15 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     a.bpc_near = groups == 2 ? pl.bpc_near : pl.bpc;
     a.nch_max = pl.nch_max;
     a.stats = idx->stats_on ? (unsigned long long *)idx->stats : nullptr;
-    hipError_t e = pl.wide == 2 ? launch_vscreen(idx, q, cnt, qoff, qlist, itab, head, QN, QE, (const uint16_t *)QT,
-                                                 partial, pE, qbound,
-                                                 (int)nprobe, (int)k, pl.bpc, a.bpc_near, pl.nch_max, nvirt, tri ? 1 : 0,
-                                                 pl.grid, (int4 *)(w + pl.off_wrec),
-                                                 (int64_t)(pl.max_qblk + 1) * pl.nch_max, st)
-                   : pl.wide ? launch_wscreen(idx, q, cnt, qoff, qlist, itab, head, QN, QE, partial, pE, qbound,
-                                            (int)nprobe, (int)k, pl.bpc, a.bpc_near, pl.nch_max, nvirt, tri ? 1 : 0,
-                                            pl.grid, (int4 *)(w + pl.off_wrec),
-                                            (int64_t)(pl.max_qblk + 1) * pl.nch_max, st)
-                   : idx->metric == LIRA_METRIC_L2 ? launch_screen_rl<LIRA_METRIC_L2>(a, pl, st)
+    hipError_t e = idx->metric == LIRA_METRIC_L2 ? launch_screen_rl<LIRA_METRIC_L2>(a, pl, st)
                                                    : launch_screen_rl<LIRA_METRIC_IP>(a, pl, st);
     if (e != hipSuccess) return fail(LIRA_EHIP, std::string("k_screen launch: ") + hipGetErrorString(e));
     if (ev[2]) LIRA_HIP_TRY(hipEventRecord(ev[2], st));
+    if (a.stats && filter && npairs > 0) {
+        hipLaunchKernelGGL(k_prune_stats, dim3((unsigned)((npairs + 255) / 256)), dim3(256), 0, st, probe, plive,
+                           npairs, (int)idx->n_lists, idx->list_size, a.stats);
+        LIRA_HIP_TRY(hipGetLastError());
+    }
 
     SMergeArgs m;
     m.partial = partial;
@@ -3250,7 +2512,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     m.per_partition = per_part ? 1 : 0;
     m.stats = a.stats;
     m.split = pl.split;
-    m.unsorted = pl.wide == 2 ? 1 : 0;
+    m.unsorted = 0;
     if (idx->metric == LIRA_METRIC_L2)
         launch_smerge<LIRA_METRIC_L2>(Rm, m, st);
     else

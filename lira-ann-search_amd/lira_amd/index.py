@@ -271,8 +271,11 @@ class PartitionedIndex:
         v = (ctypes.c_uint64 * 8)()
         with torch.cuda.device(self.device):
             _lib.call("lira_index_stats_read", self._h, v)
+        # ([1] / [3] mean chunks_nominal / blocks_dropped on the all-exact scan and the
+        # plan filter's removed pairs / their (query, candidate) pairs on the screened one)
         return {"chunks_computed": v[0], "chunks_nominal": v[1], "blocks": v[2], "blocks_dropped": v[3],
-                "blocks_skipped": v[4], "rechecked": v[5], "rescans": v[6], "survivors": v[7]}
+                "blocks_skipped": v[4], "rechecked": v[5], "rescans": v[6], "survivors": v[7],
+                "pairs_pruned_plan": v[1], "candidates_pruned_plan": v[3]}
 
     def set_option(self, name: str, value) -> None:
         """Set one LIRA_OPT_* knob by name (see include/lira_hip.h)."""

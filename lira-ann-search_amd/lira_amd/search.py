@@ -192,9 +192,11 @@ class ProbePipeline:
     @torch.no_grad()
     def run(self, threshold: float | None = None):
         """One pass over self.q (stream-ordered, asynchronous), at `threshold`
-        (default: the pipeline's own)."""
-        if threshold is not None:
+        (default: the pipeline's own).  A new threshold drops a captured graph:
+        the graph holds lira_select_probes' threshold argument of capture time."""
+        if threshold is not None and float(threshold) != self.thr:
             self.thr = float(threshold)
+            self.graph = None
         centroid_dist(self.q, self.C, self.mean, self.scale, out=self.dist)
         self.scores.copy_(self.model(self.dist, self.q))
         self._select_scan()
@@ -233,6 +235,9 @@ class ProbePipeline:
         return self
 
     def replay(self):
+        if self.graph is None:
+            raise RuntimeError("ProbePipeline.replay: no captured graph (capture() first; run() at a new "
+                               "threshold drops the graph, whose selection threshold is fixed at capture)")
         self.graph.replay()
 
 

@@ -197,6 +197,13 @@ def test_probe_pipeline_graph_matches_eager_and_oracle():
     Do, Io, _ = oracle.scan_topk(q, off, ids, x[ids], pr, 10, oracle.L2, 1)
     assert np.array_equal(I0.cpu().numpy(), Io)
     assert np.array_equal(D0.cpu().numpy().view(np.uint32), Do.view(np.uint32))
+    # a run at another threshold drops the graph (its selection threshold is baked in)
+    pipe.run(0.5)
+    assert pipe.graph is not None
+    pipe.run(0.3)
+    assert pipe.graph is None
+    with pytest.raises(RuntimeError, match="no captured graph"):
+        pipe.replay()
 
 
 def test_search_engine_results_do_not_alias():
@@ -247,10 +254,12 @@ def test_order_probes_matches_numpy(mp, nb):
     for i in range(n):
         m = int(rng.integers(0, min(mp, nb) + 1))
         probe[i, :m] = rng.permutation(nb)[:m]
+        if i % 7 == 0 and m < mp:  # an out-of-range id: kept (after the valid ones) for the scan's ERANGE
+            probe[i, m] = nb + i % 5
         rng.shuffle(probe[i])  # -1 slots anywhere
     got = order_probes(torch.from_numpy(probe).cuda(), torch.from_numpy(key).cuda()).cpu().numpy()
     for i in range(n):
-        v = probe[i][probe[i] >= 0]
+        v = probe[i][(probe[i] >= 0) & (probe[i] < nb)]
         kk = key[i, v] + np.float32(0.0)  # (-0 orders as +0)
-        want = v[np.lexsort((v, kk))]
+        want = np.concatenate([v[np.lexsort((v, kk))], np.sort(probe[i][probe[i] >= nb])])
         assert np.array_equal(got[i, :len(want)], want) and (got[i, len(want):] == -1).all()

@@ -86,12 +86,6 @@ def check_vs_oracle(x, q, d2b, probe, b, k, metric, dedup=True):
             assert np.array_equal(I, Io), f"ids differ (xhi={xhi})"
             assert np.array_equal(bits(D), bits(Do)), f"distances differ (xhi={xhi})"
         idx.set_option("xhi", -1)
-        # the wide screen k_screen_w / the wave-resident k_screen_v where they apply
-        for wide in (1, 2):
-            idx.set_option("wide", wide)
-            D, I, nc = run(idx, q, probe, k, dedup=dedup)
-            idx.set_option("wide", 0)
-            assert np.array_equal(I, Io) and np.array_equal(bits(D), bits(Do)), f"differ (wide={wide})"
     if k <= 120:
         # the compact index (no fp32 tiles: row-major + split-bf16 copies only)
         idc = make_index(x, d2b, b, metric, keep_tiles=False)
@@ -378,10 +372,9 @@ def test_options_do_not_change_results(metric):
     x, q, d2b, probe = clustered_case(61, 20000, 48, 8, 700, 3)
     idx = make_index(x, d2b, 8, metric)
     ref = run(idx, q, probe, 10)
-    for name, vals in (("qr", (128,)), ("two_phase", (0, 2)), ("seed", (0, 2, 3)), ("share", (0,)),
+    for name, vals in (("qr", (128,)), ("two_phase", (0, 2)), ("seed", (0,)), ("share", (0,)),
                        ("prune", (0,)), ("split", (0,)), ("mfma", (0, 2)), ("rounds", (1, 64)),
-                       ("near_rounds", (2, 8)), ("screen", (0,)), ("ring", (2, 3, 4)), ("probes_hint", (1, 4)), ("xhi", (0, 1, 2)),
-                       ("wide", (1, 2))):
+                       ("near_rounds", (2, 8)), ("screen", (0,)), ("probes_hint", (1, 4)), ("xhi", (0, 1, 2))):
         old = idx.get_option(name)
         for v in vals:
             idx.set_option(name, v)
@@ -394,27 +387,18 @@ def test_options_do_not_change_results(metric):
         D0, I0, _ = run(idx0, q, probe, k)
         D1, I1, _ = run(idx, q, probe, k)
         assert np.array_equal(I0, I1) and np.array_equal(bits(D0), bits(D1)), ("order", k)
-        idx.set_option("pipeline", 1)  # k_screen_s for k > 56
-        D2, I2, _ = run(idx, q, probe, k)
-        idx.set_option("pipeline", 0)
-        assert np.array_equal(I2, I1) and np.array_equal(bits(D2), bits(D1)), ("pipeline", k)
         idx.set_option("qr", 32)  # 32 queries per item at RL 4 (k > 56, full split)
         D3, I3, _ = run(idx, q, probe, k)
         idx.set_option("qr", 0)
         assert np.array_equal(I3, I1) and np.array_equal(bits(D3), bits(D1)), ("qr32", k)
-    # the pipelined screen k_screen_s (LIRA_OPT_PIPELINE = 1 with a ring size):
-    # every RL 1 ring / query-block instantiation at k = 10, RL 2 at k = 40
-    idx.set_option("pipeline", 1)
-    for kk, qr, ring in ((10, 64, 2), (10, 64, 4), (10, 128, 3), (10, 128, 4), (40, 0, 4)):
-        idx.set_option("qr", qr)
-        idx.set_option("ring", ring)
-        want = ref if kk == 10 else run(make_index(x, d2b, 8, metric), q, probe, kk)
-        D, I, nc = run(idx, q, probe, kk)
-        assert "k_screen_s" in idx.describe(q.shape[0], probe.shape[1], kk), (qr, ring)
-        assert np.array_equal(I, want[1]) and np.array_equal(bits(D), bits(want[0])), (kk, qr, ring)
-    idx.set_option("pipeline", 0)
-    idx.set_option("qr", 0)
-    idx.set_option("ring", 0)
+    # the removed screen variants (k_screen_s / _w / _v, k_seed_b): 0 still reads back, others refused
+    from lira_amd import LiraError
+    for name, bad in (("pipeline", 1), ("ring", 3), ("wide", 1), ("seed", 2)):
+        with pytest.raises(LiraError, match="EUNSUPPORTED"):
+            idx.set_option(name, bad)
+    for name in ("pipeline", "ring", "wide"):
+        idx.set_option(name, 0)
+        assert idx.get_option(name) == 0
 
 
 @pytest.mark.parametrize("metric", ["L2", "inner_product"])
