@@ -42,6 +42,7 @@ import torch  # noqa: E402
 # peaks (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0          # HBM3E spec
 L2LDS_PEAK_GBS = 18800.0       # LDS-DMA gather into LDS from the XCD L2, chip-wide (upper end, measured)
+L2_PEAK_GBS = 34500.0          # L2 read bandwidth, chip-wide (MI355X_MICROARCH.md, L2 per XCD)
 MFMA_F32_PEAK_TFLOPS = 157.3   # v_mfma_f32_*_f32 dense = fp32 vector peak
 MFMA_BF16_PEAK_TFLOPS = 2516.6  # dense bf16 MFMA, 16 x the f32 rate
 VALU_F32_PEAK_TOPS = 78.64     # non-FMA fp32 lane ops/s (157.3 TFLOP/s counts an FMA as 2)
@@ -277,7 +278,7 @@ def time_batch(args, index, q, centres, nprobe, k, world, dist, gdev, nq_total, 
 
 def run_workload(args, data, rank, world, gpu, dev, dist, primary):
     """Build one config on one distribution, time the step, measure everything."""
-    from lira_amd import PartitionedIndex, centroid_gemm, rank_nearest
+    from lira_amd import PartitionedIndex, RankWorkspace, centroid_gemm, rank_nearest
     from lira_amd.distributed import shard_bounds
     from lira_amd.synthetic import CONFIGS, LATENT_DIM, N_MUL, workload
 
@@ -365,6 +366,7 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
     if args.sweep and world == 1:
         out["sweep"] = sweep_options(args, index, local_step, D, I, nq, nprobe, k)
 
+    ws = RankWorkspace(max(1, nq), B, dev)
     out["kernels_ms_per_step"]["rank_nearest"] = event_ms(
         lambda: rank_nearest(q, centres, nprobe, out=probe, workspace=ws))
 
@@ -376,7 +378,7 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
     split = "split-bf16" in kernel or hh
     hix = "hi-x" in kernel  # hi-only x: 2 products per dim (qh, ql) x xh, half the X bytes
     kname = kernel.split()[0]
-    if kname == "k_screen_m":
+    if kname in ("k_screen_m", "k_screen_r"):
         # (row, cand) pairs x dpad x products x 2
         flops = work["chunks_computed"] * dpad * (2 if hh else 4 if hix else 8 if split else 2)
         mfma_peak = MFMA_BF16_PEAK_TFLOPS if split else MFMA_F32_PEAK_TFLOPS
@@ -384,10 +386,17 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
     else:
         flops = work["chunks_computed"] * dpad * 2
         mfma_peak, mfma_what = MFMA_F32_PEAK_TFLOPS, "fp32 VALU (v_pk_fma_f32)"
-    # L2 -> LDS bytes (LDS-DMA) per launch: X (256 candidates), Q (qr rows), xadj
-    staged = work["blocks"] * (256 * dpad * (2 if hix else 4) + qr * dpad * (2 if hh else 4) + 1024)
-    st_name, st_peak = "l2_lds", L2LDS_PEAK_GBS
-    st_what = "bytes staged L2/MALL -> LDS by LDS-DMA (tiles + query chunk + xadj per computed block)"
+    if kname == "k_screen_r":
+        # L2 -> VGPR bytes per launch: per computed tile (64 candidates) their hi parts + xadj
+        # (the work counter "blocks" counts tiles for this kernel)
+        staged = work["blocks"] * (64 * dpad * 2 + 256)
+        st_name, st_peak = "l2_vgpr", L2_PEAK_GBS
+        st_what = "bytes loaded L2/MALL -> VGPRs (x hi parts + xadj per computed tile; queries from LDS)"
+    else:
+        # L2 -> LDS bytes (LDS-DMA) per launch: X (256 candidates), Q (qr rows), xadj
+        staged = work["blocks"] * (256 * dpad * (2 if hix else 4) + qr * dpad * (2 if hh else 4) + 1024)
+        st_name, st_peak = "l2_lds", L2LDS_PEAK_GBS
+        st_what = "bytes staged L2/MALL -> LDS by LDS-DMA (tiles + query chunk + xadj per computed block)"
     traffic, pmc_src = None, None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_scan_{args.config}_{data}.json")
     if os.path.exists(pmc_path):
@@ -427,6 +436,8 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
                  "pairs_pruned_plan": work["pairs_pruned_plan"],
                  "candidates_pruned_plan": work["candidates_pruned_plan"],
                  "blocks_pruned_plan": work["candidates_pruned_plan"] / (qr * 256.0),
+                 "blocks_unit": "tiles of 64 candidates x 64 rows" if kname == "k_screen_r"
+                 else "blocks of 256 candidates x qr rows",
                  "blocks_pruned_plan_note": "(query, candidate) pairs the plan's partition filter removed, in "
                                             "units of one screen block (qr query rows x 256 candidates); "
                                             "blocks_skipped = blocks the in-kernel triangle test skipped",

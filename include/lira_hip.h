@@ -165,6 +165,10 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *                        each list's rows by ascending distance to the list's pivot, so tile radius
  *                        ranges are narrow and the triangle-inequality skip drops more; 0: list order.
  *                        Results never depend on it.
+ *   LIRA_OPT_RSCREEN     1 (default): the wave-streaming screen k_screen_r where it applies (L2 on the
+ *                        centred split copy with the hi x hi screen, k <= 24, dpad <= 128, the
+ *                        per-query seed on, not PER_PARTITION): query rows' hi parts in LDS, each
+ *                        wave streaming its own candidate tiles into registers; 0: k_screen_m
  */
 #define LIRA_OPT_KEEP_TILES 1
 #define LIRA_OPT_SCREEN 2
@@ -184,6 +188,7 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
 #define LIRA_OPT_XHI 16
 #define LIRA_OPT_ORDER 17
 #define LIRA_OPT_WIDE 18
+#define LIRA_OPT_RSCREEN 19
 int lira_index_set_option(lira_index *idx, int option, int64_t value);
 int lira_index_get_option(const lira_index *idx, int option, int64_t *value);
 /* 1 if the index holds the fp32 tile copy (LIRA_OPT_KEEP_TILES at build time) */

@@ -758,6 +758,7 @@ int lira_index_set_option(lira_index *idx, int option, int64_t value) {
         case LIRA_OPT_PROBES_HINT: if (!in(0, 1 << 20)) break; o.probes_hint = v; return LIRA_OK;
         case LIRA_OPT_XHI: if (!in(-1, 2)) break; o.xhi = v; return LIRA_OK;
         case LIRA_OPT_ORDER: if (!in(0, 1)) break; o.order = v; return LIRA_OK;
+        case LIRA_OPT_RSCREEN: if (!in(0, 1)) break; o.rscreen = v; return LIRA_OK;
         default: return fail(LIRA_EINVAL, "unknown option " + std::to_string(option));
     }
     return fail(LIRA_EINVAL, "value " + std::to_string(value) + " out of range for option " + std::to_string(option));
@@ -785,6 +786,7 @@ int lira_index_get_option(const lira_index *idx, int option, int64_t *value) {
         case LIRA_OPT_PROBES_HINT: *value = o.probes_hint; break;
         case LIRA_OPT_XHI: *value = o.xhi; break;
         case LIRA_OPT_ORDER: *value = o.order; break;
+        case LIRA_OPT_RSCREEN: *value = o.rscreen; break;
         default: return fail(LIRA_EINVAL, "unknown option " + std::to_string(option));
     }
     return LIRA_OK;

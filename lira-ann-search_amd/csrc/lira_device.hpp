@@ -309,6 +309,63 @@ __device__ __forceinline__ int mbcnt64(u64 m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
 }
 
+// ---- shared by the screening kernels (k_screen_m, k_screen_r) ----
+// XCD-aware work queues (k_plan): claim the next item of this workgroup's own
+// XCD's queue, stealing from the others (in order) once it is empty; -1 when
+// every queue is.  Thread 0 only; xq[9] (LDS) = the queue starts + end, x /
+// tries the claimant's state.
+__device__ __forceinline__ int xcd_id() {
+    unsigned v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+    return (int)(v & 7u);
+}
+// Once the claimant's queue is empty it reads all 8 claim counters at once (one
+// round trip) and steals from the first queue that still has items: walking
+// the queues with one atomic each in turn cost every workgroup up to 8
+// serial atomic round trips at the end of the scan.  tries = 8: all empty.
+__device__ __forceinline__ int claim_item(int32_t *head, const int *xq, int &x, int &tries) {
+    if (tries >= 8) return -1;
+    {
+        const int i = xq[x] + atomicAdd(&head[2 + x], 1);
+        if (i < xq[x + 1]) return i;
+    }
+    for (;;) {
+        int c[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) c[r] = __hip_atomic_load(&head[2 + r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int pick = -1;
+#pragma unroll
+        for (int s = 1; s <= 8; ++s) {
+            const int r = (x + s) & 7;
+            if (pick < 0 && xq[r] + c[r] < xq[r + 1]) pick = r;
+        }
+        if (pick < 0) {
+            tries = 8;
+            return -1;
+        }
+        x = pick;
+        const int i = xq[x] + atomicAdd(&head[2 + x], 1);
+        if (i < xq[x + 1]) return i;
+    }
+}
+
+// Inclusive prefix sum within each 16-lane group (= DPP row): 4 row_shr
+// steps with zero fill, no LDS round trips (a __shfl_up chain was 4
+// dependent ds_bpermutes per selection pass)
+__device__ __forceinline__ int row16_incl_scan(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);  // row_shr:8
+    return v;
+}
+// lane 15 of each 16-lane group, broadcast to the group (the group's total)
+__device__ __forceinline__ int row16_total(int inc) {
+    const int t0 = __builtin_amdgcn_readlane(inc, 15), t1 = __builtin_amdgcn_readlane(inc, 31);
+    const int t2 = __builtin_amdgcn_readlane(inc, 47), t3 = __builtin_amdgcn_readlane(inc, 63);
+    const int g = (int)(threadIdx.x & 63) >> 4;
+    return g == 0 ? t0 : g == 1 ? t1 : g == 2 ? t2 : t3;
+}
 // ---- per-query merge helpers (k_merge, k_smerge) ----
 __device__ __forceinline__ void emit_key(u64 key, int metric, float *D, int64_t *I) {
     if (key == kEmptyKey) {

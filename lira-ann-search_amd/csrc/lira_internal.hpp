@@ -51,6 +51,7 @@ struct lira_opts {
     int probes_hint = 0;
     int xhi = -1;
     int order = 1;
+    int rscreen = 1;
 };
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device):

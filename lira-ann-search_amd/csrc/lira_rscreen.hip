@@ -1,0 +1,578 @@
+// lira_rscreen.hip -- k_screen_r, the wave-streaming screen (gfx950): the
+// default screen of lira_scan_topk for L2, k <= 24, dpad <= 128.  Replaces
+// search.cpp:468-493 (the per-query loop over the candidates of the probed
+// buckets) with results identical to the all-exact scan: it screens every
+// (query, candidate) pair with a rigorous bound and leaves the exact re-check
+// and the top-k to k_smerge (lira_screen.hip), exactly as k_screen_m does.
+// The error model is k_screen_m<..., 3>'s (hi x hi, lira_bounds.hpp err_E,
+// split = 3), evaluated in fp32 with explicit outward rounding.
+//
+// Why a second screen.  k_screen_m stages each candidate block through LDS
+// once for its 64 query rows: per 32 dims of a 256-candidate block every wave
+// issues 5 LDS-DMA pieces and 17 fragment reads and meets the other three
+// waves at a barrier, so the slowest wave's selection gates the next chunk
+// (0.18 of HBM peak, MFMA busy 5-11 %, 46-55 % of wave
+// cycles parked).  Here:
+//   * the item's 64 query rows' hi parts live in registers for the whole item
+//     (A operands: dpad / 32 x 4 row groups x 8 bf16 per lane, 64 VGPRs at
+//     d = 128), loaded once per item from the per-pair records (k_seed_t);
+//   * each wave streams its OWN candidate tiles (64 rows each; tiles u, u + 4,
+//     ... of the item): B fragments straight from HBM/L2 into registers, one
+//     16-B load per lane feeding 4 MFMAs, the next tile's loads issued under
+//     the current tile's MFMAs -- no LDS staging of candidates, no DMA issue,
+//     no barrier inside an item;
+//   * the four waves share the item's 64 row lists (LDS, sorted, 32 keys);
+//     each wave appends survivors to its own per-row buffers (16 keys) and
+//     merges a full buffer into the shared list under a per-row LDS lock;
+//     thresholds are refreshed per tile from the shared lists, the per-row
+//     running error bound and the query's published bound.
+// Per tile and wave: 4 x dpad/32 x 4 v_mfma_f32_16x16x32_bf16 (64 at d = 128:
+// 64 rows x 64 candidates), 4 dpad/32 + 1 loads, ~100 VALU of selection.
+//
+// MFMA layout (cdna_hip_programming.md, 16x16x32 bf16): A = 16 query rows x
+// 32 dims (lane l: row l & 15, dims 8 (l >> 4) ..), B = 32 dims x 16
+// candidates (lane l: candidate slot l & 15 of group i, the same dims), read
+// from Xb's hi quarters: 16-dim chunk 2c + (g >> 1), part g & 1, slot 16 i +
+// (l & 15) = storage row 4 (l & 15) + i of the tile.  D: lane (g, j) holds
+// rows 4 g + reg of the row group, candidate 4 j + i.
+#include <atomic>
+
+#include "lira_bounds.hpp"
+#include "lira_internal.hpp"
+#include "lira_rscreen.hpp"
+
+namespace lira {
+
+typedef __bf16 rbf16x8 __attribute__((ext_vector_type(8)));
+typedef float rf4 __attribute__((ext_vector_type(4)));
+
+static constexpr int kRQ = 64;          // query rows per item
+static constexpr int kRW = 4;           // waves per workgroup
+static constexpr int kRK2 = 32;         // row list keys (k <= 24)
+static constexpr int kRBC = 16;         // survivor buffer keys per (wave, row)
+static constexpr int kRMaxTiles = 512;  // tiles per item (the plan caps a chunk at 128 blocks)
+static constexpr int kROCap = 128;      // overflow queue entries per wave (per tile's selection)
+
+struct RSmem {
+    static constexpr int aq = 0;                                    // [4 chunks][4 row groups][64 lanes] 16 B: A operands
+    static constexpr int lists = aq + 4 * 4 * 64 * 16;              // [64][32] u64
+    static constexpr int bufs = lists + kRQ * kRK2 * 8;              // [4][64][16] u64
+    static constexpr int bufc = bufs + kRW * kRQ * kRBC * 8;         // [4][64] int
+    static constexpr int hs = bufc + kRW * kRQ * 4;                  // [4][64] float: the wave's thresholds
+    static constexpr int tst = hs + kRW * kRQ * 4;                   // [512] float2: tile radius ranges
+    static constexpr int trs = tst + kRMaxTiles * 8;                 // [512] float: tile hi residuals
+    static constexpr int pair = trs + kRMaxTiles * 4;                // [64] int
+    static constexpr int qn = pair + kRQ * 4;                        // [64] float4: qn, ||q'|| (up), qres, ||q - c||
+    static constexpr int erun = qn + kRQ * 16;                       // [64] float bits: running error bound
+    static constexpr int lock = erun + kRQ * 4;                      // [64] int
+    static constexpr int opub = lock + kRQ * 4;                      // [64] uint: bound last published
+    static constexpr int resc = opub + kRQ * 4;                      // [64] int: row needs k_smerge's rescan
+    static constexpr int oqk = resc + kRQ * 4;                       // [4][kROCap] u64: overflow queue keys
+    static constexpr int oqr = oqk + kRW * kROCap * 8;               // [4][kROCap] u8: their rows
+    static constexpr int meta = oqr + kRW * kROCap;                  // [16] int
+    static constexpr int total = meta + 64;
+};
+static_assert(RSmem::total <= 80 * 1024, "k_screen_r: two workgroups per CU");
+
+// a value the compiler must treat as produced here (keeps per-lane address
+// arithmetic from being hoisted out of the loops: hipcc otherwise precomputed
+// ~80 VGPRs of row addresses for the 16 selection entries)
+__device__ __forceinline__ int opaque(int x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
+// outward rounding by a margin covering a handful of fp32 roundings
+__device__ __forceinline__ float rup(float x) { return __builtin_fmaf(__builtin_fabsf(x), 0x1p-20f, x) + 0x1p-125f; }
+__device__ __forceinline__ float rdn(float x) { return __builtin_fmaf(-__builtin_fabsf(x), 0x1p-20f, x) - 0x1p-125f; }
+
+// err_E<L2>(qnorm, Rb, d, split = 3, dpad, centred = 1, hres, qres) in fp32:
+// every term is >= 0, so the ~16 roundings stay below 2^-20 relative and the
+// final factor covers them; + 2^-125 >= d 2^-140 (lira_bounds.hpp)
+__device__ __forceinline__ float errE_r(float qnorm, float Rb, float hres, float qres, float dp) {
+    const float ex = hres >= 0.0f ? hres * 1.0001f : 0x1p-8f * 1.02f * Rb;
+    const float ed = ex * qnorm + qres * (Rb + ex) * 1.0001f + 2.0f * dp * 0x1p-22f * 1.02f * qnorm * (Rb + ex) +
+                     2.0f * dp * 0x1p-96f * (qnorm + Rb + ex + 1.0f);
+    const float s = qnorm + Rb;
+    return (2.0f * ed + (1.05f * 8.0f + 2.01f + 2.0f) * 0x1p-24f * s * s) * (1.0f + 0x1p-18f) + 0x1p-125f;
+}
+
+// L2 screened score of a candidate from wv = fl(dot - xadj): s~ = fl(qn - 2 wv)
+// (k_screen_m: fma(-2, dot, fl(qn + 2 xadj)); this form's extra rounding is in
+// errE_r's 2 u s^2)
+__device__ __forceinline__ u64 rkey(float wv, float qn, uint32_t pos) {
+    const float s = qn - 2.0f * wv;
+    return ((u64)f2ord(s) << 32) | pos;
+}
+
+// Merge this wave's buffer of `row` (n keys) into the shared list, under the
+// row's LDS lock: raise the row's running error bound to the wave's first
+// (readers take the list's k-th key, then the bound: program order in both),
+// half-wave merge, publish the query's bound if the list's k-th improved.
+__device__ __forceinline__ void flush_row(u64 *lists, const u64 *mybuf, int *lock_s, uint32_t *erun_s,
+                                       uint32_t *opub_s, const int *pair_s, int row, int n, int ew_bits, int k,
+                                       uint32_t *qbound, int nprobe, float gP) {
+    const int lane = lane_id(), hl = lane & 31;
+    if (lane == 0) {
+        while (atomicCAS(lock_s + row, 0, 1) != 0) __builtin_amdgcn_s_sleep(1);
+        atomicMax(erun_s + row, (uint32_t)ew_bits);
+    }
+    asm volatile("" ::: "memory");
+    u64 lst[1] = {lists[row * kRK2 + hl]};
+    const u64 b = hl < n ? mybuf[row * kRBC + hl] : kEmptyKey;
+    half_merge_batch1<1>(lst, b);
+    if (lane < 32) lists[row * kRK2 + hl] = lst[0];
+    if (lane == k - 1 && lst[0] != kEmptyKey && qbound) {
+        const int pr = pair_s[row];
+        if (pr >= 0) {
+            const float er = __uint_as_float(erun_s[row]);
+            const uint32_t P = f2ord(rup(rup(key_score(lst[0]) + er) * gP) + 0x1p-125f);
+            if (P < opub_s[row]) {
+                opub_s[row] = P;
+                atomicMin(qbound + pr / nprobe, P);
+            }
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (LDS in order: the list is written before the unlock)
+    if (lane == 0) *(volatile int *)(lock_s + row) = 0;
+    __builtin_amdgcn_wave_barrier();
+}
+
+// After a tile's selection (the accumulators dead): merge this wave's full row
+// buffers into the lists, then move the overflow queue into the buffers (LDS
+// atomic slots), merging every buffer that fills, until the queue is empty.
+__device__ __forceinline__ void drain_buffers(u64 *lists, u64 *mybuf, int *mybufc, int *lock_s, uint32_t *erun_s,
+                                           uint32_t *opub_s, const int *pair_s, const u64 *oq_key,
+                                           const uint8_t *oq_row, int nq, float Ew, int k, uint32_t *qbound,
+                                           int nprobe, float gP) {
+    const int lane = lane_id();
+    auto flush_full = [&]() {
+        u64 full = __ballot(mybufc[lane] >= kRBC);  // lane = row
+        while (full) {
+            const int row = __builtin_ctzll(full);
+            full &= full - 1;
+            flush_row(lists, mybuf, lock_s, erun_s, opub_s, pair_s, row, kRBC,
+                      __builtin_amdgcn_readlane(__float_as_int(Ew), row), k, qbound, nprobe, gP);
+            if (lane == 0) mybufc[row] = 0;
+            __builtin_amdgcn_wave_barrier();
+        }
+    };
+    flush_full();
+    for (int e0 = 0; e0 < nq; e0 += 64) {
+        const int e = e0 + lane;
+        bool pend = e < nq;
+        const int row = pend ? oq_row[e] : 0;
+        const u64 key = pend ? oq_key[e] : kEmptyKey;
+        while (__any(pend)) {
+            if (pend) {
+                const int slot = atomicAdd(mybufc + row, 1);
+                if (slot < kRBC) {
+                    mybuf[row * kRBC + slot] = key;
+                    pend = false;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            // rows the round filled (a lane that overflowed left its row's count above kRBC)
+            if (lane < kRQ && mybufc[lane] > kRBC) mybufc[lane] = kRBC;
+            __builtin_amdgcn_wave_barrier();
+            flush_full();
+        }
+    }
+}
+
+template <int NC>  // 32-dim chunks: dpad = 32 NC
+__global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    u64 *lists = (u64 *)(smem + RSmem::lists);
+    u64 *bufs = (u64 *)(smem + RSmem::bufs);
+    int *bufc = (int *)(smem + RSmem::bufc);
+    float *hs = (float *)(smem + RSmem::hs);
+    float2 *tst = (float2 *)(smem + RSmem::tst);
+    float *trs = (float *)(smem + RSmem::trs);
+    int *pair_s = (int *)(smem + RSmem::pair);
+    float4 *rec_s = (float4 *)(smem + RSmem::qn);
+    const uint4 *aq_s = (const uint4 *)(smem + RSmem::aq);
+    uint32_t *erun_s = (uint32_t *)(smem + RSmem::erun);
+    int *lock_s = (int *)(smem + RSmem::lock);
+    uint32_t *opub_s = (uint32_t *)(smem + RSmem::opub);
+    int *rescan_s = (int *)(smem + RSmem::resc);
+    int *meta = (int *)(smem + RSmem::meta);
+    __shared__ int xq[9];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, cj = lane & 15;
+    const int k = a.k;
+    const float dp = (float)a.dpad;
+    u64 *mybuf = bufs + wave * kRQ * kRBC;
+    int *mybufc = bufc + wave * kRQ;
+    float *myh = hs + wave * kRQ;
+    u64 *oq_key = (u64 *)(smem + RSmem::oqk) + wave * kROCap;
+    uint8_t *oq_row = (uint8_t *)(smem + RSmem::oqr) + wave * kROCap;
+    int ovf = 0;  // overflow queue fill (wave-uniform)
+    const bool TRI = a.tstat != nullptr;
+    // B fragment: the lane's byte offset inside a tile's 32-dim chunk
+    const uint32_t lane_off = (uint32_t)((g >> 1) * 4096 + (g & 1) * 1024 + cj * 16);
+    const int64_t tile_bytes = a.dpad * 64 * 4;
+    unsigned long long n_tiles = 0, n_skip = 0, n_surv = 0;
+
+    const int bpc_near_d = __builtin_amdgcn_readfirstlane(a.head[19]);
+    int qx = 0, qtries = 0, nxt = -1;
+    int4 e_nxt = make_int4(0, 0, 0, 0);
+    if (tid == 0) {
+        for (int r = 0; r < 9; ++r) xq[r] = a.head[10 + r];
+        qx = xcd_id();
+        nxt = claim_item(a.head, xq, qx, qtries);
+        if (nxt >= 0) e_nxt = a.itab[nxt];
+    }
+    for (;;) {
+        if (tid == 0) {  // the next item claimed, and its entry loaded, one item ahead
+            const int item = nxt, ok = item >= 0;
+            int4 e = make_int4(0, 0, 0, 0);
+            if (ok) {
+                e = e_nxt;
+                nxt = claim_item(a.head, xq, qx, qtries);
+                if (nxt >= 0) e_nxt = a.itab[nxt];
+            }
+            meta[0] = ok;
+            meta[1] = e.x;
+            meta[2] = e.y;
+            meta[3] = e.z;
+        }
+        __syncthreads();
+        if (!meta[0]) break;
+        const int vp = __builtin_amdgcn_readfirstlane(meta[1]);
+        const int qb = __builtin_amdgcn_readfirstlane(meta[2]);
+        const int ch = __builtin_amdgcn_readfirstlane(meta[3]);
+        const int p = vp >= a.n_lists ? vp - a.n_lists : vp;
+        const int tile0 = __builtin_amdgcn_readfirstlane(a.tile_off[p]);
+        const int ntl = __builtin_amdgcn_readfirstlane(a.tile_off[p + 1]) - tile0;
+        const int bpc = vp < a.n_lists && a.n_virt > a.n_lists ? bpc_near_d : a.bpc;
+        const int tb_begin = ch * bpc * 4;
+        const int nt = min(ntl, tb_begin + bpc * 4) - tb_begin;  // the item's tiles (<= kRMaxTiles)
+        const int tbase = tile0 + tb_begin;
+        const float R = a.rmax[p];
+
+        // ---- item prologue: row records, lists, tile statistics
+        const int nval = a.cnt[vp] - qb * kRQ;
+        const int my_pair = lane < nval ? a.qlist[a.qoff[vp] + qb * kRQ + lane] : -1;  // lane = row
+        const float4 qrec = my_pair >= 0 ? a.QN[my_pair] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const float my_qres = my_pair >= 0 ? a.QE[my_pair] : 0.0f;
+        const int my_q = my_pair >= 0 ? my_pair / a.nprobe : -1;
+        if (wave == 0) {
+            pair_s[lane] = my_pair;
+            rec_s[lane] = make_float4(qrec.x, qrec.y, my_qres, qrec.w);
+            erun_s[lane] = 0u;
+            lock_s[lane] = 0;
+            opub_s[lane] = ~0u;
+            rescan_s[lane] = 0;
+        }
+        mybufc[lane] = 0;
+        {
+            uint4 *l4 = (uint4 *)lists;
+            const uint4 e4 = make_uint4(~0u, ~0u, ~0u, ~0u);
+            for (int i = tid; i < kRQ * kRK2 / 2; i += 256) l4[i] = e4;
+        }
+        if (TRI)
+            for (int i = tid; i < nt; i += 256) {
+                tst[i] = a.tstat[tbase + i];
+                trs[i] = a.tres ? a.tres[tbase + i] : -1.0f;
+            }
+        __syncthreads();
+
+        // A operands into LDS, in fragment order: [chunk c][row group rg][lane (g, j)]
+        // = row 16 rg + j, dims 32 c + 8 g .. + 7 (each wave reads 1 KiB per (c, rg))
+        for (int e = tid; e < NC * 4 * 64; e += 256) {
+            const int l = e & 63, rg = (e >> 6) & 3, c = e >> 8;
+            const int pr = pair_s[16 * rg + (l & 15)];
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (pr >= 0) v = *(const uint4 *)(a.QH + (int64_t)pr * a.dpad + 32 * c + 8 * (l >> 4));
+            ((uint4 *)(smem + RSmem::aq))[e] = v;
+        }
+        __syncthreads();
+
+        // ---- per-row bound state (lane = row)
+        uint32_t pub = a.qbound && my_q >= 0 ? __hip_atomic_load(a.qbound + my_q, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT) : ~0u;
+        float Tc = -1.0f, Ac = __builtin_inff(), triA = -__builtin_inff(), triB = __builtin_inff();
+        float Ew = 0.0f;  // the largest error bound of the tiles this wave screened (lane = row)
+        // T: the row's bound on its final k-th exact score (shared list, published bound)
+        auto update_T = [&]() {
+            const u64 kk = lists[lane * kRK2 + k - 1];
+            asm volatile("" ::: "memory");  // (the list's key first, then its bound: see flush_row)
+            const float er = __uint_as_float(erun_s[lane]);
+            float T = __builtin_inff();
+            if (kk != kEmptyKey) T = rup(rup(key_score(kk) + er) * a.gP) + 0x1p-125f;
+            if (pub != ~0u) T = fminf(T, ord2f(pub));
+            if (a.qbound && my_q >= 0)
+                pub = __hip_atomic_load(a.qbound + my_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (T != Tc) {
+                Tc = T;
+                Ac = T < 3e38f ? rup(rup(fmaxf(T, 0.0f) + 0x1p-125f) * a.invF) : __builtin_inff();
+                if (my_pair < 0) {
+                    triA = __builtin_inff();
+                    triB = -__builtin_inff();
+                } else if (T < 3e38f) {
+                    const float rad = rup(__builtin_sqrtf(Ac)), dq = rec_s[lane].w;
+                    triA = rdn(rdn(dq) - rad);
+                    triB = rup(rup(dq) + rad);
+                } else {
+                    triA = -__builtin_inff();
+                    triB = __builtin_inff();
+                }
+            }
+        };
+        // tile u is needed by no row (wave-uniform)
+        auto skip = [&](int u) {
+            if (!TRI) return false;
+            const float2 r = tst[u];
+            return __all(r.y < triA || r.x > triB) != 0;
+        };
+
+        int u = wave;
+        update_T();
+        while (u < nt && skip(u)) {
+            ++n_skip;
+            u += kRW;
+        }
+        // B operands: a ring of RS chunks of [candidate group]; chunk s (of the
+        // wave's chunk sequence: tile after tile) sits in slot s mod RS, and its
+        // slot is reloaded with chunk s + RS as soon as its MFMAs have issued
+        // (RS = NC: the next tile's chunk; RS = 2 at d = 128: two chunks ahead,
+        // 32 VGPRs instead of 64)
+        constexpr int RS = NC % 2 == 0 && NC >= 4 ? 2 : NC;
+        rbf16x8 B[RS][4];
+        if (u < nt) {
+            const char *base = a.Xb + (int64_t)(tbase + u) * tile_bytes + lane_off;
+#pragma unroll
+            for (int c = 0; c < RS; ++c)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) B[c][i] = *(const rbf16x8 *)(base + c * 8192 + i * 256);
+        }
+
+        while (u < nt) {
+            // the tile's xadj (in flight under the thresholds and the MFMAs)
+            const rf4 xa = *(const rf4 *)(a.xadj + (int64_t)(tbase + u) * 64 + 4 * cj);
+            // ---- thresholds for tile u (lane = row), then each lane's 16 rows
+            update_T();
+            {
+                float h = __builtin_inff();
+                if (my_pair >= 0) {
+                    const float4 rr = rec_s[lane];
+                    const float my_qn = rr.x, my_qnorm = rr.y, my_qres = rr.z;
+                    const float2 r = TRI ? tst[u] : make_float2(0.0f, R);
+                    const float Rb = TRI ? fminf(R, rup(r.y)) : R;
+                    const float Eb = errE_r(my_qnorm, Rb, TRI ? trs[u] : -1.0f, my_qres, dp);
+                    Ew = fmaxf(Ew, Eb);
+                    h = -__builtin_inff();
+                    if (Ac < 3e38f) {
+                        const float lim = rup(Ac + Eb), s = my_qnorm + Rb;
+                        h = rdn(0.5f * (my_qn - lim) - (__builtin_fabsf(my_qn) + __builtin_fabsf(lim)) * 0x1p-22f -
+                                1.06f * 0x1p-24f * s * s);
+                    }
+                    h = fmaxf(h, -3.40282347e38f);  // (padding, xadj = +inf, never passes)
+                }
+                myh[lane] = h;
+            }
+            __builtin_amdgcn_wave_barrier();
+
+            // ---- the next tile of this wave (skip test with the current intervals)
+            int un = u + kRW;
+            while (un < nt && skip(un)) {
+                ++n_skip;
+                un += kRW;
+            }
+            const int ul = un < nt ? un : u;  // (the last tile's loads repeat the current tile)
+            const char *cbase = a.Xb + (int64_t)(tbase + u) * tile_bytes + lane_off;
+            const char *nbase = a.Xb + (int64_t)(tbase + ul) * tile_bytes + lane_off;
+
+            // ---- 64 rows x 64 candidates; each B fragment's slot reloaded after its 4 MFMAs
+            rf4 acc[4][4];
+#pragma unroll
+            for (int rg = 0; rg < 4; ++rg)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[rg][i] = (rf4)(0.0f);
+            // per chunk: the next chunk's A fragments (LDS), this chunk's 16 MFMAs, the
+            // slot's reloads; a scheduling barrier per chunk keeps the reloads where
+            // they are (left alone, hipcc sank them next to their consumers)
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const int sl = c % RS, cn = c + RS;  // slot; the chunk that goes into it next
+                rbf16x8 Acur[4];
+#pragma unroll
+                for (int rg = 0; rg < 4; ++rg) Acur[rg] = __builtin_bit_cast(rbf16x8, aq_s[(c * 4 + rg) * 64 + lane]);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+#pragma unroll
+                    for (int rg = 0; rg < 4; ++rg)
+                        acc[rg][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Acur[rg], B[sl][i], acc[rg][i], 0, 0, 0);
+                    B[sl][i] = cn < NC ? *(const rbf16x8 *)(cbase + cn * 8192 + i * 256)
+                                       : *(const rbf16x8 *)(nbase + (cn - NC) * 8192 + i * 256);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            ++n_tiles;
+            // wv = fl(dot - xadj) in place (the test's operand; the key's score is
+            // fl(qn - 2 wv), errE_r's 2 u s^2 allowance)
+#pragma unroll
+            for (int rg = 0; rg < 4; ++rg)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[rg][i] = acc[rg][i] - xa[i];
+
+            // ---- selection: pass iff fl(dot - xadj) >= h (k_screen_m's test).  Per
+            // (row group, register) entry the four rows 16 rg + 4 g + reg (one per lane
+            // group): one max over the lane's 4 candidates and one compare per row;
+            // passing keys go to this wave's row buffers (ranks from a 16-lane prefix
+            // sum), keys past a full buffer to the overflow queue; both are drained
+            // below, once the accumulators are dead
+            const int g4 = opaque(4 * g);  // (row = 16 rg + g4 + reg)
+            const uint32_t pos0 = (uint32_t)((tbase + u) * 64) + (uint32_t)opaque(4 * cj);
+            bool drain = false;
+#pragma unroll
+            for (int rg = 0; rg < 4; ++rg) {
+                __builtin_amdgcn_sched_barrier(0);
+                const rf4 hv = *(const rf4 *)(myh + 16 * rg + g4);  // rows 16 rg + 4 g + reg
+#pragma unroll
+                for (int reg = 0; reg < 4; ++reg) {
+                    const float hp = hv[reg];
+                    const float m = fmaxf(fmaxf(fmaxf(acc[rg][0][reg], acc[rg][1][reg]), acc[rg][2][reg]), acc[rg][3][reg]);
+                    if (!__any(m >= hp)) continue;
+#ifdef RS_NOSLOW
+                    drain = true; continue;
+#endif
+                    int pm = 0;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) pm |= (acc[rg][i][reg] >= hp) << i;
+                    const int row = 16 * rg + g4 + reg;  // this lane group's row
+                    const int n_l = __builtin_popcount(pm);
+                    const int inc = row16_incl_scan(n_l);
+                    const int tot = row16_total(inc);
+                    const int bc = mybufc[row];
+                    const float qn_r = rec_s[row].x;
+                    int rank = bc + inc - n_l;  // buffer rank of my first key
+                    n_surv += (unsigned long long)n_l;
+                    bool over = false;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        if ((pm >> i) & 1) {
+                            if (rank < kRBC) mybuf[row * kRBC + rank] = rkey(acc[rg][i][reg], qn_r, pos0 + i);
+                            over = over || rank >= kRBC;
+                            ++rank;
+                        }
+                    }
+                    if (__any(over)) {  // (rare) past the buffer: the overflow queue, or the row's rescan mark
+                        int r2 = bc + inc - n_l;
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const bool o = ((pm >> i) & 1) && r2 >= kRBC;
+                            r2 += (pm >> i) & 1;
+                            const u64 bo = __ballot(o);
+                            if (!bo) continue;
+                            const int slot = ovf + mbcnt64(bo);
+                            if (o) {
+                                if (slot < kROCap) {
+                                    oq_key[slot] = rkey(acc[rg][i][reg], qn_r, pos0 + i);
+                                    oq_row[slot] = (uint8_t)row;
+                                } else {
+                                    rescan_s[row] = 1;  // k_smerge re-scans this (pair, chunk) exactly
+                                }
+                            }
+                            ovf += popc64(bo);
+                        }
+                    }
+                    if (cj == 0) mybufc[row] = min(kRBC, bc + tot);
+                    drain = drain || __any(bc + tot >= kRBC);
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
+#ifndef RS_NODRAIN
+            if (drain || ovf) {
+                drain_buffers(lists, mybuf, mybufc, lock_s, erun_s, opub_s, pair_s, oq_key, oq_row, min(ovf, kROCap),
+                              Ew, k, a.qbound, a.nprobe, a.gP);
+                ovf = 0;
+            }
+#endif
+            u = un;
+        }
+
+        // ---- item epilogue: every wave's buffers into the lists (rows split over
+        // the waves, two per pass: one per half-wave), then the lists out
+        if (mybufc[lane] > 0) atomicMax(erun_s + lane, __float_as_uint(Ew));
+        __syncthreads();
+        const int ln = opaque(lane);  // (lane-derived addresses computed here, not hoisted)
+#pragma unroll 1
+        for (int j = 0; j < 16; j += 2) {
+            const int hl = ln & 31, row = wave * 16 + j + (ln >> 5);
+            const int c0 = bufc[0 * kRQ + row], c1 = bufc[1 * kRQ + row], c2 = bufc[2 * kRQ + row],
+                      c3 = bufc[3 * kRQ + row];
+            const int n = c0 + c1 + c2 + c3;
+            if (!__any(n > 0)) continue;
+            for (int r0 = 0; __any(n > r0); r0 += 32) {
+                const int e = r0 + hl;
+                u64 b = kEmptyKey;
+                if (e < n) {
+                    const int w = e < c0 ? 0 : e < c0 + c1 ? 1 : e < c0 + c1 + c2 ? 2 : 3;
+                    const int off = e - (w == 0 ? 0 : w == 1 ? c0 : w == 2 ? c0 + c1 : c0 + c1 + c2);
+                    b = bufs[(w * kRQ + row) * kRBC + off];
+                }
+                u64 lst[1] = {lists[row * kRK2 + hl]};
+                half_merge_batch1<1>(lst, b);
+                lists[row * kRK2 + hl] = lst[0];
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        __syncthreads();
+#pragma unroll 1
+        for (int j = 0; j < 16; j += 2) {
+            const int hl = ln & 31, row = wave * 16 + j + (ln >> 5);
+            const int pr = pair_s[row];
+            // (a row that lost keys: its last slot <= any bound, so k_smerge re-scans the chunk exactly)
+            if (pr >= 0)
+                a.partial[((int64_t)pr * a.nch_max + ch) * kRK2 + hl] =
+                    hl == kRK2 - 1 && rescan_s[row] ? ((u64)f2ord(-3.40282347e38f) << 32) : lists[row * kRK2 + hl];
+        }
+        if (my_pair >= 0) {
+            const float er = __uint_as_float(erun_s[lane]);
+            a.pE[(int64_t)my_pair * a.nch_max + ch] = fmaxf(er, 0x1p-126f);  // (>= every listed key's bound)
+            const u64 kk = lists[lane * kRK2 + k - 1];
+            if (a.qbound && kk != kEmptyKey)
+                atomicMin(a.qbound + my_q, f2ord(rup(rup(key_score(kk) + er) * a.gP) + 0x1p-125f));
+        }
+        __syncthreads();
+    }
+    n_surv = wave_sum_u64(n_surv);
+    if (a.stats && lane == 0) {
+        atomicAdd(a.stats + 0, n_tiles * 64ull * 64ull);  // (row, candidate) pairs screened
+        atomicAdd(a.stats + 2, n_tiles);                   // tiles computed (of 64 candidates)
+        atomicAdd(a.stats + 4, n_skip);                    // tiles skipped by the triangle test
+        atomicAdd(a.stats + 7, n_surv);                    // survivors appended
+    }
+}
+
+}  // namespace lira
+
+namespace lira {
+
+bool rscreen_shape_ok(int64_t dpad, int64_t k) { return k >= 1 && k <= 24 && dpad >= 32 && dpad <= 128 && dpad % 32 == 0; }
+int rscreen_smem() { return RSmem::total; }
+
+template <int NC>
+static hipError_t launch_r(const RArgs &a, int grid, hipStream_t st) {
+    static std::atomic<uint64_t> attr{0};
+    hipError_t e = set_smem_attr_once(attr, (const void *)k_screen_r<NC>, RSmem::total);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_screen_r<NC>), dim3(grid), dim3(256), RSmem::total, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_rscreen(const RArgs &a, int grid, hipStream_t st) {
+    switch (a.dpad / 32) {
+        case 1: return launch_r<1>(a, grid, st);
+        case 2: return launch_r<2>(a, grid, st);
+        case 3: return launch_r<3>(a, grid, st);
+        case 4: return launch_r<4>(a, grid, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace lira

@@ -1,0 +1,36 @@
+// lira_rscreen.hpp -- arguments of the wave-streaming screen k_screen_r
+// (lira_rscreen.hip), filled by screen_topk (lira_screen.hip).
+#pragma once
+#include "lira_device.hpp"
+
+namespace lira {
+
+struct RArgs {
+    const char *Xb;          // split-bf16 copy (bytes): per tile and 16-dim chunk 4 KiB [g 4][p 64][8 bf16]
+    const float *xadj;       // centred fl(||x'||^2)/2 per storage row (+inf: padding)
+    const float *rmax;       // per list: max ||x'|| (centred)
+    const float2 *tstat;     // per tile: lo <= ||x - c|| <= hi (NULL: no triangle skip)
+    const float *tres;       // per tile: max ||x' - hi(x')||
+    const int32_t *tile_off, *cnt, *qoff, *qlist;
+    const int4 *itab;        // item -> (virtual partition, query block, chunk, -)
+    int32_t *head;           // plan counters / XCD queue bounds (k_plan)
+    const float4 *QN;        // per pair: qn = fl(||q'||^2), ||q'|| (up), pair, fl(||q - c||)
+    const float *QE;         // per pair: ||q' - hi(q')|| (up)
+    const uint16_t *QH;      // per pair: hi(q') as bf16, dpad dims
+    u64 *partial;            // [pair][nch_max][32] row lists (k_smerge's input)
+    float *pE;               // [pair][nch_max] each list's screening-error bound
+    uint32_t *qbound;        // [nq] f2ord(bound on the final k-th exact score)
+    int64_t d, dpad;
+    int n_lists, n_virt, nprobe, k, bpc, nch_max;
+    float gP;                // >= 1 + (d + 4) 2^-24 (bound_P's factor, rounded up)
+    float invF;              // >= 1 / (1 - (d + 4) 2^-24) (s_lim's factor, rounded up)
+    unsigned long long *stats;
+};
+
+// the shapes k_screen_r implements: L2 on the centred split copy, hi x hi,
+// k <= 24 (32-key row lists), dpad <= 128 (the queries' hi parts in registers)
+bool rscreen_shape_ok(int64_t dpad, int64_t k);
+int rscreen_smem();
+hipError_t launch_rscreen(const RArgs &a, int grid, hipStream_t st);
+
+}  // namespace lira

@@ -50,6 +50,9 @@
 #include "lira_bounds.hpp"
 #include "lira_device.hpp"
 #include "lira_internal.hpp"
+#include "lira_rscreen.hpp"
+
+#include <cmath>
 
 namespace lira {
 
@@ -325,45 +328,6 @@ bool debug_build() { return false; }
 #define LIRA_SGLDS sglds16
 #endif
 
-// XCD-aware work queues (k_plan): claim the next item of this workgroup's own
-// XCD's queue, stealing from the others (in order) once it is empty; -1 when
-// every queue is.  Thread 0 only; xq[9] (LDS) = the queue starts + end, x /
-// tries the claimant's state.
-__device__ __forceinline__ int xcd_id() {
-    unsigned v;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
-    return (int)(v & 7u);
-}
-// Once the claimant's queue is empty it reads all 8 claim counters at once (one
-// round trip) and steals from the first queue that still has items: walking
-// the queues with one atomic each in turn cost every workgroup up to 8
-// serial atomic round trips at the end of the scan.  tries = 8: all empty.
-__device__ __forceinline__ int claim_item(int32_t *head, const int *xq, int &x, int &tries) {
-    if (tries >= 8) return -1;
-    {
-        const int i = xq[x] + atomicAdd(&head[2 + x], 1);
-        if (i < xq[x + 1]) return i;
-    }
-    for (;;) {
-        int c[8];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) c[r] = __hip_atomic_load(&head[2 + r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int pick = -1;
-#pragma unroll
-        for (int s = 1; s <= 8; ++s) {
-            const int r = (x + s) & 7;
-            if (pick < 0 && xq[r] + c[r] < xq[r + 1]) pick = r;
-        }
-        if (pick < 0) {
-            tries = 8;
-            return -1;
-        }
-        x = pick;
-        const int i = xq[x] + atomicAdd(&head[2 + x], 1);
-        if (i < xq[x + 1]) return i;
-    }
-}
-
 // acc += x * splat(q.lo) / splat(q.hi) on packed fp32.  Inline asm: hipcc
 // otherwise copies every odd-register splat source with a v_mov first (one
 // extra VALU op per 8 FMAs), while op_sel reads either half in place.
@@ -374,23 +338,6 @@ __device__ __forceinline__ void pkfma_hi(f2 &acc, f2 x, f2 q) {
     asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(x), "v"(q));
 }
 
-// Inclusive prefix sum within each 16-lane group (= DPP row): 4 row_shr
-// steps with zero fill, no LDS round trips (a __shfl_up chain was 4
-// dependent ds_bpermutes per selection pass)
-__device__ __forceinline__ int row16_incl_scan(int v) {
-    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);  // row_shr:1
-    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);  // row_shr:2
-    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);  // row_shr:4
-    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);  // row_shr:8
-    return v;
-}
-// lane 15 of each 16-lane group, broadcast to the group (the group's total)
-__device__ __forceinline__ int row16_total(int inc) {
-    const int t0 = __builtin_amdgcn_readlane(inc, 15), t1 = __builtin_amdgcn_readlane(inc, 31);
-    const int t2 = __builtin_amdgcn_readlane(inc, 47), t3 = __builtin_amdgcn_readlane(inc, 63);
-    const int g = (int)(threadIdx.x & 63) >> 4;
-    return g == 0 ? t0 : g == 1 ? t1 : g == 2 ? t2 : t3;
-}
 // the value lane 4 g + reg holds (lanes 0..15: one per query row), for every
 // lane of group g (4 v_readlane instead of a ds_bpermute)
 __device__ __forceinline__ float from_row_lane(float v, int reg, int g) {
@@ -2039,6 +1986,7 @@ static int screen_smem(int qr, int rl) {
 struct SPlan {
     int rl = 1, qr = 64, K2 = 32, bpc = 1, bpc_near = 1, nch_max = 1, grid = 1, smem = 0, mfma = 1, split = 0;
     int bpc_near_min = 1, workers = 1;  // the plan picks group 0's chunk size in [bpc_near_min, bpc_near]
+    int rs = 0;  // the wave-streaming screen k_screen_r (lira_rscreen.hip) instead of k_screen_m
     int pp = 0;  // per-pair query records (QN / QE / QH per pair, k_pairs or k_seed_t<.., PAIRS>)
                  // instead of k_qstage's per-block copy: the hi x hi k_screen_m
     int64_t max_qblk = 0;
@@ -2094,6 +2042,10 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // (the wide k_screen_w and wave-resident k_screen_v screens measured 0.571 /
     // 1.50 ms against 0.325 on SIFT1M: removed in round 4)
     pl.pp = pl.split == 3;
+    // k_screen_r where it applies (its own preconditions on the scan's flags are in screen_topk)
+    pl.rs = op.rscreen && pl.split == 3 && idx->metric == LIRA_METRIC_L2 && idx->xadjc && idx->pivot &&
+            rscreen_shape_ok(idx->dpad, k) && !(flags & LIRA_SCAN_PER_PARTITION) && op.seed && idx->X &&
+            idx->lstat;
     pl.smem = !pl.mfma       ? screen_smem(pl.qr, pl.rl)
               : pl.qr == 128 ? (pl.split == 2 ? SSmem<128, 1, true, true>::total
                                 : pl.rl == 1 ? SSmem<128, 1, true>::total : SSmem<128, 2, true>::total)
@@ -2202,7 +2154,8 @@ size_t screen_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe, 
 // the kernel a screened scan of this shape runs (lira_scan_describe)
 std::string screen_describe(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, unsigned flags) {
     SPlan pl = make_splan(idx, nq, nprobe, k, flags);
-    std::string s = pl.mfma ? (pl.split == 3 ? "k_screen_m hi-x hi-q bf16 v_mfma_f32_16x16x32_bf16"
+    std::string s = pl.rs ? std::string("k_screen_r hi-x hi-q bf16 v_mfma_f32_16x16x32_bf16 (wave-streaming)")
+                    : pl.mfma ? (pl.split == 3 ? "k_screen_m hi-x hi-q bf16 v_mfma_f32_16x16x32_bf16"
                                  : pl.split == 2 ? "k_screen_m hi-x split-bf16 v_mfma_f32_16x16x32_bf16"
                                  : pl.split ? "k_screen_m split-bf16 v_mfma_f32_16x16x32_bf16"
                                         : "k_screen_m fp32 v_mfma_f32_16x16x4_f32")
@@ -2468,8 +2421,43 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     a.bpc_near = groups == 2 ? pl.bpc_near : pl.bpc;
     a.nch_max = pl.nch_max;
     a.stats = idx->stats_on ? (unsigned long long *)idx->stats : nullptr;
-    hipError_t e = idx->metric == LIRA_METRIC_L2 ? launch_screen_rl<LIRA_METRIC_L2>(a, pl, st)
-                                                   : launch_screen_rl<LIRA_METRIC_IP>(a, pl, st);
+    hipError_t e;
+    if (pl.rs && fused && centred && qbound && pl.bpc <= 128 && pl.bpc_near <= 128) {
+        RArgs r;
+        r.Xb = (const char *)idx->Xb;
+        r.xadj = idx->xadjc;
+        r.rmax = idx->rmaxc;
+        r.tstat = tri ? idx->tstat : nullptr;
+        r.tres = idx->tres;
+        r.tile_off = idx->tile_off;
+        r.cnt = cnt;
+        r.qoff = qoff;
+        r.qlist = qlist;
+        r.itab = itab;
+        r.head = head;
+        r.QN = QN;
+        r.QE = QE;
+        r.QH = QH;
+        r.partial = partial;
+        r.pE = pE;
+        r.qbound = qbound;
+        r.d = idx->d;
+        r.dpad = idx->dpad;
+        r.n_lists = (int)idx->n_lists;
+        r.n_virt = nvirt;
+        r.nprobe = (int)nprobe;
+        r.k = (int)k;
+        r.bpc = pl.bpc;
+        r.nch_max = pl.nch_max;
+        const double g = ((double)idx->d + 4.0) * 0x1p-24;
+        r.gP = std::nextafter((float)((1.0 + g) * (1.0 + 0x1p-50)), INFINITY);
+        r.invF = std::nextafter((float)((1.0 / (1.0 - g)) * (1.0 + 0x1p-50)), INFINITY);
+        r.stats = a.stats;
+        e = launch_rscreen(r, pl.grid, st);
+    } else {
+        e = idx->metric == LIRA_METRIC_L2 ? launch_screen_rl<LIRA_METRIC_L2>(a, pl, st)
+                                          : launch_screen_rl<LIRA_METRIC_IP>(a, pl, st);
+    }
     if (e != hipSuccess) return fail(LIRA_EHIP, std::string("k_screen launch: ") + hipGetErrorString(e));
     if (ev[2]) LIRA_HIP_TRY(hipEventRecord(ev[2], st));
     if (a.stats && filter && npairs > 0) {

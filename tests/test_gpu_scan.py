@@ -86,6 +86,11 @@ def check_vs_oracle(x, q, d2b, probe, b, k, metric, dedup=True):
             assert np.array_equal(I, Io), f"ids differ (xhi={xhi})"
             assert np.array_equal(bits(D), bits(Do)), f"distances differ (xhi={xhi})"
         idx.set_option("xhi", -1)
+        # the hi x hi screen as k_screen_m (LIRA_OPT_RSCREEN = 0) where k_screen_r is the default
+        idx.set_option("rscreen", 0)
+        D, I, nc = run(idx, q, probe, k, dedup=dedup)
+        idx.set_option("rscreen", 1)
+        assert np.array_equal(I, Io) and np.array_equal(bits(D), bits(Do)), "differ (rscreen=0)"
     if k <= 120:
         # the compact index (no fp32 tiles: row-major + split-bf16 copies only)
         idc = make_index(x, d2b, b, metric, keep_tiles=False)
@@ -374,7 +379,8 @@ def test_options_do_not_change_results(metric):
     ref = run(idx, q, probe, 10)
     for name, vals in (("qr", (128,)), ("two_phase", (0, 2)), ("seed", (0,)), ("share", (0,)),
                        ("prune", (0,)), ("split", (0,)), ("mfma", (0, 2)), ("rounds", (1, 64)),
-                       ("near_rounds", (2, 8)), ("screen", (0,)), ("probes_hint", (1, 4)), ("xhi", (0, 1, 2))):
+                       ("near_rounds", (2, 8)), ("screen", (0,)), ("probes_hint", (1, 4)), ("xhi", (0, 1, 2)),
+                       ("rscreen", (0,))):
         old = idx.get_option(name)
         for v in vals:
             idx.set_option(name, v)
@@ -421,20 +427,16 @@ def test_split_screen_extreme_values(metric):
     check_vs_oracle(x, q, d2b, probe, b, 10, metric)
 
 
-@pytest.mark.parametrize("wide", [1, 2])
 @pytest.mark.parametrize("d,uniform,red", [(48, False, 0.0), (96, False, 0.2), (128, False, 0.0), (128, True, 0.0),
                                            (100, True, 0.1)])
-def test_wide_screen_vs_oracle(d, uniform, red, wide):
-    # the wide screen k_screen_w (256 rows per item, 128-candidate blocks, 16-KiB
-    # ring slots): several query blocks per list, lists of several chunks with a
-    # partial last block (one tile) and padded rows, partial query blocks,
-    # redundant rows with and without dedup
+def test_screen_many_blocks_vs_oracle(d, uniform, red):
+    # the default screen over several query blocks per list, lists of several
+    # chunks with a partial last block (one tile) and padded rows, partial query
+    # blocks, redundant rows with and without dedup, at 1 / 8 (auto) / 64 items
+    # per workgroup
     n, b, nq, nprobe, k = 60000, 10, 1500, 4, 10
     x, q, d2b, probe = random_case(300 + d, n, d, b, nq, nprobe, "L2", red=red, uniform=uniform)
     idx = make_index(x, d2b, b, "L2")
-    idx.set_option("wide", wide)
-    name = "k_screen_w" if wide == 1 else "k_screen_v"
-    assert name in idx.describe(nq, nprobe, k), idx.describe(nq, nprobe, k)
     off, ids = oracle.build_csr(d2b, b)
     vecs = oracle.gather_lists(x, off, ids)
     for dedup in (True, False):
@@ -447,14 +449,12 @@ def test_wide_screen_vs_oracle(d, uniform, red, wide):
         idx.set_option("rounds", 0)
 
 
-@pytest.mark.parametrize("wide", [1, 2])
-def test_wide_screen_clustered_filter_and_ties(wide):
-    # separated clusters: k_pairs drops the far pairs (no work items), the
-    # triangle skip drops blocks; small-integer vectors: exact ties at the k-th
+def test_screen_clustered_filter_and_ties():
+    # separated clusters: the plan's filter drops the far pairs (no work items,
+    # counted), the triangle skip drops blocks; small-integer vectors: exact
+    # ties at the k-th
     x, q, d2b, probe = clustered_case(71, 40000, 128, 16, 900, 6, ints=True)
     idx = make_index(x, d2b, 16, "L2")
-    idx.set_option("wide", wide)
-    assert ("k_screen_w" if wide == 1 else "k_screen_v") in idx.describe(q.shape[0], probe.shape[1], 10)
     off, ids = oracle.build_csr(d2b, 16)
     vecs = oracle.gather_lists(x, off, ids)
     for k in (1, 10, 24):
@@ -467,3 +467,4 @@ def test_wide_screen_clustered_filter_and_ties(wide):
         st = idx.stats_read()
         idx.set_stats(False)
         assert st["blocks"] > 0
+        assert st["pairs_pruned_plan"] > 0 and st["candidates_pruned_plan"] >= st["pairs_pruned_plan"]
