@@ -51,7 +51,7 @@ static constexpr int kRW = 4;           // waves per workgroup
 static constexpr int kRK2 = 32;         // row list keys (k <= 24)
 static constexpr int kRBC = 16;         // survivor buffer keys per (wave, row)
 static constexpr int kRMaxTiles = 512;  // tiles per item (the plan caps a chunk at 128 blocks)
-static constexpr int kROCap = 128;      // overflow queue entries per wave (per tile's selection)
+static constexpr int kROCap = 128;      // survivor queue entries per wave (>= two candidate masks)
 
 struct RSmem {
     static constexpr int aq = 0;                                    // [4 chunks][4 row groups][64 lanes] 16 B: A operands
@@ -66,13 +66,25 @@ struct RSmem {
     static constexpr int erun = qn + kRQ * 16;                       // [64] float bits: running error bound
     static constexpr int lock = erun + kRQ * 4;                      // [64] int
     static constexpr int opub = lock + kRQ * 4;                      // [64] uint: bound last published
-    static constexpr int resc = opub + kRQ * 4;                      // [64] int: row needs k_smerge's rescan
-    static constexpr int oqk = resc + kRQ * 4;                       // [4][kROCap] u64: overflow queue keys
+    static constexpr int oqk = opub + kRQ * 4;                       // [4][kROCap] u64: survivor queue keys
     static constexpr int oqr = oqk + kRW * kROCap * 8;               // [4][kROCap] u8: their rows
-    static constexpr int meta = oqr + kRW * kROCap;                  // [16] int
+    static constexpr int kth = oqr + kRW * kROCap;                   // [64] u64: each list's k-th key
+    static constexpr int meta = kth + kRQ * 8;                       // [16] int
     static constexpr int total = meta + 64;
 };
 static_assert(RSmem::total <= 80 * 1024, "k_screen_r: two workgroups per CU");
+static_assert(kROCap >= 128, "a drained queue takes two full candidate masks");
+
+// Timing experiment (-DRS_CLOCKS builds only): per-wave cycle split of the
+// kernel, summed over waves, read by lira_debug_rs_clocks
+#ifdef RS_CLOCKS
+__device__ unsigned long long g_rs_clk[16];
+#define RCLK(v) const long long v = clock64()
+#define RACC(slot, a, b) (clk[slot] += (unsigned long long)((b) - (a)))
+#else
+#define RCLK(v)
+#define RACC(slot, a, b)
+#endif
 
 // a value the compiler must treat as produced here (keeps per-lane address
 // arithmetic from being hoisted out of the loops: hipcc otherwise precomputed
@@ -88,10 +100,15 @@ __device__ __forceinline__ float rdn(float x) { return __builtin_fmaf(-__builtin
 
 // err_E<L2>(qnorm, Rb, d, split = 3, dpad, centred = 1, hres, qres) in fp32:
 // every term is >= 0, so the ~16 roundings stay below 2^-20 relative and the
-// final factor covers them; + 2^-125 >= d 2^-140 (lira_bounds.hpp)
+// final factor covers them; + 2^-125 >= d 2^-140 (lira_bounds.hpp).
+// The MFMA chain here starts from C = -xadj (no separate fl(dot - xadj)): one
+// more add, and every partial sum is bounded by xadj + ||q'|| (R + rho), xadj <=
+// fl(Rb^2) / 2, so the accumulation term counts dpad + 1 adds at 2^-22 of that
+// (lira_bounds.hpp's model: any order or rounding mode at <= 2^-22 per add)
 __device__ __forceinline__ float errE_r(float qnorm, float Rb, float hres, float qres, float dp) {
     const float ex = hres >= 0.0f ? hres * 1.0001f : 0x1p-8f * 1.02f * Rb;
-    const float ed = ex * qnorm + qres * (Rb + ex) * 1.0001f + 2.0f * dp * 0x1p-22f * 1.02f * qnorm * (Rb + ex) +
+    const float ed = ex * qnorm + qres * (Rb + ex) * 1.0001f +
+                     2.0f * (dp + 1.0f) * 0x1p-22f * 1.02f * (qnorm * (Rb + ex) + 0.5001f * Rb * Rb) +
                      2.0f * dp * 0x1p-96f * (qnorm + Rb + ex + 1.0f);
     const float s = qnorm + Rb;
     return (2.0f * ed + (1.05f * 8.0f + 2.01f + 2.0f) * 0x1p-24f * s * s) * (1.0f + 0x1p-18f) + 0x1p-125f;
@@ -105,23 +122,36 @@ __device__ __forceinline__ u64 rkey(float wv, float qn, uint32_t pos) {
     return ((u64)f2ord(s) << 32) | pos;
 }
 
+// Buffered survivors carry fl(dot - xadj) instead of the score: wkey = (f2ord(-wv),
+// storage position), ascending in the score for a fixed row; converted to the
+// list key (rkey, the same arithmetic) when merged, where the row's qn is one
+// broadcast read (the selection then needs no LDS read)
+__device__ __forceinline__ u64 wkey(float wv, uint32_t pos) { return ((u64)f2ord(-wv) << 32) | pos; }
+__device__ __forceinline__ u64 wkey_to_key(u64 wk, float qn) {
+    return rkey(-ord2f((uint32_t)(wk >> 32)), qn, (uint32_t)wk);
+}
+
 // Merge this wave's buffer of `row` (n keys) into the shared list, under the
 // row's LDS lock: raise the row's running error bound to the wave's first
 // (readers take the list's k-th key, then the bound: program order in both),
 // half-wave merge, publish the query's bound if the list's k-th improved.
-__device__ __forceinline__ void flush_row(u64 *lists, const u64 *mybuf, int *lock_s, uint32_t *erun_s,
+__device__ __forceinline__ void flush_row(u64 *lists, u64 *kth_s, const u64 *mybuf, int *lock_s, uint32_t *erun_s,
                                        uint32_t *opub_s, const int *pair_s, int row, int n, int ew_bits, int k,
-                                       uint32_t *qbound, int nprobe, float gP) {
+                                       uint32_t *qbound, int nprobe, float gP, float qn_row) {
     const int lane = lane_id(), hl = lane & 31;
+#ifdef RS_CLOCKS
+    if (lane == 0) atomicAdd(&g_rs_clk[12], 1ull);
+#endif
     if (lane == 0) {
         while (atomicCAS(lock_s + row, 0, 1) != 0) __builtin_amdgcn_s_sleep(1);
         atomicMax(erun_s + row, (uint32_t)ew_bits);
     }
     asm volatile("" ::: "memory");
     u64 lst[1] = {lists[row * kRK2 + hl]};
-    const u64 b = hl < n ? mybuf[row * kRBC + hl] : kEmptyKey;
+    const u64 b = hl < n ? wkey_to_key(mybuf[row * kRBC + hl], qn_row) : kEmptyKey;
     half_merge_batch1<1>(lst, b);
     if (lane < 32) lists[row * kRK2 + hl] = lst[0];
+    if (lane == k - 1) kth_s[row] = lst[0];
     if (lane == k - 1 && lst[0] != kEmptyKey && qbound) {
         const int pr = pair_s[row];
         if (pr >= 0) {
@@ -138,21 +168,21 @@ __device__ __forceinline__ void flush_row(u64 *lists, const u64 *mybuf, int *loc
     __builtin_amdgcn_wave_barrier();
 }
 
-// After a tile's selection (the accumulators dead): merge this wave's full row
-// buffers into the lists, then move the overflow queue into the buffers (LDS
-// atomic slots), merging every buffer that fills, until the queue is empty.
-__device__ __forceinline__ void drain_buffers(u64 *lists, u64 *mybuf, int *mybufc, int *lock_s, uint32_t *erun_s,
-                                           uint32_t *opub_s, const int *pair_s, const u64 *oq_key,
-                                           const uint8_t *oq_row, int nq, float Ew, int k, uint32_t *qbound,
-                                           int nprobe, float gP) {
+// Merge this wave's full row buffers into the lists, then move the survivor
+// queue (raw fl(-xadj + dot) bits, position; row) into the buffers (LDS atomic
+// slots), merging every buffer that fills, until the queue is empty.
+__device__ __forceinline__ void drain_buffers(u64 *lists, u64 *kth_s, u64 *mybuf, int *mybufc, int *lock_s,
+                                           uint32_t *erun_s, uint32_t *opub_s, const int *pair_s,
+                                           const float4 *rec_s, const u64 *oq_key, const uint8_t *oq_row, int nq,
+                                           float Ew, int k, uint32_t *qbound, int nprobe, float gP) {
     const int lane = lane_id();
     auto flush_full = [&]() {
         u64 full = __ballot(mybufc[lane] >= kRBC);  // lane = row
         while (full) {
             const int row = __builtin_ctzll(full);
             full &= full - 1;
-            flush_row(lists, mybuf, lock_s, erun_s, opub_s, pair_s, row, kRBC,
-                      __builtin_amdgcn_readlane(__float_as_int(Ew), row), k, qbound, nprobe, gP);
+            flush_row(lists, kth_s, mybuf, lock_s, erun_s, opub_s, pair_s, row, kRBC,
+                      __builtin_amdgcn_readlane(__float_as_int(Ew), row), k, qbound, nprobe, gP, rec_s[row].x);
             if (lane == 0) mybufc[row] = 0;
             __builtin_amdgcn_wave_barrier();
         }
@@ -162,7 +192,11 @@ __device__ __forceinline__ void drain_buffers(u64 *lists, u64 *mybuf, int *mybuf
         const int e = e0 + lane;
         bool pend = e < nq;
         const int row = pend ? oq_row[e] : 0;
-        const u64 key = pend ? oq_key[e] : kEmptyKey;
+        u64 key = kEmptyKey;
+        if (pend) {  // (the queue holds fl(-xadj + dot) raw: the selection does no conversion)
+            const u64 q = oq_key[e];
+            key = wkey(__uint_as_float((uint32_t)(q >> 32)), (uint32_t)q);
+        }
         while (__any(pend)) {
             if (pend) {
                 const int slot = atomicAdd(mybufc + row, 1);
@@ -195,8 +229,8 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
     uint32_t *erun_s = (uint32_t *)(smem + RSmem::erun);
     int *lock_s = (int *)(smem + RSmem::lock);
     uint32_t *opub_s = (uint32_t *)(smem + RSmem::opub);
-    int *rescan_s = (int *)(smem + RSmem::resc);
     int *meta = (int *)(smem + RSmem::meta);
+    u64 *kth_s = (u64 *)(smem + RSmem::kth);
     __shared__ int xq[9];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -209,12 +243,15 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
     float *myh = hs + wave * kRQ;
     u64 *oq_key = (u64 *)(smem + RSmem::oqk) + wave * kROCap;
     uint8_t *oq_row = (uint8_t *)(smem + RSmem::oqr) + wave * kROCap;
-    int ovf = 0;  // overflow queue fill (wave-uniform)
     const bool TRI = a.tstat != nullptr;
     // B fragment: the lane's byte offset inside a tile's 32-dim chunk
     const uint32_t lane_off = (uint32_t)((g >> 1) * 4096 + (g & 1) * 1024 + cj * 16);
     const int64_t tile_bytes = a.dpad * 64 * 4;
     unsigned long long n_tiles = 0, n_skip = 0, n_surv = 0;
+#ifdef RS_CLOCKS
+    unsigned long long clk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long surv_g0 = 0, tiles_g0 = 0;
+#endif
 
     const int bpc_near_d = __builtin_amdgcn_readfirstlane(a.head[19]);
     int qx = 0, qtries = 0, nxt = -1;
@@ -226,6 +263,7 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
         if (nxt >= 0) e_nxt = a.itab[nxt];
     }
     for (;;) {
+        RCLK(t_item);
         if (tid == 0) {  // the next item claimed, and its entry loaded, one item ahead
             const int item = nxt, ok = item >= 0;
             int4 e = make_int4(0, 0, 0, 0);
@@ -265,7 +303,7 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
             erun_s[lane] = 0u;
             lock_s[lane] = 0;
             opub_s[lane] = ~0u;
-            rescan_s[lane] = 0;
+            kth_s[lane] = kEmptyKey;
         }
         mybufc[lane] = 0;
         {
@@ -291,35 +329,30 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
         }
         __syncthreads();
 
-        // ---- per-row bound state (lane = row)
-        uint32_t pub = a.qbound && my_q >= 0 ? __hip_atomic_load(a.qbound + my_q, __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_AGENT) : ~0u;
+        // ---- per-row bound state (lane = row; qbound is always set here)
+        const float my_qn = qrec.x, my_qnorm = qrec.y, my_dq = qrec.w;
+        const uint32_t *pub_at = a.qbound + (my_q >= 0 ? my_q : 0);  // (a padding row reads query 0's: unused)
+        uint32_t pub = __hip_atomic_load(pub_at, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         float Tc = -1.0f, Ac = __builtin_inff(), triA = -__builtin_inff(), triB = __builtin_inff();
         float Ew = 0.0f;  // the largest error bound of the tiles this wave screened (lane = row)
-        // T: the row's bound on its final k-th exact score (shared list, published bound)
+        // T: the row's bound on its final k-th exact score (shared list, published bound).
+        // No divergent branch (the published bound's load stays countable for the
+        // compiler's waits: a conditional one cost a vmcnt(0) per tile)
         auto update_T = [&]() {
-            const u64 kk = lists[lane * kRK2 + k - 1];
+            const u64 kk = kth_s[lane];
             asm volatile("" ::: "memory");  // (the list's key first, then its bound: see flush_row)
             const float er = __uint_as_float(erun_s[lane]);
-            float T = __builtin_inff();
-            if (kk != kEmptyKey) T = rup(rup(key_score(kk) + er) * a.gP) + 0x1p-125f;
-            if (pub != ~0u) T = fminf(T, ord2f(pub));
-            if (a.qbound && my_q >= 0)
-                pub = __hip_atomic_load(a.qbound + my_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (T != Tc) {
+            float T = kk != kEmptyKey ? rup(rup(key_score(kk) + er) * a.gP) + 0x1p-125f : __builtin_inff();
+            T = fminf(T, ord2f(pub));  // (~0u, nothing published: a NaN, which fminf ignores)
+            pub = __hip_atomic_load(pub_at, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__any(T != Tc)) {  // (recomputed for every lane: an unchanged T gives the same values)
                 Tc = T;
-                Ac = T < 3e38f ? rup(rup(fmaxf(T, 0.0f) + 0x1p-125f) * a.invF) : __builtin_inff();
-                if (my_pair < 0) {
-                    triA = __builtin_inff();
-                    triB = -__builtin_inff();
-                } else if (T < 3e38f) {
-                    const float rad = rup(__builtin_sqrtf(Ac)), dq = rec_s[lane].w;
-                    triA = rdn(rdn(dq) - rad);
-                    triB = rup(rup(dq) + rad);
-                } else {
-                    triA = -__builtin_inff();
-                    triB = __builtin_inff();
-                }
+                const bool fin = T < 3e38f;
+                Ac = fin ? rup(rup(fmaxf(T, 0.0f) + 0x1p-125f) * a.invF) : __builtin_inff();
+                // (v_sqrt_f32, <= 1 ulp: inside rup's 2^-20 margin)
+                const float rad = rup(__builtin_amdgcn_sqrtf(Ac));
+                triA = my_pair < 0 ? __builtin_inff() : fin ? rdn(rdn(my_dq) - rad) : -__builtin_inff();
+                triB = my_pair < 0 ? -__builtin_inff() : fin ? rup(rup(my_dq) + rad) : __builtin_inff();
             }
         };
         // tile u is needed by no row (wave-uniform)
@@ -330,6 +363,8 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
         };
 
         int u = wave;
+        RCLK(t_pro);
+        RACC(0, t_item, t_pro);
         update_T();
         while (u < nt && skip(u)) {
             ++n_skip;
@@ -342,24 +377,37 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
         // 32 VGPRs instead of 64)
         constexpr int RS = NC % 2 == 0 && NC >= 4 ? 2 : NC;
         rbf16x8 B[RS][4];
+        rf4 xa_n = (rf4)(0.0f);  // the next tile's xadj (candidates 4 cj .. + 3)
         if (u < nt) {
             const char *base = a.Xb + (int64_t)(tbase + u) * tile_bytes + lane_off;
 #pragma unroll
             for (int c = 0; c < RS; ++c)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) B[c][i] = *(const rbf16x8 *)(base + c * 8192 + i * 256);
+            xa_n = *(const rf4 *)(a.xadj + (int64_t)(tbase + u) * 64 + 4 * cj);
         }
+        int ovf = 0;  // survivor queue fill (wave-uniform)
+        // survivor queue -> this wave's row buffers (full ones merged into the lists)
+        auto drain = [&]() {
+#ifdef RS_NODRAIN  // timing experiment: the queue is discarded (results invalid)
+            ovf = 0;
+            return;
+#endif
+            drain_buffers(lists, kth_s, mybuf, mybufc, lock_s, erun_s, opub_s, pair_s, rec_s, oq_key, oq_row, ovf, Ew,
+                          k, a.qbound, a.nprobe, a.gP);
+            ovf = 0;
+        };
 
+        RCLK(t_loop0);
+        RACC(1, t_pro, t_loop0);
         while (u < nt) {
-            // the tile's xadj (in flight under the thresholds and the MFMAs)
-            const rf4 xa = *(const rf4 *)(a.xadj + (int64_t)(tbase + u) * 64 + 4 * cj);
+            RCLK(t_a);
+            const rf4 xa = xa_n;
             // ---- thresholds for tile u (lane = row), then each lane's 16 rows
             update_T();
             {
                 float h = __builtin_inff();
                 if (my_pair >= 0) {
-                    const float4 rr = rec_s[lane];
-                    const float my_qn = rr.x, my_qnorm = rr.y, my_qres = rr.z;
                     const float2 r = TRI ? tst[u] : make_float2(0.0f, R);
                     const float Rb = TRI ? fminf(R, rup(r.y)) : R;
                     const float Eb = errE_r(my_qnorm, Rb, TRI ? trs[u] : -1.0f, my_qres, dp);
@@ -383,18 +431,29 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
                 un += kRW;
             }
             const int ul = un < nt ? un : u;  // (the last tile's loads repeat the current tile)
+#ifdef RS_SAMETILE  // timing experiment: every load reads the item's first tile (L2-resident)
+            const char *cbase = a.Xb + (int64_t)tbase * tile_bytes + lane_off, *nbase = cbase;
+#else
             const char *cbase = a.Xb + (int64_t)(tbase + u) * tile_bytes + lane_off;
             const char *nbase = a.Xb + (int64_t)(tbase + ul) * tile_bytes + lane_off;
+#endif
+            xa_n = *(const rf4 *)(a.xadj + (int64_t)(tbase + ul) * 64 + 4 * cj);
+            // the rows' thresholds in selection order (read under the MFMAs)
+            const int g4 = opaque(4 * g);  // (row = 16 rg + g4 + reg)
+            rf4 hv[4];
+#pragma unroll
+            for (int rg = 0; rg < 4; ++rg) hv[rg] = *(const rf4 *)(myh + 16 * rg + g4);
+            RCLK(t_b);
+            RACC(2, t_a, t_b);
 
-            // ---- 64 rows x 64 candidates; each B fragment's slot reloaded after its 4 MFMAs
+            // ---- 64 rows x 64 candidates: acc = -xadj + dot (the first chunk's MFMAs
+            // take C = -xadj of their candidate; lane (g, j) holds candidates 4 j + i
+            // of rows 4 g + reg, so C is the same for every row group); each B
+            // fragment's slot reloaded after its 4 MFMAs
             rf4 acc[4][4];
-#pragma unroll
-            for (int rg = 0; rg < 4; ++rg)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) acc[rg][i] = (rf4)(0.0f);
-            // per chunk: the next chunk's A fragments (LDS), this chunk's 16 MFMAs, the
-            // slot's reloads; a scheduling barrier per chunk keeps the reloads where
-            // they are (left alone, hipcc sank them next to their consumers)
+            // per chunk: the A fragments (LDS), this chunk's 16 MFMAs, the slot's
+            // reloads; a scheduling barrier per chunk keeps the reloads where they are
+            // (left alone, hipcc sank them next to their consumers)
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
                 const int sl = c % RS, cn = c + RS;  // slot; the chunk that goes into it next
@@ -403,97 +462,103 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
                 for (int rg = 0; rg < 4; ++rg) Acur[rg] = __builtin_bit_cast(rbf16x8, aq_s[(c * 4 + rg) * 64 + lane]);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
+                    const rf4 cx = (rf4)(-xa[i]);
 #pragma unroll
                     for (int rg = 0; rg < 4; ++rg)
-                        acc[rg][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Acur[rg], B[sl][i], acc[rg][i], 0, 0, 0);
+                        acc[rg][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Acur[rg], B[sl][i], c == 0 ? cx : acc[rg][i],
+                                                                             0, 0, 0);
                     B[sl][i] = cn < NC ? *(const rbf16x8 *)(cbase + cn * 8192 + i * 256)
                                        : *(const rbf16x8 *)(nbase + (cn - NC) * 8192 + i * 256);
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
             ++n_tiles;
-            // wv = fl(dot - xadj) in place (the test's operand; the key's score is
-            // fl(qn - 2 wv), errE_r's 2 u s^2 allowance)
-#pragma unroll
-            for (int rg = 0; rg < 4; ++rg)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) acc[rg][i] = acc[rg][i] - xa[i];
+#ifdef RS_CLOCKS
+            if (vp < a.n_lists && a.n_virt > a.n_lists) ++tiles_g0;
+#endif
+            RCLK(t_c);
+            RACC(3, t_b, t_c);
 
-            // ---- selection: pass iff fl(dot - xadj) >= h (k_screen_m's test).  Per
-            // (row group, register) entry the four rows 16 rg + 4 g + reg (one per lane
-            // group): one max over the lane's 4 candidates and one compare per row;
-            // passing keys go to this wave's row buffers (ranks from a 16-lane prefix
-            // sum), keys past a full buffer to the overflow queue; both are drained
-            // below, once the accumulators are dead
-            const int g4 = opaque(4 * g);  // (row = 16 rg + g4 + reg)
-            const uint32_t pos0 = (uint32_t)((tbase + u) * 64) + (uint32_t)opaque(4 * cj);
-            bool drain = false;
+            // ---- selection: pass iff acc = -xadj + dot >= h.  Per (row group, register)
+            // entry e = 4 rg + reg, lane group g holds row 16 rg + 4 g + reg: four
+            // compares into wave masks (one per candidate slot i), skipped together
+            // when all are empty; each non-empty mask's lanes append (wv, position,
+            // row) to the wave's survivor queue at slots from the mask's prefix count,
+            // a mask that would overflow the queue draining it first
+            RCLK(t_d);
+            RACC(4, t_c, t_d);
+            const uint32_t pos0 = (uint32_t)((tbase + u) * 64) + (uint32_t)(4 * cj);
+            // The pass runs over (entry, half) steps h = 2 e + (i >> 1); a step that
+            // would overflow the queue stops it there, the queue is drained (one
+            // inlined call site) and the pass resumes at that step (rare)
+            for (int s0 = 0;;) {
+                // (the accumulators as if redefined: keeps the compares from being
+                // hoisted out of this loop, which cost 64 masks held in SGPRs)
 #pragma unroll
-            for (int rg = 0; rg < 4; ++rg) {
-                __builtin_amdgcn_sched_barrier(0);
-                const rf4 hv = *(const rf4 *)(myh + 16 * rg + g4);  // rows 16 rg + 4 g + reg
+                for (int rg = 0; rg < 4; ++rg)
 #pragma unroll
-                for (int reg = 0; reg < 4; ++reg) {
-                    const float hp = hv[reg];
-                    const float m = fmaxf(fmaxf(fmaxf(acc[rg][0][reg], acc[rg][1][reg]), acc[rg][2][reg]), acc[rg][3][reg]);
-                    if (!__any(m >= hp)) continue;
-#ifdef RS_NOSLOW
-                    drain = true; continue;
+                    for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(acc[rg][i]));
+                int stop = 32;
+#pragma unroll
+                for (int rg = 0; rg < 4; ++rg) {
+#pragma unroll
+                    for (int reg = 0; reg < 4; ++reg) {
+                        const int e = 4 * rg + reg;
+                        if (2 * e + 1 < s0 || 2 * e >= stop) continue;
+                        const float hp = hv[rg][reg];
+                        u64 m[4];
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) m[i] = __ballot(acc[rg][i][reg] >= hp);
+                        if (!(m[0] | m[1] | m[2] | m[3])) continue;
+#ifdef RS_CLOCKS
+                        clk[7] += 1ull << 32;  // (entries with survivors, high half)
 #endif
-                    int pm = 0;
+                        const uint8_t row = (uint8_t)(16 * rg + g4 + reg);
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) pm |= (acc[rg][i][reg] >= hp) << i;
-                    const int row = 16 * rg + g4 + reg;  // this lane group's row
-                    const int n_l = __builtin_popcount(pm);
-                    const int inc = row16_incl_scan(n_l);
-                    const int tot = row16_total(inc);
-                    const int bc = mybufc[row];
-                    const float qn_r = rec_s[row].x;
-                    int rank = bc + inc - n_l;  // buffer rank of my first key
-                    n_surv += (unsigned long long)n_l;
-                    bool over = false;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        if ((pm >> i) & 1) {
-                            if (rank < kRBC) mybuf[row * kRBC + rank] = rkey(acc[rg][i][reg], qn_r, pos0 + i);
-                            over = over || rank >= kRBC;
-                            ++rank;
-                        }
-                    }
-                    if (__any(over)) {  // (rare) past the buffer: the overflow queue, or the row's rescan mark
-                        int r2 = bc + inc - n_l;
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            const bool o = ((pm >> i) & 1) && r2 >= kRBC;
-                            r2 += (pm >> i) & 1;
-                            const u64 bo = __ballot(o);
-                            if (!bo) continue;
-                            const int slot = ovf + mbcnt64(bo);
-                            if (o) {
-                                if (slot < kROCap) {
-                                    oq_key[slot] = rkey(acc[rg][i][reg], qn_r, pos0 + i);
-                                    oq_row[slot] = (uint8_t)row;
-                                } else {
-                                    rescan_s[row] = 1;  // k_smerge re-scans this (pair, chunk) exactly
-                                }
+                        for (int hf = 0; hf < 2; ++hf) {
+                            const int h = 2 * e + hf;
+                            if (h < s0 || h >= stop) continue;
+                            const u64 ma = m[2 * hf], mb = m[2 * hf + 1];
+                            const int n = popc64(ma) + popc64(mb);
+                            if (!n) continue;
+                            if (ovf + n > kROCap) {  // (n <= 128: fits once drained)
+                                stop = h;
+                                continue;
                             }
-                            ovf += popc64(bo);
+                            n_surv += (unsigned long long)n;
+#ifdef RS_CLOCKS
+                            if (vp < a.n_lists && a.n_virt > a.n_lists) surv_g0 += (unsigned long long)n;
+#endif
+#ifdef RS_NOSURV  // timing experiment: survivors dropped (results invalid)
+                            continue;
+#endif
+                            if ((ma >> lane) & 1ull) {
+                                const int slot = ovf + mbcnt64(ma);
+                                oq_key[slot] = ((u64)__float_as_uint(acc[rg][2 * hf][reg]) << 32) | (pos0 + 2u * hf);
+                                oq_row[slot] = row;
+                            }
+                            if ((mb >> lane) & 1ull) {
+                                const int slot = ovf + popc64(ma) + mbcnt64(mb);
+                                oq_key[slot] = ((u64)__float_as_uint(acc[rg][2 * hf + 1][reg]) << 32) | (pos0 + 2u * hf + 1u);
+                                oq_row[slot] = row;
+                            }
+                            ovf += n;
                         }
                     }
-                    if (cj == 0) mybufc[row] = min(kRBC, bc + tot);
-                    drain = drain || __any(bc + tot >= kRBC);
-                    __builtin_amdgcn_wave_barrier();
                 }
-            }
-#ifndef RS_NODRAIN
-            if (drain || ovf) {
-                drain_buffers(lists, mybuf, mybufc, lock_s, erun_s, opub_s, pair_s, oq_key, oq_row, min(ovf, kROCap),
-                              Ew, k, a.qbound, a.nprobe, a.gP);
-                ovf = 0;
-            }
+                if (stop == 32) break;
+#ifdef RS_CLOCKS
+                n_skip += 1ull << 32;  // (mid-selection drains, high half)
 #endif
+                drain();
+                s0 = stop;
+            }
+            RCLK(t_e);
+            RACC(5, t_d, t_e);
             u = un;
         }
+        if (ovf) drain();
+        RCLK(t_epi);
 
         // ---- item epilogue: every wave's buffers into the lists (rows split over
         // the waves, two per pass: one per half-wave), then the lists out
@@ -507,13 +572,17 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
                       c3 = bufc[3 * kRQ + row];
             const int n = c0 + c1 + c2 + c3;
             if (!__any(n > 0)) continue;
+#ifdef RS_NOEPI  // timing experiment: buffers not merged at the item's end (results invalid)
+            continue;
+#endif
+            const float qn_r = rec_s[row].x;
             for (int r0 = 0; __any(n > r0); r0 += 32) {
                 const int e = r0 + hl;
                 u64 b = kEmptyKey;
                 if (e < n) {
                     const int w = e < c0 ? 0 : e < c0 + c1 ? 1 : e < c0 + c1 + c2 ? 2 : 3;
                     const int off = e - (w == 0 ? 0 : w == 1 ? c0 : w == 2 ? c0 + c1 : c0 + c1 + c2);
-                    b = bufs[(w * kRQ + row) * kRBC + off];
+                    b = wkey_to_key(bufs[(w * kRQ + row) * kRBC + off], qn_r);
                 }
                 u64 lst[1] = {lists[row * kRK2 + hl]};
                 half_merge_batch1<1>(lst, b);
@@ -526,10 +595,7 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
         for (int j = 0; j < 16; j += 2) {
             const int hl = ln & 31, row = wave * 16 + j + (ln >> 5);
             const int pr = pair_s[row];
-            // (a row that lost keys: its last slot <= any bound, so k_smerge re-scans the chunk exactly)
-            if (pr >= 0)
-                a.partial[((int64_t)pr * a.nch_max + ch) * kRK2 + hl] =
-                    hl == kRK2 - 1 && rescan_s[row] ? ((u64)f2ord(-3.40282347e38f) << 32) : lists[row * kRK2 + hl];
+            if (pr >= 0) a.partial[((int64_t)pr * a.nch_max + ch) * kRK2 + hl] = lists[row * kRK2 + hl];
         }
         if (my_pair >= 0) {
             const float er = __uint_as_float(erun_s[lane]);
@@ -539,8 +605,23 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
                 atomicMin(a.qbound + my_q, f2ord(rup(rup(key_score(kk) + er) * a.gP) + 0x1p-125f));
         }
         __syncthreads();
+        RCLK(t_end);
+        RACC(6, t_epi, t_end);
+#ifdef RS_CLOCKS
+        clk[7] += 1;
+#endif
     }
-    n_surv = wave_sum_u64(n_surv);
+#ifdef RS_CLOCKS
+    if (lane == 0) {
+        for (int i = 0; i < 8; ++i) atomicAdd(&g_rs_clk[i], clk[i]);
+        atomicAdd(&g_rs_clk[8], n_tiles);
+        atomicAdd(&g_rs_clk[9], n_skip);
+        atomicAdd(&g_rs_clk[10], 1ull);
+        atomicAdd(&g_rs_clk[11], n_surv);
+        atomicAdd(&g_rs_clk[13], surv_g0);
+        atomicAdd(&g_rs_clk[14], tiles_g0);
+    }
+#endif
     if (a.stats && lane == 0) {
         atomicAdd(a.stats + 0, n_tiles * 64ull * 64ull);  // (row, candidate) pairs screened
         atomicAdd(a.stats + 2, n_tiles);                   // tiles computed (of 64 candidates)
@@ -564,6 +645,20 @@ static hipError_t launch_r(const RArgs &a, int grid, hipStream_t st) {
     hipLaunchKernelGGL((k_screen_r<NC>), dim3(grid), dim3(256), RSmem::total, st, a);
     return hipGetLastError();
 }
+
+#ifdef RS_CLOCKS
+}  // namespace lira
+// slots: 0 item prologue, 1 first tile setup, 2 thresholds, 3 MFMA loop (+ its loads' waits),
+// 4 pass masks, 5 survivor queue (+ drains), 6 epilogue, 7 items; 8 tiles, 9 skipped tiles, 10 waves
+extern "C" int lira_debug_rs_clocks(unsigned long long *out16) {
+    hipDeviceSynchronize();
+    hipMemcpyFromSymbol(out16, HIP_SYMBOL(lira::g_rs_clk), 16 * 8);
+    unsigned long long z[16] = {0};
+    hipMemcpyToSymbol(HIP_SYMBOL(lira::g_rs_clk), z, 16 * 8);
+    return 0;
+}
+namespace lira {
+#endif
 
 hipError_t launch_rscreen(const RArgs &a, int grid, hipStream_t st) {
     switch (a.dpad / 32) {

@@ -209,23 +209,40 @@ __device__ __forceinline__ void plan_body(const int32_t *cnt, const int32_t *til
     // finds its partition by a binary search over the LDS prefix sums): one
     // thread per partition writing its items in turn serialised ~30 stores
     // per thread (SIFT1M: k_plan 26 -> ~8 us).
-    __shared__ int32_t s_g[1024];
+    // Two groups: each queue first holds chunk 0 of its group-0 partitions (every
+    // query block's nearest-partition items that start the bound chain), then
+    // the rest in partition order.  The ~2 items per workgroup that start at
+    // once run on the seed's bound; the later group-0 chunks start from the
+    // bounds the chunk-0 items published (k-th of a chunk instead of k-th of
+    // 128 seed rows): the nearest partition's survivors are most of the screen's
+    // selection work (SIFT1M latent: 79 % of them on 14 % of the tiles).
+    // Slots per queue: m0 chunk-0 slots, then m partition slots; s_d = the
+    // slot's first chunk.
+    __shared__ int32_t s_g[1024], s_d[1024];
     __syncthreads();
     const int m = (n_virt + 7) / 8;
+    const bool two = n_virt > n_lists;
+    const int m0 = two ? (n_lists + 7) / 8 : 0, M = m0 + m;
     if (threadIdx.x == 0) carry_b = 0;
     __syncthreads();
-    for (int base = 0; base < 8 * m; base += 1024) {
+    for (int base = 0; base < 8 * M; base += 1024) {
         const int vv = base + threadIdx.x;
-        const int v = vv < 8 * m ? (vv % m) * 8 + vv / m : n_virt;
-        int items = 0, nqb = 0, nc = 0;
+        const int r = vv / M, j = vv % M;
+        const bool first = j < m0;  // a chunk-0 slot
+        int v = vv < 8 * M ? (first ? j : j - m0) * 8 + r : n_virt;
+        if (first && v >= n_lists) v = n_virt;
+        int items = 0, nqb = 0, nc = 0, c0 = 0;
         if (v < n_virt) {
             nc = nch[v];
             nqb = (cnt[v] + qr - 1) / qr;
-            items = nqb * nc;
+            const bool g0 = two && v < n_lists;
+            items = first ? (nc > 0 ? nqb : 0) : g0 ? nqb * max(0, nc - 1) : nqb * nc;
+            c0 = !first && g0 ? 1 : 0;
         }
         s_b[threadIdx.x] = items;
         s_a[threadIdx.x] = v;
         s_c[threadIdx.x] = nqb;
+        s_d[threadIdx.x] = c0;
         s_g[threadIdx.x] = v < n_virt ? qblk_off[v] : 0;
         __syncthreads();
         for (int off = 1; off < 1024; off <<= 1) {
@@ -235,7 +252,7 @@ __device__ __forceinline__ void plan_body(const int32_t *cnt, const int32_t *til
             __syncthreads();
         }
         const int i0 = carry_b + s_b[threadIdx.x] - items;
-        if (vv < 8 * m && vv % m == 0) head[10 + vv / m] = i0;
+        if (vv < 8 * M && j == 0) head[10 + r] = i0;
         const int total = s_b[1023];
         for (int i = threadIdx.x; i < total; i += 1024) {
             int lo = 0, hi = 1023;  // first slot whose inclusive prefix exceeds i
@@ -244,8 +261,8 @@ __device__ __forceinline__ void plan_body(const int32_t *cnt, const int32_t *til
                 if (s_b[mid] > i) hi = mid; else lo = mid + 1;
             }
             const int local = i - (lo ? s_b[lo - 1] : 0), nq_b = s_c[lo];
-            const int ch = local / nq_b, qb = local - ch * nq_b;
-            itab[carry_b + i] = make_int4(s_a[lo], qb, ch, s_g[lo] + qb);
+            const int cl = local / nq_b, qb = local - cl * nq_b;
+            itab[carry_b + i] = make_int4(s_a[lo], qb, s_d[lo] + cl, s_g[lo] + qb);
         }
         __syncthreads();
         if (threadIdx.x == 1023) carry_b += s_b[1023];
