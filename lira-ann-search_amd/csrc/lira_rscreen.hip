@@ -67,8 +67,7 @@ struct RSmem {
     static constexpr int lock = erun + kRQ * 4;                      // [64] int
     static constexpr int opub = lock + kRQ * 4;                      // [64] uint: bound last published
     static constexpr int oqk = opub + kRQ * 4;                       // [4][kROCap] u64: survivor queue keys
-    static constexpr int oqr = oqk + kRW * kROCap * 8;               // [4][kROCap] u8: their rows
-    static constexpr int kth = oqr + kRW * kROCap;                   // [64] u64: each list's k-th key
+    static constexpr int kth = oqk + kRW * kROCap * 8;               // [64] u64: each list's k-th key
     static constexpr int meta = kth + kRQ * 8;                       // [16] int
     static constexpr int total = meta + 64;
 };
@@ -138,7 +137,7 @@ __device__ __forceinline__ u64 wkey_to_key(u64 wk, float qn) {
 __device__ __forceinline__ void flush_row(u64 *lists, u64 *kth_s, const u64 *mybuf, int *lock_s, uint32_t *erun_s,
                                        uint32_t *opub_s, const int *pair_s, int row, int n, int ew_bits, int k,
                                        uint32_t *qbound, int nprobe, float gP, float qn_row) {
-    const int lane = lane_id(), hl = lane & 31;
+    const int lane = opaque(lane_id()), hl = lane & 31;  // (opaque: addresses computed here, not hoisted)
 #ifdef RS_CLOCKS
     if (lane == 0) atomicAdd(&g_rs_clk[12], 1ull);
 #endif
@@ -169,13 +168,13 @@ __device__ __forceinline__ void flush_row(u64 *lists, u64 *kth_s, const u64 *myb
 }
 
 // Merge this wave's full row buffers into the lists, then move the survivor
-// queue (raw fl(-xadj + dot) bits, position; row) into the buffers (LDS atomic
-// slots), merging every buffer that fills, until the queue is empty.
+// queue into the buffers (LDS atomic slots), merging every buffer that fills,
+// until the queue is empty.
 __device__ __forceinline__ void drain_buffers(u64 *lists, u64 *kth_s, u64 *mybuf, int *mybufc, int *lock_s,
                                            uint32_t *erun_s, uint32_t *opub_s, const int *pair_s,
-                                           const float4 *rec_s, const u64 *oq_key, const uint8_t *oq_row, int nq,
+                                           const float4 *rec_s, const u64 *oq_key, uint32_t pos_base, int nq,
                                            float Ew, int k, uint32_t *qbound, int nprobe, float gP) {
-    const int lane = lane_id();
+    const int lane = opaque(lane_id());
     auto flush_full = [&]() {
         u64 full = __ballot(mybufc[lane] >= kRBC);  // lane = row
         while (full) {
@@ -191,12 +190,11 @@ __device__ __forceinline__ void drain_buffers(u64 *lists, u64 *kth_s, u64 *mybuf
     for (int e0 = 0; e0 < nq; e0 += 64) {
         const int e = e0 + lane;
         bool pend = e < nq;
-        const int row = pend ? oq_row[e] : 0;
-        u64 key = kEmptyKey;
-        if (pend) {  // (the queue holds fl(-xadj + dot) raw: the selection does no conversion)
-            const u64 q = oq_key[e];
-            key = wkey(__uint_as_float((uint32_t)(q >> 32)), (uint32_t)q);
-        }
+        // (queue entry: fl(-xadj + dot) bits | row << 16 | the candidate's position in
+        // the item; the selection does no conversion)
+        const u64 q = pend ? oq_key[e] : 0ull;
+        const int row = (int)((q >> 16) & 63u);
+        const u64 key = pend ? wkey(__uint_as_float((uint32_t)(q >> 32)), pos_base + (uint32_t)(q & 0xffffu)) : kEmptyKey;
         while (__any(pend)) {
             if (pend) {
                 const int slot = atomicAdd(mybufc + row, 1);
@@ -242,7 +240,6 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
     int *mybufc = bufc + wave * kRQ;
     float *myh = hs + wave * kRQ;
     u64 *oq_key = (u64 *)(smem + RSmem::oqk) + wave * kROCap;
-    uint8_t *oq_row = (uint8_t *)(smem + RSmem::oqr) + wave * kROCap;
     const bool TRI = a.tstat != nullptr;
     // B fragment: the lane's byte offset inside a tile's 32-dim chunk
     const uint32_t lane_off = (uint32_t)((g >> 1) * 4096 + (g & 1) * 1024 + cj * 16);
@@ -254,30 +251,30 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
 #endif
 
     const int bpc_near_d = __builtin_amdgcn_readfirstlane(a.head[19]);
-    int qx = 0, qtries = 0, nxt = -1;
-    int4 e_nxt = make_int4(0, 0, 0, 0);
-    if (tid == 0) {
-        for (int r = 0; r < 9; ++r) xq[r] = a.head[10 + r];
+    // Items are claimed by the last wave's lane 0 (its tiles are u = 3, 7, ...: the
+    // fewest when the item's tile count is not a multiple of 4), right after its
+    // tile loop: the claim's atomic and the entry's load overlap the other waves'
+    // last tiles instead of holding every wave at the item's first barrier
+    int qx = 0, qtries = 0;
+    auto claim_into_meta = [&]() {
+        const int it = claim_item(a.head, xq, qx, qtries);
+        const int4 e = it >= 0 ? a.itab[it] : make_int4(0, 0, 0, 0);
+        meta[0] = it >= 0;
+        meta[1] = e.x;
+        meta[2] = e.y;
+        meta[3] = e.z;
+        meta[4] = 0;  // the item's max tile radius / hi residual (bits), max-reduced in its prologue
+        meta[5] = 0;
+    };
+    if (tid < 9) xq[tid] = a.head[10 + tid];
+    __syncthreads();
+    if (wave == kRW - 1 && lane == 0) {
         qx = xcd_id();
-        nxt = claim_item(a.head, xq, qx, qtries);
-        if (nxt >= 0) e_nxt = a.itab[nxt];
+        claim_into_meta();
     }
+    __syncthreads();
     for (;;) {
         RCLK(t_item);
-        if (tid == 0) {  // the next item claimed, and its entry loaded, one item ahead
-            const int item = nxt, ok = item >= 0;
-            int4 e = make_int4(0, 0, 0, 0);
-            if (ok) {
-                e = e_nxt;
-                nxt = claim_item(a.head, xq, qx, qtries);
-                if (nxt >= 0) e_nxt = a.itab[nxt];
-            }
-            meta[0] = ok;
-            meta[1] = e.x;
-            meta[2] = e.y;
-            meta[3] = e.z;
-        }
-        __syncthreads();
         if (!meta[0]) break;
         const int vp = __builtin_amdgcn_readfirstlane(meta[1]);
         const int qb = __builtin_amdgcn_readfirstlane(meta[2]);
@@ -290,6 +287,25 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
         const int nt = min(ntl, tb_begin + bpc * 4) - tb_begin;  // the item's tiles (<= kRMaxTiles)
         const int tbase = tile0 + tb_begin;
         const float R = a.rmax[p];
+        int u = wave;
+        // B operands: a ring of RS chunks of [candidate group]; chunk s (of the
+        // wave's chunk sequence: tile after tile) sits in slot s mod RS, and its
+        // slot is reloaded with chunk s + RS as soon as its MFMAs have issued
+        // (RS = NC: the next tile's chunk; RS = 2 at d = 128: two chunks ahead,
+        // 32 VGPRs instead of 64).  The wave's first tile is requested before the
+        // prologue (under its loads and barriers), and again only if skipped.
+        constexpr int RS = NC % 2 == 0 && NC >= 4 ? 2 : NC;
+        rbf16x8 B[RS][4];
+        rf4 xa_n = (rf4)(0.0f);  // the next tile's xadj (candidates 4 cj .. + 3)
+        auto load_first = [&]() {
+            const char *base = a.Xb + (int64_t)(tbase + u) * tile_bytes + lane_off;
+#pragma unroll
+            for (int c = 0; c < RS; ++c)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) B[c][i] = *(const rbf16x8 *)(base + c * 8192 + i * 256);
+            xa_n = *(const rf4 *)(a.xadj + (int64_t)(tbase + u) * 64 + 4 * cj);
+        };
+        if (u < nt) load_first();
 
         // ---- item prologue: row records, lists, tile statistics
         const int nval = a.cnt[vp] - qb * kRQ;
@@ -297,6 +313,7 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
         const float4 qrec = my_pair >= 0 ? a.QN[my_pair] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         const float my_qres = my_pair >= 0 ? a.QE[my_pair] : 0.0f;
         const int my_q = my_pair >= 0 ? my_pair / a.nprobe : -1;
+        __syncthreads();  // (the previous item's epilogue is done with the LDS state)
         if (wave == 0) {
             pair_s[lane] = my_pair;
             rec_s[lane] = make_float4(qrec.x, qrec.y, my_qres, qrec.w);
@@ -311,11 +328,21 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
             const uint4 e4 = make_uint4(~0u, ~0u, ~0u, ~0u);
             for (int i = tid; i < kRQ * kRK2 / 2; i += 256) l4[i] = e4;
         }
-        if (TRI)
+        if (TRI) {
+            float rb = 0.0f, hr = 0.0f;
             for (int i = tid; i < nt; i += 256) {
-                tst[i] = a.tstat[tbase + i];
-                trs[i] = a.tres ? a.tres[tbase + i] : -1.0f;
+                const float2 t2 = a.tstat[tbase + i];
+                tst[i] = t2;
+                rb = fmaxf(rb, t2.y);
+                if (a.tres) {
+                    const float tr = a.tres[tbase + i];
+                    trs[i] = tr;
+                    hr = fmaxf(hr, tr);
+                }
             }
+            atomicMax((uint32_t *)meta + 4, __float_as_uint(rb));  // (>= 0: ordered as integers)
+            if (a.tres) atomicMax((uint32_t *)meta + 5, __float_as_uint(hr));
+        }
         __syncthreads();
 
         // A operands into LDS, in fragment order: [chunk c][row group rg][lane (g, j)]
@@ -334,7 +361,13 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
         const uint32_t *pub_at = a.qbound + (my_q >= 0 ? my_q : 0);  // (a padding row reads query 0's: unused)
         uint32_t pub = __hip_atomic_load(pub_at, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         float Tc = -1.0f, Ac = __builtin_inff(), triA = -__builtin_inff(), triB = __builtin_inff();
-        float Ew = 0.0f;  // the largest error bound of the tiles this wave screened (lane = row)
+        // The screening error bound is the item's (its largest tile radius and hi
+        // residual: err_E is monotone in both), so a row's threshold changes only
+        // when its T does; Ew = the bound of every key this item lists (lane = row)
+        const float Rb_item = TRI ? fminf(R, rup(__uint_as_float((uint32_t)meta[4]))) : R;
+        const float hres_item = TRI && a.tres ? __uint_as_float((uint32_t)meta[5]) : -1.0f;
+        const float Ew = my_pair >= 0 ? errE_r(my_qnorm, Rb_item, hres_item, my_qres, dp) : 0.0f;
+        const int g4 = opaque(4 * g);  // (selection rows: 16 rg + g4 + reg)
         // T: the row's bound on its final k-th exact score (shared list, published bound).
         // No divergent branch (the published bound's load stays countable for the
         // compiler's waits: a conditional one cost a vmcnt(0) per tile)
@@ -353,6 +386,19 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
                 const float rad = rup(__builtin_amdgcn_sqrtf(Ac));
                 triA = my_pair < 0 ? __builtin_inff() : fin ? rdn(rdn(my_dq) - rad) : -__builtin_inff();
                 triB = my_pair < 0 ? -__builtin_inff() : fin ? rup(rup(my_dq) + rad) : __builtin_inff();
+                // pass iff fl(-xadj + dot) >= h (lane = row), then the rows in selection order
+                float h = __builtin_inff();
+                if (my_pair >= 0) {
+                    h = -__builtin_inff();
+                    if (fin) {
+                        const float lim = rup(Ac + Ew), sq = my_qnorm + Rb_item;
+                        h = rdn(0.5f * (my_qn - lim) - (__builtin_fabsf(my_qn) + __builtin_fabsf(lim)) * 0x1p-22f -
+                                1.06f * 0x1p-24f * sq * sq);
+                    }
+                    h = fmaxf(h, -3.40282347e38f);  // (padding, xadj = +inf, never passes)
+                }
+                myh[lane] = h;
+                __builtin_amdgcn_wave_barrier();
             }
         };
         // tile u is needed by no row (wave-uniform)
@@ -362,29 +408,15 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
             return __all(r.y < triA || r.x > triB) != 0;
         };
 
-        int u = wave;
         RCLK(t_pro);
         RACC(0, t_item, t_pro);
         update_T();
-        while (u < nt && skip(u)) {
-            ++n_skip;
-            u += kRW;
-        }
-        // B operands: a ring of RS chunks of [candidate group]; chunk s (of the
-        // wave's chunk sequence: tile after tile) sits in slot s mod RS, and its
-        // slot is reloaded with chunk s + RS as soon as its MFMAs have issued
-        // (RS = NC: the next tile's chunk; RS = 2 at d = 128: two chunks ahead,
-        // 32 VGPRs instead of 64)
-        constexpr int RS = NC % 2 == 0 && NC >= 4 ? 2 : NC;
-        rbf16x8 B[RS][4];
-        rf4 xa_n = (rf4)(0.0f);  // the next tile's xadj (candidates 4 cj .. + 3)
-        if (u < nt) {
-            const char *base = a.Xb + (int64_t)(tbase + u) * tile_bytes + lane_off;
-#pragma unroll
-            for (int c = 0; c < RS; ++c)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) B[c][i] = *(const rbf16x8 *)(base + c * 8192 + i * 256);
-            xa_n = *(const rf4 *)(a.xadj + (int64_t)(tbase + u) * 64 + 4 * cj);
+        if (u < nt && skip(u)) {
+            do {
+                ++n_skip;
+                u += kRW;
+            } while (u < nt && skip(u));
+            if (u < nt) load_first();
         }
         int ovf = 0;  // survivor queue fill (wave-uniform)
         // survivor queue -> this wave's row buffers (full ones merged into the lists)
@@ -393,8 +425,8 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
             ovf = 0;
             return;
 #endif
-            drain_buffers(lists, kth_s, mybuf, mybufc, lock_s, erun_s, opub_s, pair_s, rec_s, oq_key, oq_row, ovf, Ew,
-                          k, a.qbound, a.nprobe, a.gP);
+            drain_buffers(lists, kth_s, mybuf, mybufc, lock_s, erun_s, opub_s, pair_s, rec_s, oq_key,
+                          (uint32_t)tbase * 64u, ovf, Ew, k, a.qbound, a.nprobe, a.gP);
             ovf = 0;
         };
 
@@ -403,26 +435,8 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
         while (u < nt) {
             RCLK(t_a);
             const rf4 xa = xa_n;
-            // ---- thresholds for tile u (lane = row), then each lane's 16 rows
+            // ---- the row bounds (thresholds rewritten where one changed)
             update_T();
-            {
-                float h = __builtin_inff();
-                if (my_pair >= 0) {
-                    const float2 r = TRI ? tst[u] : make_float2(0.0f, R);
-                    const float Rb = TRI ? fminf(R, rup(r.y)) : R;
-                    const float Eb = errE_r(my_qnorm, Rb, TRI ? trs[u] : -1.0f, my_qres, dp);
-                    Ew = fmaxf(Ew, Eb);
-                    h = -__builtin_inff();
-                    if (Ac < 3e38f) {
-                        const float lim = rup(Ac + Eb), s = my_qnorm + Rb;
-                        h = rdn(0.5f * (my_qn - lim) - (__builtin_fabsf(my_qn) + __builtin_fabsf(lim)) * 0x1p-22f -
-                                1.06f * 0x1p-24f * s * s);
-                    }
-                    h = fmaxf(h, -3.40282347e38f);  // (padding, xadj = +inf, never passes)
-                }
-                myh[lane] = h;
-            }
-            __builtin_amdgcn_wave_barrier();
 
             // ---- the next tile of this wave (skip test with the current intervals)
             int un = u + kRW;
@@ -439,7 +453,6 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
 #endif
             xa_n = *(const rf4 *)(a.xadj + (int64_t)(tbase + ul) * 64 + 4 * cj);
             // the rows' thresholds in selection order (read under the MFMAs)
-            const int g4 = opaque(4 * g);  // (row = 16 rg + g4 + reg)
             rf4 hv[4];
 #pragma unroll
             for (int rg = 0; rg < 4; ++rg) hv[rg] = *(const rf4 *)(myh + 16 * rg + g4);
@@ -487,7 +500,7 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
             // a mask that would overflow the queue draining it first
             RCLK(t_d);
             RACC(4, t_c, t_d);
-            const uint32_t pos0 = (uint32_t)((tbase + u) * 64) + (uint32_t)(4 * cj);
+            const uint32_t lpos0 = (uint32_t)(u * 64 + 4 * cj);
             // The pass runs over (entry, half) steps h = 2 e + (i >> 1); a step that
             // would overflow the queue stops it there, the queue is drained (one
             // inlined call site) and the pass resumes at that step (rare)
@@ -498,6 +511,9 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
                 for (int rg = 0; rg < 4; ++rg)
 #pragma unroll
                     for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(acc[rg][i]));
+                // (likewise the entries' low words: row << 16 | position, from one value
+                // per pass -- hoisted, the 32 precomputed words were spilled)
+                const uint32_t low0 = (uint32_t)opaque((int)(((uint32_t)g4 << 16) | lpos0));
                 int stop = 32;
 #pragma unroll
                 for (int rg = 0; rg < 4; ++rg) {
@@ -513,13 +529,13 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
 #ifdef RS_CLOCKS
                         clk[7] += 1ull << 32;  // (entries with survivors, high half)
 #endif
-                        const uint8_t row = (uint8_t)(16 * rg + g4 + reg);
+                        const uint32_t low = low0 + ((uint32_t)(16 * rg + reg) << 16);
 #pragma unroll
                         for (int hf = 0; hf < 2; ++hf) {
                             const int h = 2 * e + hf;
                             if (h < s0 || h >= stop) continue;
                             const u64 ma = m[2 * hf], mb = m[2 * hf + 1];
-                            const int n = popc64(ma) + popc64(mb);
+                            const int na = popc64(ma), n = na + popc64(mb);
                             if (!n) continue;
                             if (ovf + n > kROCap) {  // (n <= 128: fits once drained)
                                 stop = h;
@@ -532,16 +548,12 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
 #ifdef RS_NOSURV  // timing experiment: survivors dropped (results invalid)
                             continue;
 #endif
-                            if ((ma >> lane) & 1ull) {
-                                const int slot = ovf + mbcnt64(ma);
-                                oq_key[slot] = ((u64)__float_as_uint(acc[rg][2 * hf][reg]) << 32) | (pos0 + 2u * hf);
-                                oq_row[slot] = row;
-                            }
-                            if ((mb >> lane) & 1ull) {
-                                const int slot = ovf + popc64(ma) + mbcnt64(mb);
-                                oq_key[slot] = ((u64)__float_as_uint(acc[rg][2 * hf + 1][reg]) << 32) | (pos0 + 2u * hf + 1u);
-                                oq_row[slot] = row;
-                            }
+                            // queue entry: fl(-xadj + dot) bits | row << 16 | position in the item
+                            if ((ma >> lane) & 1ull)
+                                oq_key[ovf + mbcnt64(ma)] = ((u64)__float_as_uint(acc[rg][2 * hf][reg]) << 32) | (low + 2u * hf);
+                            if ((mb >> lane) & 1ull)
+                                oq_key[ovf + na + mbcnt64(mb)] =
+                                    ((u64)__float_as_uint(acc[rg][2 * hf + 1][reg]) << 32) | (low + 2u * hf + 1u);
                             ovf += n;
                         }
                     }
@@ -558,6 +570,7 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
             u = un;
         }
         if (ovf) drain();
+        if (wave == kRW - 1 && lane == 0) claim_into_meta();  // (the next item; read after the barriers below)
         RCLK(t_epi);
 
         // ---- item epilogue: every wave's buffers into the lists (rows split over
@@ -591,11 +604,16 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
             }
         }
         __syncthreads();
+        // (sorted lists: the keys, the first empty one and the last slot are all
+        // k_smerge reads -- its walk stops at the first key beyond its limit)
 #pragma unroll 1
         for (int j = 0; j < 16; j += 2) {
             const int hl = ln & 31, row = wave * 16 + j + (ln >> 5);
             const int pr = pair_s[row];
-            if (pr >= 0) a.partial[((int64_t)pr * a.nch_max + ch) * kRK2 + hl] = lists[row * kRK2 + hl];
+            const u64 key = lists[row * kRK2 + hl];
+            const u64 full = __ballot(key != kEmptyKey);
+            const int nv = __builtin_popcount((uint32_t)(ln >> 5 ? full >> 32 : full));
+            if (pr >= 0 && (hl <= nv || hl == kRK2 - 1)) a.partial[((int64_t)pr * a.nch_max + ch) * kRK2 + hl] = key;
         }
         if (my_pair >= 0) {
             const float er = __uint_as_float(erun_s[lane]);
@@ -604,7 +622,6 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
             if (a.qbound && kk != kEmptyKey)
                 atomicMin(a.qbound + my_q, f2ord(rup(rup(key_score(kk) + er) * a.gP) + 0x1p-125f));
         }
-        __syncthreads();
         RCLK(t_end);
         RACC(6, t_epi, t_end);
 #ifdef RS_CLOCKS

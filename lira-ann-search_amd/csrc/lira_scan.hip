@@ -112,7 +112,7 @@ __global__ __launch_bounds__(256) void k_count(const int32_t *probe, int64_t npa
 // query blocks ceil(cnt / qr) per virtual partition.
 // (blockDim.x == 1024; plan_body is also block 0's share of k_plan_fill)
 // bpc_near_min < bpc_near (two groups): group 0's chunk size is chosen here, in
-// [bpc_near_min, bpc_near], as about a quarter of a worker's share of the
+// [bpc_near_min, bpc_near], as about 1 / near_div of a worker's share of the
 // blocks the batch will screen -- the seed's per-pair estimates on every 8th
 // query, summed in head[64..127] (k_seed_t<..., PAIRS>: whole lists for slot 0, else the share
 // of the list's tiles inside the triangle interval), divided by the rows per
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256) void k_count(const int32_t *probe, int64_t npa
 __device__ __forceinline__ void plan_body(const int32_t *cnt, const int32_t *tile_off, int n_lists, int n_virt,
                                           int bpc, int bpc_near, int qr, int32_t *qoff, int32_t *item_off,
                                           int32_t *nch, int32_t *head, int32_t *qblk_off, int4 *itab,
-                                          int bpc_near_min, int workers) {
+                                          int bpc_near_min, int workers, int near_div) {
     __shared__ int32_t s_a[1024], s_b[1024], s_c[1024];
     __shared__ int32_t carry_a, carry_b, carry_c, s_nchmax;
     if (threadIdx.x == 0) carry_a = carry_b = carry_c = s_nchmax = 0;
@@ -138,7 +138,7 @@ __device__ __forceinline__ void plan_body(const int32_t *cnt, const int32_t *til
         __syncthreads();
         if (threadIdx.x == 0) {
             const long long per = (long long)(8ull * w / (unsigned long long)max(1, qr)) / max(1, workers);  // (1/8 sampled)
-            s_a[0] = (int)min<long long>(bpc_near, max<long long>(bpc_near_min, (per + 3) / 4));
+            s_a[0] = (int)min<long long>(bpc_near, max<long long>(bpc_near_min, (per + near_div - 1) / near_div));
         }
         __syncthreads();
         bpc_near = s_a[0];
@@ -274,9 +274,10 @@ __global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t
                                                int n_lists, int n_virt, int bpc, int bpc_near, int qr,
                                                int32_t *qoff,
                                                int32_t *item_off, int32_t *nch, int32_t *head,
-                                               int32_t *qblk_off, int4 *itab, int bpc_near_min, int workers) {
+                                               int32_t *qblk_off, int4 *itab, int bpc_near_min, int workers,
+                                               int near_div) {
     plan_body(cnt, tile_off, n_lists, n_virt, bpc, bpc_near, qr, qoff, item_off, nch, head, qblk_off, itab,
-              bpc_near_min, workers);
+              bpc_near_min, workers, near_div);
 }
 
 // bucket -> pair ids.  Each block reserves its slice of every bucket once
@@ -332,13 +333,13 @@ __global__ __launch_bounds__(1024) void k_plan_fill(const int32_t *probe, int64_
                                                     int bpc_near, int qr, int32_t *qoff, int32_t *item_off,
                                                     int32_t *nch, int32_t *head, int32_t *qblk_off, int4 *itab,
                                                     int32_t *cursor, int32_t *qlist, int bpc_near_min,
-                                                    int workers) {
+                                                    int workers, int near_div) {
     __shared__ int32_t sq[kFuseMax], hist[kFuseMax], base[kFuseMax], scan[1024];
     __shared__ int32_t carry;
     const int n_virt = groups * n_lists, tid = threadIdx.x;
     if (blockIdx.x == 0)
         plan_body(cnt, tile_off, n_lists, n_virt, bpc, bpc_near, qr, qoff, item_off, nch, head, qblk_off, itab,
-                  bpc_near_min, workers);
+                  bpc_near_min, workers, near_div);
     // exclusive prefix of cnt over the virtual partitions -> sq
     if (tid == 0) carry = 0;
     for (int b = tid; b < n_virt; b += 1024) hist[b] = 0;
@@ -1169,7 +1170,7 @@ static int exact_topk(lira_index *idx, const float *q, int64_t nq, const int32_t
     hipLaunchKernelGGL(k_count, dim3(pg), dim3(256), hc, st, probe, npairs, nl, (int)nprobe, split, groups,
                        cnt, idx->err);
     hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, nv, pl.bpc, pl.bpc, kQT, qoff,
-                       item_off, nch, head, (int32_t *)nullptr, (int4 *)nullptr, pl.bpc, 1);
+                       item_off, nch, head, (int32_t *)nullptr, (int4 *)nullptr, pl.bpc, 1, 4);
     hipLaunchKernelGGL(k_fill, dim3(pg), dim3(256), hf, st, probe, npairs, nl, (int)nprobe, split, groups,
                        qoff, cursor, qlist);
     LIRA_HIP_TRY(hipGetLastError());
@@ -1293,7 +1294,7 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
 hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npairs, int nprobe, int bpc,
                        int bpc_near, int qr, int groups, int32_t *cnt, int32_t *cursor, int32_t *qoff, int32_t *item_off,
                        int32_t *nch, int32_t *head, int32_t *qlist, int32_t *qblk_off, int4 *itab,
-                       hipStream_t st, int bpc_near_min, int workers) {
+                       hipStream_t st, int bpc_near_min, int workers, int near_div) {
     const int nl = (int)idx->n_lists, nv = groups * nl;
     const unsigned pg = (unsigned)((npairs + kPairsPerBlock - 1) / kPairsPerBlock);
     const size_t hc = nv <= kHistMax ? (size_t)nv * 4 : 0;
@@ -1302,11 +1303,11 @@ hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npai
     if (nv <= kFuseMax && qblk_off) {
         hipLaunchKernelGGL(k_plan_fill, dim3(std::max(pg, 1u)), dim3(1024), 0, st, probe, npairs, nl, nprobe, groups, cnt,
                            idx->tile_off, bpc, bpc_near, qr, qoff, item_off, nch, head, qblk_off, itab, cursor, qlist,
-                           bpc_near_min, workers);
+                           bpc_near_min, workers, near_div);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, nv, bpc, bpc_near, qr, qoff,
-                       item_off, nch, head, qblk_off, itab, bpc_near_min, workers);
+                       item_off, nch, head, qblk_off, itab, bpc_near_min, workers, near_div);
     hipLaunchKernelGGL(k_fill, dim3(pg), dim3(256), hf, st, probe, npairs, nl, nprobe, 1, groups, qoff, cursor,
                        qlist);
     return hipGetLastError();

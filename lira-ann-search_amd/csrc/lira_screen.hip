@@ -60,7 +60,7 @@ hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npai
                        int bpc_near,
                        int qr, int groups, int32_t *cnt, int32_t *cursor, int32_t *qoff, int32_t *item_off,
                        int32_t *nch, int32_t *head, int32_t *qlist, int32_t *qblk_off, int4 *itab,
-                       hipStream_t st, int bpc_near_min, int workers);
+                       hipStream_t st, int bpc_near_min, int workers, int near_div);
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -2063,7 +2063,11 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // merge than k_scan's 16 (measured: SIFT1M scan + merge 1.47 -> 1.22 ms on
     // the mixture, 4.80 -> 4.66 ms on latent data; 4 and 32 slower overall)
     const int workers = pl.grid;
-    const int rounds = op.rounds > 0 ? op.rounds : 8;
+    // (k_screen_r: 4.  Its waves take an item's tiles in turn and meet at the item's
+    // end, so longer items balance better: measured SIFT1M latent scan 0.80 ->
+    // 0.73 ms at rounds 4 with near_rounds 1, mixture 0.253 -> 0.240 ms with
+    // group 0's items at half instead of a quarter of a worker's share)
+    const int rounds = op.rounds > 0 ? op.rounds : pl.rs ? 4 : 8;
     const int64_t target = (int64_t)rounds * workers;
     // (LIRA_OPT_PROBES_HINT: the probe lists are mostly -1 padding, e.g. a
     // threshold selection padded to B; size the chunking for the expected pairs)
@@ -2081,7 +2085,7 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // per workgroup left the slowest workgroup with two (LIRA_OPT_NEAR_ROUNDS;
     // measured SIFT1M mixture scan 1.08 -> 1.04 ms at 2, slower at 4 and 8:
     // more lists, more survivors)
-    const int near_rounds = op.near_rounds > 0 ? op.near_rounds : 2;
+    const int near_rounds = op.near_rounds > 0 ? op.near_rounds : pl.rs ? 1 : 2;
     {
         const int64_t est0 = std::min<int64_t>(nq, (nq + pl.qr - 1) / pl.qr + idx->n_lists);
         const int64_t split0 = std::max<int64_t>(1, ((int64_t)near_rounds * workers + est0 - 1) / std::max<int64_t>(1, est0));
@@ -2096,7 +2100,7 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     }
     // k_screen_m + k_smerge with the default near_rounds: the plan picks group 0's
     // chunk size on the device (plan_body) from the seed's estimate of the blocks
-    // the batch will screen, down to 6 rounds' worth
+    // the batch will screen, down to 6 rounds' worth (k_screen_r: 3)
     pl.workers = (int)workers;
     pl.bpc_near_min = pl.bpc_near;
     // (screen_topk's two-group rule: group 0's chunks exist only then)
@@ -2105,7 +2109,7 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
                       nq * nprobe >= 4 * (int64_t)pl.qr * idx->n_lists);
     if (two && op.near_rounds <= 0 && pl.mfma) {
         const int64_t est0 = std::min<int64_t>(nq, (nq + pl.qr - 1) / pl.qr + idx->n_lists);
-        const int64_t split6 = std::max<int64_t>(1, (6 * (int64_t)workers + est0 - 1) / std::max<int64_t>(1, est0));
+        const int64_t split6 = std::max<int64_t>(1, ((pl.rs ? 3 : 6) * (int64_t)workers + est0 - 1) / std::max<int64_t>(1, est0));
         pl.bpc_near_min = (int)std::min<int64_t>(pl.bpc_near, std::max<int64_t>(1, (max_blocks + split6 - 1) / split6));
     }
     pl.nch_max = (int)((max_blocks + pl.bpc_near_min - 1) / pl.bpc_near_min);
@@ -2355,7 +2359,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     LIRA_HIP_TRY(launch_plan(idx, pprobe, npairs, (int)nprobe, pl.bpc, groups == 2 ? pl.bpc_near : pl.bpc, pl.qr, groups, cnt, cursor, qoff, item_off,
                              nch, head, qlist, qblk, itab, st,
                              groups == 2 && fused && idx->lsamp ? pl.bpc_near_min : (groups == 2 ? pl.bpc_near : pl.bpc),
-                             pl.workers));
+                             pl.workers, pl.rs ? 2 : 4));
     if (!pl.pp) {
     const dim3 qgrid((unsigned)pl.max_qblk, (unsigned)((idx->dpad + 64 * kQSlabs - 1) / (64 * kQSlabs)));
     if (pl.qr == 128 && pl.split)
