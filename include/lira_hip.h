@@ -169,6 +169,11 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *                        centred split copy with the hi x hi screen, k <= 24, dpad <= 128, the
  *                        per-query seed on, not PER_PARTITION): query rows' hi parts in LDS, each
  *                        wave streaming its own candidate tiles into registers; 0: k_screen_m
+ *   LIRA_OPT_NEAR_FIRST  (k_screen_r) blocks of 256 candidates in the first chunk of every query
+ *                        block's nearest partition: -1 (default) 2; 0: chunks of one size.  Those
+ *                        small first chunks are queued first; the query block's later chunks wait
+ *                        for its first one, so they start from the bounds it published instead of
+ *                        the 128-row seed's.  Results never depend on it.
  */
 #define LIRA_OPT_KEEP_TILES 1
 #define LIRA_OPT_SCREEN 2
@@ -189,6 +194,7 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
 #define LIRA_OPT_ORDER 17
 #define LIRA_OPT_WIDE 18
 #define LIRA_OPT_RSCREEN 19
+#define LIRA_OPT_NEAR_FIRST 20
 int lira_index_set_option(lira_index *idx, int option, int64_t value);
 int lira_index_get_option(const lira_index *idx, int option, int64_t *value);
 /* 1 if the index holds the fp32 tile copy (LIRA_OPT_KEEP_TILES at build time) */

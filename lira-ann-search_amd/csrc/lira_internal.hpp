@@ -52,6 +52,7 @@ struct lira_opts {
     int xhi = -1;
     int order = 1;
     int rscreen = 1;
+    int near_first = -1;  // LIRA_OPT_NEAR_FIRST (-1: the default, 2 blocks)
 };
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device):

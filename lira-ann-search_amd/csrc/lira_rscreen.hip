@@ -263,6 +263,7 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
         meta[1] = e.x;
         meta[2] = e.y;
         meta[3] = e.z;
+        meta[6] = e.w;  // (the query block's index over all buckets)
         meta[4] = 0;  // the item's max tile radius / hi residual (bits), max-reduced in its prologue
         meta[5] = 0;
     };
@@ -282,9 +283,15 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
         const int p = vp >= a.n_lists ? vp - a.n_lists : vp;
         const int tile0 = __builtin_amdgcn_readfirstlane(a.tile_off[p]);
         const int ntl = __builtin_amdgcn_readfirstlane(a.tile_off[p + 1]) - tile0;
-        const int bpc = vp < a.n_lists && a.n_virt > a.n_lists ? bpc_near_d : a.bpc;
-        const int tb_begin = ch * bpc * 4;
-        const int nt = min(ntl, tb_begin + bpc * 4) - tb_begin;  // the item's tiles (<= kRMaxTiles)
+        // chunk ch of the bucket: group 0 (each query's nearest partition) has a
+        // first chunk of head[21] blocks, then chunks of head[19]; the others a.bpc
+        const bool g0 = vp < a.n_lists && a.n_virt > a.n_lists;
+        const int b0 = __builtin_amdgcn_readfirstlane(a.head[21]);
+        const int blk0 = g0 ? (ch == 0 ? 0 : b0 + (ch - 1) * bpc_near_d) : ch * a.bpc;
+        const int nbk = g0 ? (ch == 0 ? b0 : bpc_near_d) : a.bpc;
+        const int tb_begin = blk0 * 4;
+        const int nt = min(ntl, tb_begin + nbk * 4) - tb_begin;  // the item's tiles (<= kRMaxTiles)
+        const int qblk = __builtin_amdgcn_readfirstlane(meta[6]);
         const int tbase = tile0 + tb_begin;
         const float R = a.rmax[p];
         int u = wave;
@@ -313,6 +320,14 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
         const float4 qrec = my_pair >= 0 ? a.QN[my_pair] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         const float my_qres = my_pair >= 0 ? a.QE[my_pair] : 0.0f;
         const int my_q = my_pair >= 0 ? my_pair / a.nprobe : -1;
+        // a later chunk of a nearest partition waits for the query block's first
+        // chunk, whose epilogue publishes the rows' bounds (queued ahead of it in
+        // the same queue, so it is claimed and running: no wait can deadlock).  The
+        // bounds are hints -- a stale or missing one is only looser -- so the wait
+        // is also bounded (~2^14 polls).  Polls and the flag are atomics: they act
+        // at the memory side, past the XCDs' non-coherent L2s.
+        if (g0 && ch > 0 && a.done0 && tid == 0)
+            for (int it = 0; it < (1 << 14) && atomicAdd(a.done0 + qblk, 0) == 0; ++it) __builtin_amdgcn_s_sleep(8);
         __syncthreads();  // (the previous item's epilogue is done with the LDS state)
         if (wave == 0) {
             pair_s[lane] = my_pair;
@@ -478,8 +493,12 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
                     const rf4 cx = (rf4)(-xa[i]);
 #pragma unroll
                     for (int rg = 0; rg < 4; ++rg)
+#ifdef RS_NOMFMA  // timing experiment: no MFMAs (results invalid)
+                        acc[rg][i] = c == 0 ? cx : acc[rg][i] + (rf4)((float)Acur[rg][0] * (float)B[sl][i][0] * 0.0f);
+#else
                         acc[rg][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Acur[rg], B[sl][i], c == 0 ? cx : acc[rg][i],
                                                                              0, 0, 0);
+#endif
                     B[sl][i] = cn < NC ? *(const rbf16x8 *)(cbase + cn * 8192 + i * 256)
                                        : *(const rbf16x8 *)(nbase + (cn - NC) * 8192 + i * 256);
                 }
@@ -504,6 +523,16 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
             // The pass runs over (entry, half) steps h = 2 e + (i >> 1); a step that
             // would overflow the queue stops it there, the queue is drained (one
             // inlined call site) and the pass resumes at that step (rare)
+#ifdef RS_NOSEL  // timing experiment: no selection (results invalid)
+            if (__builtin_amdgcn_readfirstlane(lane) == 0) {
+                float z = 0.0f;
+#pragma unroll
+                for (int rg = 0; rg < 4; ++rg)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) z += acc[rg][i][0];
+                if (z == 12345.0f) n_surv += 1;
+            } else
+#endif
             for (int s0 = 0;;) {
                 // (the accumulators as if redefined: keeps the compares from being
                 // hoisted out of this loop, which cost 64 masks held in SGPRs)
@@ -621,6 +650,11 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
             const u64 kk = lists[lane * kRK2 + k - 1];
             if (a.qbound && kk != kEmptyKey)
                 atomicMin(a.qbound + my_q, f2ord(rup(rup(key_score(kk) + er) * a.gP) + 0x1p-125f));
+        }
+        if (g0 && ch == 0 && a.done0) {  // the query block's later chunks may start
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this wave's published bounds landed)
+            __syncthreads();
+            if (tid == 0) atomicAdd(a.done0 + qblk, 1);
         }
         RCLK(t_end);
         RACC(6, t_epi, t_end);

@@ -25,6 +25,7 @@ struct RArgs {
     float gP;                // >= 1 + (d + 4) 2^-24 (bound_P's factor, rounded up)
     float invF;              // >= 1 / (1 - (d + 4) 2^-24) (s_lim's factor, rounded up)
     unsigned long long *stats;
+    int32_t *done0;          // per query block: its nearest partition's first chunk is done (NULL: no waits)
 };
 
 // the shapes k_screen_r implements: L2 on the centred split copy, hi x hi,

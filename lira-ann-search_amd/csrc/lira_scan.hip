@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256) void k_count(const int32_t *probe, int64_t npa
 __device__ __forceinline__ void plan_body(const int32_t *cnt, const int32_t *tile_off, int n_lists, int n_virt,
                                           int bpc, int bpc_near, int qr, int32_t *qoff, int32_t *item_off,
                                           int32_t *nch, int32_t *head, int32_t *qblk_off, int4 *itab,
-                                          int bpc_near_min, int workers, int near_div) {
+                                          int bpc_near_min, int workers, int near_div, int near0) {
     __shared__ int32_t s_a[1024], s_b[1024], s_c[1024];
     __shared__ int32_t carry_a, carry_b, carry_c, s_nchmax;
     if (threadIdx.x == 0) carry_a = carry_b = carry_c = s_nchmax = 0;
@@ -144,7 +144,12 @@ __device__ __forceinline__ void plan_body(const int32_t *cnt, const int32_t *til
         bpc_near = s_a[0];
         __syncthreads();
     }
-    if (threadIdx.x == 0) head[19] = bpc_near;
+    // near0 > 0 (two groups): group 0's first chunk is near0 blocks, the rest
+    // bpc_near; head[21] = the first chunk's size (= bpc_near when uniform)
+    if (threadIdx.x == 0) {
+        head[19] = bpc_near;
+        head[21] = near0 > 0 && n_virt > n_lists ? near0 : bpc_near;
+    }
     __syncthreads();
     for (int base = 0; base < n_virt; base += 1024) {
         int p = base + threadIdx.x;
@@ -154,8 +159,10 @@ __device__ __forceinline__ void plan_body(const int32_t *cnt, const int32_t *til
             const int pp = p >= n_lists ? p - n_lists : p;
             int ntl = tile_off[pp + 1] - tile_off[pp];
             int nblk = (ntl + kBlockTiles - 1) / kBlockTiles;
-            const int b = n_virt > n_lists && p < n_lists ? bpc_near : bpc;  // group 0: bpc_near
+            const bool g0 = n_virt > n_lists && p < n_lists;
+            const int b = g0 ? bpc_near : bpc;  // group 0: bpc_near
             int nc = (nblk + b - 1) / b;
+            if (g0 && near0 > 0) nc = nblk <= 0 ? 0 : nblk <= near0 ? 1 : 1 + (nblk - near0 + bpc_near - 1) / bpc_near;
             nch[p] = nc;
             nqb = (c + qr - 1) / qr;
             items = nqb * nc;
@@ -275,9 +282,9 @@ __global__ __launch_bounds__(1024) void k_plan(const int32_t *cnt, const int32_t
                                                int32_t *qoff,
                                                int32_t *item_off, int32_t *nch, int32_t *head,
                                                int32_t *qblk_off, int4 *itab, int bpc_near_min, int workers,
-                                               int near_div) {
+                                               int near_div, int near0) {
     plan_body(cnt, tile_off, n_lists, n_virt, bpc, bpc_near, qr, qoff, item_off, nch, head, qblk_off, itab,
-              bpc_near_min, workers, near_div);
+              bpc_near_min, workers, near_div, near0);
 }
 
 // bucket -> pair ids.  Each block reserves its slice of every bucket once
@@ -333,13 +340,13 @@ __global__ __launch_bounds__(1024) void k_plan_fill(const int32_t *probe, int64_
                                                     int bpc_near, int qr, int32_t *qoff, int32_t *item_off,
                                                     int32_t *nch, int32_t *head, int32_t *qblk_off, int4 *itab,
                                                     int32_t *cursor, int32_t *qlist, int bpc_near_min,
-                                                    int workers, int near_div) {
+                                                    int workers, int near_div, int near0) {
     __shared__ int32_t sq[kFuseMax], hist[kFuseMax], base[kFuseMax], scan[1024];
     __shared__ int32_t carry;
     const int n_virt = groups * n_lists, tid = threadIdx.x;
     if (blockIdx.x == 0)
         plan_body(cnt, tile_off, n_lists, n_virt, bpc, bpc_near, qr, qoff, item_off, nch, head, qblk_off, itab,
-                  bpc_near_min, workers, near_div);
+                  bpc_near_min, workers, near_div, near0);
     // exclusive prefix of cnt over the virtual partitions -> sq
     if (tid == 0) carry = 0;
     for (int b = tid; b < n_virt; b += 1024) hist[b] = 0;
@@ -1170,7 +1177,7 @@ static int exact_topk(lira_index *idx, const float *q, int64_t nq, const int32_t
     hipLaunchKernelGGL(k_count, dim3(pg), dim3(256), hc, st, probe, npairs, nl, (int)nprobe, split, groups,
                        cnt, idx->err);
     hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, nv, pl.bpc, pl.bpc, kQT, qoff,
-                       item_off, nch, head, (int32_t *)nullptr, (int4 *)nullptr, pl.bpc, 1, 4);
+                       item_off, nch, head, (int32_t *)nullptr, (int4 *)nullptr, pl.bpc, 1, 4, 0);
     hipLaunchKernelGGL(k_fill, dim3(pg), dim3(256), hf, st, probe, npairs, nl, (int)nprobe, split, groups,
                        qoff, cursor, qlist);
     LIRA_HIP_TRY(hipGetLastError());
@@ -1294,7 +1301,7 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
 hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npairs, int nprobe, int bpc,
                        int bpc_near, int qr, int groups, int32_t *cnt, int32_t *cursor, int32_t *qoff, int32_t *item_off,
                        int32_t *nch, int32_t *head, int32_t *qlist, int32_t *qblk_off, int4 *itab,
-                       hipStream_t st, int bpc_near_min, int workers, int near_div) {
+                       hipStream_t st, int bpc_near_min, int workers, int near_div, int near0) {
     const int nl = (int)idx->n_lists, nv = groups * nl;
     const unsigned pg = (unsigned)((npairs + kPairsPerBlock - 1) / kPairsPerBlock);
     const size_t hc = nv <= kHistMax ? (size_t)nv * 4 : 0;
@@ -1303,11 +1310,11 @@ hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npai
     if (nv <= kFuseMax && qblk_off) {
         hipLaunchKernelGGL(k_plan_fill, dim3(std::max(pg, 1u)), dim3(1024), 0, st, probe, npairs, nl, nprobe, groups, cnt,
                            idx->tile_off, bpc, bpc_near, qr, qoff, item_off, nch, head, qblk_off, itab, cursor, qlist,
-                           bpc_near_min, workers, near_div);
+                           bpc_near_min, workers, near_div, near0);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, nv, bpc, bpc_near, qr, qoff,
-                       item_off, nch, head, qblk_off, itab, bpc_near_min, workers, near_div);
+                       item_off, nch, head, qblk_off, itab, bpc_near_min, workers, near_div, near0);
     hipLaunchKernelGGL(k_fill, dim3(pg), dim3(256), hf, st, probe, npairs, nl, nprobe, 1, groups, qoff, cursor,
                        qlist);
     return hipGetLastError();

@@ -60,7 +60,7 @@ hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npai
                        int bpc_near,
                        int qr, int groups, int32_t *cnt, int32_t *cursor, int32_t *qoff, int32_t *item_off,
                        int32_t *nch, int32_t *head, int32_t *qlist, int32_t *qblk_off, int4 *itab,
-                       hipStream_t st, int bpc_near_min, int workers, int near_div);
+                       hipStream_t st, int bpc_near_min, int workers, int near_div, int near0);
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -1783,9 +1783,11 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
     auto rescan = [&](int s, int p, int c, float T) {
         ++n_rescans;
         flush_pending();
-        const int bpc = a.groups == 2 && s == 0 ? a.head[19] : a.bpc;
+        // (group 0's first chunk may be smaller than the rest: head[21] blocks)
+        const bool g0 = a.groups == 2 && s == 0;
+        const int bpc = g0 ? a.head[19] : a.bpc, b0 = g0 ? a.head[21] : bpc;
         const int tile0 = a.tile_off[p], ntl = a.tile_off[p + 1] - tile0;
-        const int t0 = c * bpc * kSBT, t1 = min(ntl, t0 + bpc * kSBT);
+        const int t0 = (c == 0 ? 0 : b0 + (c - 1) * bpc) * kSBT, t1 = min(ntl, t0 + (c == 0 ? b0 : bpc) * kSBT);
         for (int t = t0; t < t1; ++t) {
             const int pos = (tile0 + t) * kTile + lane;
             const int gid = a.ids[pos];
@@ -1987,10 +1989,11 @@ struct SPlan {
     int rl = 1, qr = 64, K2 = 32, bpc = 1, bpc_near = 1, nch_max = 1, grid = 1, smem = 0, mfma = 1, split = 0;
     int bpc_near_min = 1, workers = 1;  // the plan picks group 0's chunk size in [bpc_near_min, bpc_near]
     int rs = 0;  // the wave-streaming screen k_screen_r (lira_rscreen.hip) instead of k_screen_m
+    int near0 = 0;  // (k_screen_r, two groups) blocks in group 0's first chunk; 0: uniform chunks
     int pp = 0;  // per-pair query records (QN / QE / QH per pair, k_pairs or k_seed_t<.., PAIRS>)
                  // instead of k_qstage's per-block copy: the hi x hi k_screen_m
     int64_t max_qblk = 0;
-    size_t off_cnt, off_cursor, off_head, off_qoff, off_item, off_nch, off_qblk, off_itab, off_qlist, off_qt, off_qn,
+    size_t off_cnt, off_cursor, off_head, off_done, off_qoff, off_item, off_nch, off_qblk, off_itab, off_qlist, off_qt, off_qn,
         off_partial, off_qbound, off_pqn, off_pe, off_qe, off_live, total;
 };
 
@@ -2112,7 +2115,12 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
         const int64_t split6 = std::max<int64_t>(1, ((pl.rs ? 3 : 6) * (int64_t)workers + est0 - 1) / std::max<int64_t>(1, est0));
         pl.bpc_near_min = (int)std::min<int64_t>(pl.bpc_near, std::max<int64_t>(1, (max_blocks + split6 - 1) / split6));
     }
-    pl.nch_max = (int)((max_blocks + pl.bpc_near_min - 1) / pl.bpc_near_min);
+    // (k_screen_r) group 0's small first chunks, waited for by the query block's others
+    if (pl.rs && two) {
+        const int nf = op.near_first < 0 ? 2 : op.near_first;
+        pl.near0 = (int)std::min<int64_t>(nf, max_blocks);
+    }
+    pl.nch_max = (int)((max_blocks + pl.bpc_near_min - 1) / pl.bpc_near_min) + (pl.near0 > 0 ? 1 : 0);
     pl.max_qblk = npairs / pl.qr + std::min<int64_t>(2 * idx->n_lists, npairs) + 1;
     size_t o = 0;
     auto take = [&](size_t bytes) {
@@ -2124,7 +2132,9 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     pl.off_cnt = take(nl * 4);
     pl.off_cursor = take(nl * 4);
     pl.off_head = take(128 * 4);  // [0..1] totals, [2..9] XCD queue counters, [10..18] queue bounds,
-                                  // [19] group 0's chunk size, [64..127] the seed's work estimates
+                                  // [19] group 0's chunk size, [20] the most chunks of a bucket,
+                                  // [21] group 0's first chunk size, [64..127] the seed's work estimates
+    pl.off_done = take(pl.near0 > 0 ? (size_t)(pl.max_qblk + 1) * 4 : 0);  // per query block: first chunk done
     pl.off_qoff = take((nl + 1) * 4);
     pl.off_item = take((nl + 1) * 4);
     pl.off_nch = take(nl * 4);
@@ -2274,7 +2284,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     const int64_t npairs = nq * nprobe;
 
     if (ev[0]) LIRA_HIP_TRY(hipEventRecord(ev[0], st));
-    LIRA_HIP_TRY(hipMemsetAsync(w, 0, pl.off_qoff, st));  // cnt, cursor, head
+    LIRA_HIP_TRY(hipMemsetAsync(w, 0, pl.off_qoff, st));  // cnt, cursor, head, done flags
     // Two groups (every query's first probe slot -- its nearest partition, where
     // most of its top-k lives -- queued ahead of the rest) when the bound is
     // shared across a query's items: later items then start from tight bounds.
@@ -2359,7 +2369,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     LIRA_HIP_TRY(launch_plan(idx, pprobe, npairs, (int)nprobe, pl.bpc, groups == 2 ? pl.bpc_near : pl.bpc, pl.qr, groups, cnt, cursor, qoff, item_off,
                              nch, head, qlist, qblk, itab, st,
                              groups == 2 && fused && idx->lsamp ? pl.bpc_near_min : (groups == 2 ? pl.bpc_near : pl.bpc),
-                             pl.workers, pl.rs ? 2 : 4));
+                             pl.workers, pl.rs ? 2 : 4, groups == 2 ? pl.near0 : 0));
     if (!pl.pp) {
     const dim3 qgrid((unsigned)pl.max_qblk, (unsigned)((idx->dpad + 64 * kQSlabs - 1) / (64 * kQSlabs)));
     if (pl.qr == 128 && pl.split)
@@ -2457,6 +2467,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
         r.gP = std::nextafter((float)((1.0 + g) * (1.0 + 0x1p-50)), INFINITY);
         r.invF = std::nextafter((float)((1.0 / (1.0 - g)) * (1.0 + 0x1p-50)), INFINITY);
         r.stats = a.stats;
+        r.done0 = groups == 2 && pl.near0 > 0 ? (int32_t *)(w + pl.off_done) : nullptr;
         e = launch_rscreen(r, pl.grid, st);
     } else {
         e = idx->metric == LIRA_METRIC_L2 ? launch_screen_rl<LIRA_METRIC_L2>(a, pl, st)
