@@ -393,6 +393,88 @@ static bool rank_exact64_ok(const float *q, const float *cent, int64_t nb, int64
     return nb <= 64 && d % 4 == 0 && d <= 256 && ((uintptr_t)q & 15) == 0 && ((uintptr_t)cent & 15) == 0;
 }
 
+// The same one-pass exact ranking for 64 < nb <= 256 or d > 256 (GIST1M: B =
+// 128, d = 960; DEEP10M: B = 256): CPL centroids per lane (lane b holds
+// centroids b, b + 64, ..), the centroid rows staged transposed through LDS in
+// chunks of DC4 float4 columns ([DC4][64 CPL], 64 KB) -- every query of the
+// workgroup (one per wave) consumes a chunk before the next is staged, so the
+// partial sums carry over and each one stays search.cpp:220-235's sequential
+// fp32 sum in dim order.  Then one sort of the wave's 64 CPL (sqrt, index) keys.
+// Replaces the MFMA GEMM + boundary re-check there (GIST1M 1 k queries:
+// k_centroid_gemm + k_rank_select 68 us).
+// fp32 sqrt, correctly rounded: LLVM's lowering of the IEEE sqrt written out
+// (v_sqrt_f32 is within 1 ulp; the two fma residuals pick the nearest of s and
+// its neighbours; values below 2^-96 are scaled by 2^32 first).  hipcc lowered
+// __fsqrt_rn here to the bare 1-ulp form in one kernel, and a (sqrt, index) key
+// 1 ulp off changes which of two near-equal centroids ranks first.
+__device__ __forceinline__ float sqrt_rn_f32(float x) {
+    const bool scale = x < 0x1p-96f;
+    const float xs = scale ? x * 0x1p+32f : x;
+    const float s = __builtin_amdgcn_sqrtf(xs);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rm = __builtin_fmaf(-sm, s, xs), rp = __builtin_fmaf(-sp, s, xs);
+    float r = rp > 0.0f ? sp : rm <= 0.0f ? sm : s;
+    r = scale ? r * 0x1p-16f : r;
+    return (xs == 0.0f || !(xs < __builtin_inff())) ? xs : r;  // (+-0, +inf, NaN as they are)
+}
+
+template <int CPL>
+__global__ __launch_bounds__(512) void k_rank_exact_dc(const float *__restrict__ q, int64_t nq,
+                                                      const float *__restrict__ cent, int nb, int64_t d,
+                                                      int nprobe, int32_t *out) {
+    constexpr int NC = 64 * CPL, DC4 = 4096 / NC;  // (64 KB of LDS)
+    __shared__ float4 Cs[DC4 * NC];
+    const int tid = threadIdx.x, lane = tid & 63, nw = blockDim.x >> 6;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nd4 = (int)(d >> 2);
+    const int64_t qi = (int64_t)blockIdx.x * nw + w;
+    const float4 *qr = (const float4 *)(q + (qi < nq ? qi : 0) * d);
+    float acc[CPL];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) acc[c] = 0.0f;
+    for (int j0 = 0; j0 < nd4; j0 += DC4) {
+        const int nd = min(DC4, nd4 - j0);
+        __syncthreads();  // (the previous chunk is consumed)
+        for (int i = tid; i < NC * nd; i += blockDim.x) {  // consecutive threads: consecutive float4 of one row
+            const int b = i / nd, jj = i - b * nd;
+            Cs[jj * NC + b] = b < nb ? *(const float4 *)(cent + (int64_t)b * d + 4 * (j0 + jj)) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        __syncthreads();
+        if (qi < nq) {
+#pragma unroll 4
+            for (int jj = 0; jj < nd; ++jj) {
+                const float4 qv = qr[j0 + jj];
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) {
+                    const float4 cv = Cs[jj * NC + c * 64 + lane];
+                    float df = qv.x - cv.x;
+                    acc[c] = acc[c] + df * df;
+                    df = qv.y - cv.y;
+                    acc[c] = acc[c] + df * df;
+                    df = qv.z - cv.z;
+                    acc[c] = acc[c] + df * df;
+                    df = qv.w - cv.w;
+                    acc[c] = acc[c] + df * df;
+                }
+            }
+        }
+    }
+    if (qi >= nq) return;
+    u64 key[CPL];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) key[c] = c * 64 + lane < nb ? make_key(sqrt_rn_f32(acc[c]), c * 64 + lane) : kEmptyKey;
+    wave_sort<CPL>(key);  // element r * 64 + lane in key[r]
+    int32_t *o = out + qi * nprobe;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c)
+        if (c * 64 + lane < nprobe) o[c * 64 + lane] = key[c] == kEmptyKey ? -1 : key_gid(key[c]);
+    for (int e = NC + lane; e < nprobe; e += 64) o[e] = -1;
+}
+static int rank_exact_dc_cpl(const float *q, const float *cent, int64_t nb, int64_t d) {
+    if (d % 4 != 0 || ((uintptr_t)q & 15) != 0 || ((uintptr_t)cent & 15) != 0) return 0;
+    return nb <= 64 ? 1 : nb <= 128 ? 2 : nb <= 256 ? 4 : 0;
+}
+
 // -------------------------------------------------------------- probe select
 template <int R>
 __global__ __launch_bounds__(256) void k_select_nearest(const float *__restrict__ s, int64_t n,
@@ -615,6 +697,22 @@ int lira_rank_nearest(const float *q, int64_t nq, const float *centroids, int64_
         const unsigned g = (unsigned)((nq + 8 * qpw - 1) / (8 * qpw));
         hipLaunchKernelGGL(k_rank_exact64, dim3(g), dim3(512), (size_t)d * 64 * 4, (hipStream_t)stream, q, nq,
                            centroids, (int)n_centroids, d, (int)nprobe, qpw, out_probe);
+        LIRA_HIP_TRY(hipGetLastError());
+        return LIRA_OK;
+    }
+    if (const int cpl = rank_exact_dc_cpl(q, centroids, n_centroids, d)) {  // (no workspace needed)
+        const int nw = nq >= 4096 ? 8 : 4;  // queries (waves) per workgroup: fewer for small batches
+        const unsigned g = (unsigned)((nq + nw - 1) / nw);
+        hipStream_t st = (hipStream_t)stream;
+        if (cpl == 1)
+            hipLaunchKernelGGL(k_rank_exact_dc<1>, dim3(g), dim3(64 * nw), 0, st, q, nq, centroids, (int)n_centroids, d,
+                               (int)nprobe, out_probe);
+        else if (cpl == 2)
+            hipLaunchKernelGGL(k_rank_exact_dc<2>, dim3(g), dim3(64 * nw), 0, st, q, nq, centroids, (int)n_centroids, d,
+                               (int)nprobe, out_probe);
+        else
+            hipLaunchKernelGGL(k_rank_exact_dc<4>, dim3(g), dim3(64 * nw), 0, st, q, nq, centroids, (int)n_centroids, d,
+                               (int)nprobe, out_probe);
         LIRA_HIP_TRY(hipGetLastError());
         return LIRA_OK;
     }

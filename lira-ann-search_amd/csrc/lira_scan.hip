@@ -216,7 +216,7 @@ __device__ __forceinline__ void plan_body(const int32_t *cnt, const int32_t *til
     // finds its partition by a binary search over the LDS prefix sums): one
     // thread per partition writing its items in turn serialised ~30 stores
     // per thread (SIFT1M: k_plan 26 -> ~8 us).
-    // Two groups: each queue first holds chunk 0 of its group-0 partitions (every
+    // Two groups, k_screen_r (near0 > 0): each queue first holds chunk 0 of its group-0 partitions (every
     // query block's nearest-partition items that start the bound chain), then
     // the rest in partition order.  The ~2 items per workgroup that start at
     // once run on the seed's bound; the later group-0 chunks start from the
@@ -229,7 +229,7 @@ __device__ __forceinline__ void plan_body(const int32_t *cnt, const int32_t *til
     __syncthreads();
     const int m = (n_virt + 7) / 8;
     const bool two = n_virt > n_lists;
-    const int m0 = two ? (n_lists + 7) / 8 : 0, M = m0 + m;
+    const int m0 = two && near0 > 0 ? (n_lists + 7) / 8 : 0, M = m0 + m;  // (k_screen_r's plans only)
     if (threadIdx.x == 0) carry_b = 0;
     __syncthreads();
     for (int base = 0; base < 8 * M; base += 1024) {
@@ -242,7 +242,7 @@ __device__ __forceinline__ void plan_body(const int32_t *cnt, const int32_t *til
         if (v < n_virt) {
             nc = nch[v];
             nqb = (cnt[v] + qr - 1) / qr;
-            const bool g0 = two && v < n_lists;
+            const bool g0 = m0 > 0 && v < n_lists;  // (group 0 with its chunk-0 slots split off)
             items = first ? (nc > 0 ? nqb : 0) : g0 ? nqb * max(0, nc - 1) : nqb * nc;
             c0 = !first && g0 ? 1 : 0;
         }

@@ -30,7 +30,10 @@ def test_centroid_dist_golden(name):
                                      (16, 128, 960), (70, 5, 7),
                                      # the one-pass exact kernel (nb <= 64, d % 4 == 0, d <= 256):
                                      # several workgroups with a partial last one, the LDS maximum
-                                     (1000, 64, 256), (65, 33, 100), (300, 64, 132), (37, 64, 260)])
+                                     (1000, 64, 256), (65, 33, 100), (300, 64, 132), (37, 64, 260),
+                                     # the chunked one-pass kernel (nb <= 256, d % 4 == 0): 2 and 4
+                                     # centroids per lane, 4- and 8-wave workgroups, several dim chunks
+                                     (4100, 256, 96), (4097, 200, 64), (3, 250, 1000), (129, 65, 512)])
 def test_gemm_bound_and_rank_nearest(nq, nb, d):
     from lira_amd import centroid_dist, centroid_gemm, rank_nearest, select_probes
     rng = np.random.default_rng(nq * 7 + nb)
