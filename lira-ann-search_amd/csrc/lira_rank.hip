@@ -18,6 +18,24 @@
 
 namespace lira {
 
+// fp32 sqrt, correctly rounded: LLVM's lowering of the IEEE sqrt written out
+// (v_sqrt_f32 is within 1 ulp; the two fma residuals pick the nearest of s and
+// its neighbours; values below 2^-96 are scaled by 2^32 first).  hipcc lowered
+// __fsqrt_rn to the bare 1-ulp form in k_rank_exact_dc (not in the others), and a
+// (sqrt, index) key 1 ulp off changes which of two near-equal centroids ranks
+// first; every distance and key in this file uses this one.
+__device__ __forceinline__ float sqrt_rn_f32(float x) {
+    const bool scale = x < 0x1p-96f;
+    const float xs = scale ? x * 0x1p+32f : x;
+    const float s = __builtin_amdgcn_sqrtf(xs);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rm = __builtin_fmaf(-sm, s, xs), rp = __builtin_fmaf(-sp, s, xs);
+    float r = rp > 0.0f ? sp : rm <= 0.0f ? sm : s;
+    r = scale ? r * 0x1p-16f : r;
+    return (xs == 0.0f || !(xs < __builtin_inff())) ? xs : r;  // (+-0, +inf, NaN as they are)
+}
+
+
 // ---------------------------------------------------------------- exact dist
 // Tiled like a GEMM: a workgroup owns 64 queries x 64 centroids, stages 32-dim
 // slabs of both (coalesced row loads, transposed into LDS), and each thread
@@ -68,7 +86,7 @@ __global__ __launch_bounds__(256) void k_centroid_dist(const float *__restrict__
         for (int b = 0; b < 4; ++b) {
             const int cb = c0 + tc + b;
             if (cb >= nb) continue;
-            float r = __fsqrt_rn(acc[a][b]);
+            float r = sqrt_rn_f32(acc[a][b]);
             if (mean) {
                 float s = scale[cb];
                 if (s == 0.0f) s = 1.0f;
@@ -263,7 +281,7 @@ __global__ __launch_bounds__(256) void k_rank_select(const float *__restrict__ A
                 float df = qr[j] - cr[j];
                 acc = acc + df * df;
             }
-            key = make_key(__fsqrt_rn(acc), b);
+            key = make_key(sqrt_rn_f32(acc), b);
         }
         wave_merge_batch<R>(fin, key);
     }
@@ -321,7 +339,7 @@ __global__ __launch_bounds__(256) void k_rank_select64(const float *__restrict__
             const float df = qr[j] - cr[j];
             acc = acc + df * df;
         }
-        key = make_key(__fsqrt_rn(acc), lane);
+        key = make_key(sqrt_rn_f32(acc), lane);
     }
     // rank of my key among the candidates' (keys are distinct: the index breaks ties)
     u64 cm = __ballot(cand);
@@ -383,7 +401,7 @@ __global__ __launch_bounds__(512) void k_rank_exact64(const float *__restrict__ 
             df = qv.w - cv.w;
             acc = acc + df * df;
         }
-        const u64 key = wave_sort64(lane < nb ? make_key(__fsqrt_rn(acc), lane) : kEmptyKey);
+        const u64 key = wave_sort64(lane < nb ? make_key(sqrt_rn_f32(acc), lane) : kEmptyKey);
         int32_t *o = out + qi * nprobe;
         if (lane < nprobe) o[lane] = key == kEmptyKey ? -1 : key_gid(key);
         for (int e = 64 + lane; e < nprobe; e += 64) o[e] = -1;
@@ -402,22 +420,6 @@ static bool rank_exact64_ok(const float *q, const float *cent, int64_t nb, int64
 // fp32 sum in dim order.  Then one sort of the wave's 64 CPL (sqrt, index) keys.
 // Replaces the MFMA GEMM + boundary re-check there (GIST1M 1 k queries:
 // k_centroid_gemm + k_rank_select 68 us).
-// fp32 sqrt, correctly rounded: LLVM's lowering of the IEEE sqrt written out
-// (v_sqrt_f32 is within 1 ulp; the two fma residuals pick the nearest of s and
-// its neighbours; values below 2^-96 are scaled by 2^32 first).  hipcc lowered
-// __fsqrt_rn here to the bare 1-ulp form in one kernel, and a (sqrt, index) key
-// 1 ulp off changes which of two near-equal centroids ranks first.
-__device__ __forceinline__ float sqrt_rn_f32(float x) {
-    const bool scale = x < 0x1p-96f;
-    const float xs = scale ? x * 0x1p+32f : x;
-    const float s = __builtin_amdgcn_sqrtf(xs);
-    const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
-    const float rm = __builtin_fmaf(-sm, s, xs), rp = __builtin_fmaf(-sp, s, xs);
-    float r = rp > 0.0f ? sp : rm <= 0.0f ? sm : s;
-    r = scale ? r * 0x1p-16f : r;
-    return (xs == 0.0f || !(xs < __builtin_inff())) ? xs : r;  // (+-0, +inf, NaN as they are)
-}
-
 template <int CPL>
 __global__ __launch_bounds__(512) void k_rank_exact_dc(const float *__restrict__ q, int64_t nq,
                                                       const float *__restrict__ cent, int nb, int64_t d,
