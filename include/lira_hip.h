@@ -174,6 +174,17 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *                        small first chunks are queued first; the query block's later chunks wait
  *                        for its first one, so they start from the bounds it published instead of
  *                        the 128-row seed's.  Results never depend on it.
+ *   LIRA_OPT_RESCAN      chunks whose screened list may have dropped a candidate (its 32nd key
+ *                        within the final bound's reach) are scanned exactly again: -1 (default)
+ *                        auto -- 1 where a chunk holds >= 8192 rows (BIGANN-size lists), else 0;
+ *                        1: a pass that queues them, then k_rescan over all of them at once (a
+ *                        wave per 64-row tile), whose exact survivors the merge takes; 0: inside
+ *                        the merge, one wave per query.  Results never depend on it.
+ *   LIRA_OPT_SPILL       (k_screen_r) records per query of its spill list -- the keys a full row
+ *                        list evicts that the merge may still need, rechecked like list keys so
+ *                        that no full list is re-scanned: -1 (default) 256; 0 none (full lists are
+ *                        re-scanned as by k_screen_m); a query that overflows its records has its
+ *                        full lists re-scanned instead.  Results never depend on it.
  */
 #define LIRA_OPT_KEEP_TILES 1
 #define LIRA_OPT_SCREEN 2
@@ -195,6 +206,8 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
 #define LIRA_OPT_WIDE 18
 #define LIRA_OPT_RSCREEN 19
 #define LIRA_OPT_NEAR_FIRST 20
+#define LIRA_OPT_RESCAN 21
+#define LIRA_OPT_SPILL 22
 int lira_index_set_option(lira_index *idx, int option, int64_t value);
 int lira_index_get_option(const lira_index *idx, int option, int64_t *value);
 /* 1 if the index holds the fp32 tile copy (LIRA_OPT_KEEP_TILES at build time) */

@@ -53,6 +53,8 @@ struct lira_opts {
     int order = 1;
     int rscreen = 1;
     int near_first = -1;  // LIRA_OPT_NEAR_FIRST (-1: the default, 2 blocks)
+    int rescan = -1;      // LIRA_OPT_RESCAN (-1: auto)
+    int spill = -1;       // LIRA_OPT_SPILL (-1: 256 records per query)
 };
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device):

@@ -130,13 +130,54 @@ __device__ __forceinline__ u64 wkey_to_key(u64 wk, float qn) {
     return rkey(-ord2f((uint32_t)(wk >> 32)), qn, (uint32_t)wk);
 }
 
+// A row list's merge with the keys it evicts (spill lists on): per half, lst <- the
+// 32 smallest of lst U batch, and ev = the 32 largest (what half_merge_batch1 drops)
+__device__ __forceinline__ u64 merge_evict(u64 (&lst)[1], u64 batch) {
+    u64 b[1] = {batch};
+    half_sort<1>(b);
+    const u64 rev = rev32_u64(b[0]);
+    const u64 ev = kmax(lst[0], rev);
+    lst[0] = kmin(lst[0], rev);
+    half_bitonic_merge<1>(lst);
+    return ev;
+}
+
+// Keys a row list evicted that the merge may still need go to the query's spill
+// list (k_smerge rechecks them like list keys, so a full list needs no re-scan):
+// the ones within lim(T) + E for the row's current T -- its list's new k-th bound
+// or the T its thresholds use, both >= the final one -- by the screen's own
+// rounding, which is above k_smerge's s_lim(T, E) (lira_bounds.hpp).  Per half-wave
+// (hv: this lane's half holds the row).  Past scap records the query's count shows
+// the overflow and k_smerge re-scans its full lists instead.
+__device__ __forceinline__ void spill_evicted(const RArgs &a, u64 ev, bool hv, u64 kth, float er, float Tc, int pr) {
+    float T = kth != kEmptyKey ? rup(rup(key_score(kth) + er) * a.gP) + 0x1p-125f : __builtin_inff();
+    T = fminf(T, Tc);
+    const float Ac = T < 3e38f ? rup(rup(fmaxf(T, 0.0f) + 0x1p-125f) * a.invF) : __builtin_inff();
+    const float lim = rup(Ac + er);
+    const bool sp = hv && pr >= 0 && ev != kEmptyKey && key_score(ev) <= lim;
+    const u64 m = __ballot(sp);
+    if (!m) return;
+    // (one atomic per half-wave: the halves may hold different queries' rows)
+    const int lane = lane_id();
+    const u64 hm = m & (lane < 32 ? 0xffffffffull : 0xffffffff00000000ull);
+    const int hl0 = lane & 32;
+    unsigned base = 0;
+    const int q = pr / a.nprobe;
+    if ((lane & 31) == 0 && hm) base = atomicAdd(a.scnt + q, (unsigned)__popcll(hm));
+    base = (unsigned)__shfl((int)base, hl0, 64);
+    const unsigned at = base + (unsigned)__popcll(hm & ((1ull << lane) - 1ull));
+    if (sp && at < (unsigned)a.scap)
+        a.spill[(int64_t)q * a.scap + at] = make_uint4((uint32_t)ev, (uint32_t)(ev >> 32), __float_as_uint(er), 0u);
+}
+
 // Merge this wave's buffer of `row` (n keys) into the shared list, under the
 // row's LDS lock: raise the row's running error bound to the wave's first
 // (readers take the list's k-th key, then the bound: program order in both),
 // half-wave merge, publish the query's bound if the list's k-th improved.
 __device__ __forceinline__ void flush_row(u64 *lists, u64 *kth_s, const u64 *mybuf, int *lock_s, uint32_t *erun_s,
                                        uint32_t *opub_s, const int *pair_s, int row, int n, int ew_bits, int k,
-                                       uint32_t *qbound, int nprobe, float gP, float qn_row) {
+                                       uint32_t *qbound, int nprobe, float gP, float qn_row, const RArgs &a,
+                                       float Tc_row) {
     const int lane = opaque(lane_id()), hl = lane & 31;  // (opaque: addresses computed here, not hoisted)
 #ifdef RS_CLOCKS
     if (lane == 0) atomicAdd(&g_rs_clk[12], 1ull);
@@ -148,7 +189,11 @@ __device__ __forceinline__ void flush_row(u64 *lists, u64 *kth_s, const u64 *myb
     asm volatile("" ::: "memory");
     u64 lst[1] = {lists[row * kRK2 + hl]};
     const u64 b = hl < n ? wkey_to_key(mybuf[row * kRBC + hl], qn_row) : kEmptyKey;
-    half_merge_batch1<1>(lst, b);
+    u64 ev = kEmptyKey;
+    if (a.spill)
+        ev = merge_evict(lst, b);
+    else
+        half_merge_batch1<1>(lst, b);
     if (lane < 32) lists[row * kRK2 + hl] = lst[0];
     if (lane == k - 1) kth_s[row] = lst[0];
     if (lane == k - 1 && lst[0] != kEmptyKey && qbound) {
@@ -165,6 +210,8 @@ __device__ __forceinline__ void flush_row(u64 *lists, u64 *kth_s, const u64 *myb
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (LDS in order: the list is written before the unlock)
     if (lane == 0) *(volatile int *)(lock_s + row) = 0;
     __builtin_amdgcn_wave_barrier();
+    if (a.spill)  // (after the unlock: the atomic's round trip holds no other wave)
+        spill_evicted(a, ev, lane < 32, shfl64(lst[0], k - 1), __uint_as_float(erun_s[row]), Tc_row, pair_s[row]);
 }
 
 // Merge this wave's full row buffers into the lists, then move the survivor
@@ -173,7 +220,8 @@ __device__ __forceinline__ void flush_row(u64 *lists, u64 *kth_s, const u64 *myb
 __device__ __forceinline__ void drain_buffers(u64 *lists, u64 *kth_s, u64 *mybuf, int *mybufc, int *lock_s,
                                            uint32_t *erun_s, uint32_t *opub_s, const int *pair_s,
                                            const float4 *rec_s, const u64 *oq_key, uint32_t pos_base, int nq,
-                                           float Ew, int k, uint32_t *qbound, int nprobe, float gP) {
+                                           float Ew, int k, uint32_t *qbound, int nprobe, float gP, const RArgs &a,
+                                           float Tc) {
     const int lane = opaque(lane_id());
     auto flush_full = [&]() {
         u64 full = __ballot(mybufc[lane] >= kRBC);  // lane = row
@@ -181,7 +229,8 @@ __device__ __forceinline__ void drain_buffers(u64 *lists, u64 *kth_s, u64 *mybuf
             const int row = __builtin_ctzll(full);
             full &= full - 1;
             flush_row(lists, kth_s, mybuf, lock_s, erun_s, opub_s, pair_s, row, kRBC,
-                      __builtin_amdgcn_readlane(__float_as_int(Ew), row), k, qbound, nprobe, gP, rec_s[row].x);
+                      __builtin_amdgcn_readlane(__float_as_int(Ew), row), k, qbound, nprobe, gP, rec_s[row].x, a,
+                      __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Tc), row)));
             if (lane == 0) mybufc[row] = 0;
             __builtin_amdgcn_wave_barrier();
         }
@@ -441,7 +490,7 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
             return;
 #endif
             drain_buffers(lists, kth_s, mybuf, mybufc, lock_s, erun_s, opub_s, pair_s, rec_s, oq_key,
-                          (uint32_t)tbase * 64u, ovf, Ew, k, a.qbound, a.nprobe, a.gP);
+                          (uint32_t)tbase * 64u, ovf, Ew, k, a.qbound, a.nprobe, a.gP, a, Tc);
             ovf = 0;
         };
 
@@ -627,8 +676,15 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
                     b = wkey_to_key(bufs[(w * kRQ + row) * kRBC + off], qn_r);
                 }
                 u64 lst[1] = {lists[row * kRK2 + hl]};
-                half_merge_batch1<1>(lst, b);
-                lists[row * kRK2 + hl] = lst[0];
+                if (a.spill) {
+                    const u64 ev = merge_evict(lst, b);
+                    lists[row * kRK2 + hl] = lst[0];
+                    spill_evicted(a, ev, true, shfl64(lst[0], (ln & 32) + k - 1), __uint_as_float(erun_s[row]),
+                                  __shfl(Tc, row, 64), pair_s[row]);
+                } else {
+                    half_merge_batch1<1>(lst, b);
+                    lists[row * kRK2 + hl] = lst[0];
+                }
                 __builtin_amdgcn_wave_barrier();
             }
         }

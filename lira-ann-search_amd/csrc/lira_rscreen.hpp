@@ -26,6 +26,9 @@ struct RArgs {
     float invF;              // >= 1 / (1 - (d + 4) 2^-24) (s_lim's factor, rounded up)
     unsigned long long *stats;
     int32_t *done0;          // per query block: its nearest partition's first chunk is done (NULL: no waits)
+    uint4 *spill;            // NULL, or [nq][scap] evicted keys k_smerge may need: (key lo, key hi, E bits, 0)
+    unsigned *scnt;          // [nq] records spilled (> scap: overflowed)
+    int scap;
 };
 
 // the shapes k_screen_r implements: L2 on the centred split copy, hi x hi,

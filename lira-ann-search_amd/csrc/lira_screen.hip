@@ -739,6 +739,19 @@ struct SMergeArgs {
     unsigned long long *stats;
     int unsorted;  // a list may hold its keys unsorted (k_screen_v): walk it to its first empty key
     const int32_t *head;  // head[19]: group 0's chunk size as the plan chose it
+    // LIRA_OPT_RESCAN: 0 the merge re-scans a chunk whose list may have dropped a
+    // candidate itself; 1 it only queues (q, slot, chunk, partition) in rq; 2 it takes
+    // k_rescan's exact survivors rbuf[q][0 .. rcnt[q]) instead (rfall[q]: the queue
+    // or the query's buffer overflowed -- its chunks are re-scanned here as in 0)
+    int rmode, rq_cap, rcap;
+    unsigned *rq_n, *rcnt, *rfall;
+    int4 *rq;
+    const u64 *rbuf;
+    // k_screen_r's spill lists (NULL: none): keys its row lists evicted that may still
+    // be needed, per query, (key lo, key hi, E bits, 0); scnt[q] > scap: overflowed
+    const uint4 *spill;
+    const unsigned *scnt;
+    int scap;
 };
 
 // exact score of the candidate at storage row pos (search.cpp:253-269 order)
@@ -1642,6 +1655,49 @@ __global__ __launch_bounds__(256) void k_seed_t(const float *Q, const int32_t *p
 // per-wave LDS slab [row][33] (odd stride: conflict-free row reads), and lane r
 // accumulates row r in search.cpp's order.  The 4 x 64 exact scores then meet
 // in LDS, where wave 0 forms the bound.
+// exact scores (search.cpp:253-269 order, as exact_score) of the 64 rows of one
+// tile against one query, lane r -> row r: the rows (contiguous in the row-major
+// copy) are read 32 dims at a time, coalesced (lane l loads 16-B pieces of rows
+// l/8 + 8 i), and transposed through the wave's LDS slab [row][33] (odd stride:
+// conflict-free row reads).  Wave-uniform; slab: 64 x 33 floats of its own.
+template <int METRIC>
+__device__ __forceinline__ float tile_exact(const float *qrow, const float *rows, int64_t d, float *slab, int lane) {
+    float acc = 0.0f;
+    const bool v4 = (d & 3) == 0;
+    for (int64_t j0 = 0; j0 < d; j0 += 32) {
+        const int nj = (int)min<int64_t>(32, d - j0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int r = (lane >> 3) + 8 * i, c = 4 * (lane & 7);
+            const float *src = rows + (int64_t)r * d + j0 + c;
+            float v[4];
+            if (v4 && c + 4 <= nj) {
+                const float4 f = *(const float4 *)src;
+                v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+            } else {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = c + u < nj ? src[u] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) slab[r * 33 + c + u] = v[u];
+        }
+        const float qv = (lane & 31) < nj ? qrow[j0 + (lane & 31)] : 0.0f;
+        __builtin_amdgcn_wave_barrier();
+        for (int jj = 0; jj < nj; ++jj) {
+            const float qj = __shfl(qv, jj, 64);
+            const float xv = slab[lane * 33 + jj];
+            if (METRIC == LIRA_METRIC_L2) {
+                const float df = qj - xv;
+                acc = acc + df * df;
+            } else {
+                acc = acc + qj * xv;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    return METRIC == LIRA_METRIC_L2 ? acc : -acc;
+}
+
 template <int METRIC>
 __global__ __launch_bounds__(256) void k_seed(const float *Q, const int32_t *probe, int nprobe, int n_lists,
                                               const int32_t *tile_off, const int32_t *ids, const float *Xr,
@@ -1655,45 +1711,8 @@ __global__ __launch_bounds__(256) void k_seed(const float *Q, const int32_t *pro
     if (p < 0 || p >= n_lists) return;  // workgroup-uniform
     const int tile0 = tile_off[p], nt = min(kSeedTiles, tile_off[p + 1] - tile0);
     if (nt <= 0) return;
-    float acc = 0.0f;
-    if (w < nt) {
-        float *slab = slab_all[w];
-        const float *qrow = Q + q * d;
-        const float *rows = Xr + (int64_t)(tile0 + w) * kTile * d;
-        const bool v4 = (d & 3) == 0;
-        for (int64_t j0 = 0; j0 < d; j0 += 32) {
-            const int nj = (int)min<int64_t>(32, d - j0);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int r = (lane >> 3) + 8 * i, c = 4 * (lane & 7);
-                const float *src = rows + (int64_t)r * d + j0 + c;
-                float v[4];
-                if (v4 && c + 4 <= nj) {
-                    const float4 f = *(const float4 *)src;
-                    v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
-                } else {
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) v[u] = c + u < nj ? src[u] : 0.0f;
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) slab[r * 33 + c + u] = v[u];
-            }
-            const float qv = (lane & 31) < nj ? qrow[j0 + (lane & 31)] : 0.0f;
-            __builtin_amdgcn_wave_barrier();
-            for (int jj = 0; jj < nj; ++jj) {
-                const float qj = __shfl(qv, jj, 64);
-                const float xv = slab[lane * 33 + jj];
-                if (METRIC == LIRA_METRIC_L2) {
-                    const float df = qj - xv;
-                    acc = acc + df * df;
-                } else {
-                    acc = acc + qj * xv;
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-    }
-    const float sc = METRIC == LIRA_METRIC_L2 ? acc : -acc;
+    const float sc = w < nt ? tile_exact<METRIC>(Q + q * d, Xr + (int64_t)(tile0 + w) * kTile * d, d, slab_all[w], lane)
+                            : 0.0f;
     score_s[w][lane] = w < nt && ids[(tile0 + w) * kTile + lane] >= 0 && sc == sc ? sc : __builtin_inff();
     __syncthreads();
     if (w != 0) return;
@@ -1751,6 +1770,9 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
     uint32_t *pend = s_pend[w];
     int64_t ncand = 0;
     unsigned long long n_rechecked = 0, n_rescans = 0;
+    const bool fall = a.rmode == 2 && a.rfall[q] != 0u;
+    // lists + spills hold every key within reach: no list is re-scanned
+    const bool sok = a.spill && !a.per_partition && a.scnt[q] <= (unsigned)a.scap;
 
     u64 lst[R];
     int pc = 0;  // pending survivors (storage rows) in pend[0..pc)
@@ -1781,7 +1803,6 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
     };
     // the chunk's candidates, all exact (a list that may have dropped one)
     auto rescan = [&](int s, int p, int c, float T) {
-        ++n_rescans;
         flush_pending();
         // (group 0's first chunk may be smaller than the rest: head[21] blocks)
         const bool g0 = a.groups == 2 && s == 0;
@@ -1832,10 +1853,10 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
                                       : err_E<METRIC>(qn_s, (double)a.rmax[p], dd, a.split, (double)a.dpad, a.centred);
                 lim = s_lim<METRIC>((double)T, E, dd);
                 const u64 last = src[K2 - 1];
-                over = last != kEmptyKey && (double)key_score(last) <= lim;  // (kUnsortedMark: a NaN score)
+                over = !sok && last != kEmptyKey && (double)key_score(last) <= lim;  // (kUnsortedMark: a NaN score)
                 uns = uns || last == kUnsortedMark;  // an unmerged row buffer (k_screen_m): walk to its first empty key
             }
-            bool active = p >= 0 && !over;
+            bool active = p >= 0 && !over && a.rmode != 1;
             // four keys per round (two 16-B loads; K2 % 4 == 0, lists 32-B aligned):
             // the walk is one dependent load per round
             for (int e0 = 0; __any(active); e0 += 4) {
@@ -1858,6 +1879,23 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
                 }
             }
             u64 ov = __ballot(over);
+            if (a.rmode == 1) {  // queue them for k_rescan
+                if (ov) {
+                    unsigned base = 0;
+                    if (lane == 0) base = atomicAdd(a.rq_n, (unsigned)popc64(ov));
+                    base = (unsigned)__shfl((int)base, 0, 64);
+                    const unsigned at = base + (unsigned)mbcnt64(ov);
+                    if (over) {
+                        if (at < (unsigned)a.rq_cap)
+                            a.rq[at] = make_int4((int)q, s, c, p);
+                        else
+                            a.rfall[q] = 1u;
+                    }
+                }
+                continue;
+            }
+            n_rescans += popc64(ov);
+            if (a.rmode == 2 && !fall) continue;  // k_rescan has them
             while (ov) {
                 const int ln = __builtin_ctzll(ov);
                 ov &= ov - 1;
@@ -1908,7 +1946,28 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
             if (p >= 0 && p < a.n_lists) ncand += a.list_size[p];
         }
         take_lists(0, a.nprobe, T);
+        if (a.rmode == 1) return;
+        if (sok) {  // the spilled keys within their lists' limits
+            const int ns = (int)a.scnt[q];
+            const uint4 *sp = a.spill + q * (int64_t)a.scap;
+            for (int i0 = 0; i0 < ns; i0 += 64) {
+                bool take = false;
+                uint32_t pos = 0;
+                if (i0 + lane < ns) {
+                    const uint4 r = sp[i0 + lane];
+                    const u64 key = ((u64)r.y << 32) | r.x;
+                    take = (double)key_score(key) <= s_lim<METRIC>((double)T, (double)__uint_as_float(r.z), dd);
+                    pos = r.x;
+                }
+                add(take, pos);
+            }
+        }
         flush_pending();
+        if (a.rmode == 2 && !fall) {  // k_rescan's exact survivors (all within T)
+            const int nr = (int)min(a.rcnt[q], (unsigned)a.rcap);
+            const u64 *rb = a.rbuf + q * (int64_t)a.rcap;
+            for (int i0 = 0; i0 < nr; i0 += 64) merge_batch_if<R>(lst, i0 + lane < nr ? rb[i0 + lane] : kEmptyKey);
+        }
         emit_list<R>(lst, k, a.dedup, METRIC, a.D + q * k, a.I + q * k);
     }
     if (lane == 0) {
@@ -1917,6 +1976,60 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
             atomicAdd(a.stats + 5, n_rechecked);
             if (n_rescans) atomicAdd(a.stats + 6, n_rescans);
         }
+    }
+}
+
+// ---- k_rescan (LIRA_OPT_RESCAN 1): the queued chunks, all at once ----------
+// One wave per (queued chunk, 64-row tile), grid-strided over a fixed grid (the
+// queue length is on the device): exact scores as the merge's own re-scan
+// computes them, the ones within the query's final bound T appended to its
+// buffer (rbuf[q], rcap keys; past that rfall[q] sends the query back to the
+// merge's own re-scan).  BIGANN-100M mixture: 1,629 re-scans of 32k-row chunks,
+// one wave per query in the merge, were 21 ms of a 68 ms step.
+struct RescanArgs {
+    const int4 *rq;
+    const unsigned *rq_n;
+    const float *Q, *Xr;
+    const int32_t *ids, *tile_off, *head;
+    const uint32_t *qbound;
+    u64 *rbuf;
+    unsigned *rcnt, *rfall;
+    int64_t d;
+    int rq_cap, maxT, groups, bpc, rcap;
+};
+
+template <int METRIC>
+__global__ __launch_bounds__(256) void k_rescan(RescanArgs a) {
+    __shared__ float slab_all[4][64 * 33];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t W = (int64_t)gridDim.x * 4;
+    const int64_t n = min(*a.rq_n, (unsigned)a.rq_cap), units = n * a.maxT;
+    for (int64_t u = (int64_t)blockIdx.x * 4 + w; u < units; u += W) {
+        const int64_t e = u / a.maxT;
+        const int t = (int)(u - e * a.maxT);
+        const int4 ent = a.rq[e];
+        const int q = ent.x, s = ent.y, c = ent.z, p = ent.w;
+        // the chunk's tiles, as the merge's re-scan maps them
+        const bool g0 = a.groups == 2 && s == 0;
+        const int bpc = g0 ? a.head[19] : a.bpc, b0 = g0 ? a.head[21] : bpc;
+        const int tile0 = a.tile_off[p], ntl = a.tile_off[p + 1] - tile0;
+        const int t0 = (c == 0 ? 0 : b0 + (c - 1) * bpc) * kSBT, t1 = min(ntl, t0 + (c == 0 ? b0 : bpc) * kSBT);
+        if (t0 + t >= t1 || a.rfall[q]) continue;  // (wave-uniform)
+        const float T = a.qbound[q] != ~0u ? ord2f(a.qbound[q]) : __builtin_inff();
+        const int64_t tile = tile0 + t0 + t;
+        const float sc = tile_exact<METRIC>(a.Q + (int64_t)q * a.d, a.Xr + tile * kTile * a.d, a.d, slab_all[w], lane);
+        const int gid = a.ids[tile * kTile + lane];
+        const bool take = gid >= 0 && sc <= T;
+        const u64 m = __ballot(take);
+        if (!m) continue;
+        unsigned base = 0;
+        if (lane == 0) base = atomicAdd(a.rcnt + q, (unsigned)popc64(m));
+        base = (unsigned)__shfl((int)base, 0, 64);
+        if (base + (unsigned)popc64(m) > (unsigned)a.rcap) {
+            if (lane == 0) a.rfall[q] = 1u;
+            continue;
+        }
+        if (take) a.rbuf[(int64_t)q * a.rcap + base + mbcnt64(m)] = make_key(sc, gid);
     }
 }
 
@@ -1992,7 +2105,10 @@ struct SPlan {
     int near0 = 0;  // (k_screen_r, two groups) blocks in group 0's first chunk; 0: uniform chunks
     int pp = 0;  // per-pair query records (QN / QE / QH per pair, k_pairs or k_seed_t<.., PAIRS>)
                  // instead of k_qstage's per-block copy: the hi x hi k_screen_m
+    int prescan = 0, rq_cap = 0, rcap = 0, maxT = 0;  // LIRA_OPT_RESCAN: k_rescan (queue / buffer sizes)
+    int scap = 0;  // k_screen_r's spill records per query (0: no spill lists)
     int64_t max_qblk = 0;
+    size_t off_rst, off_rq, off_rbuf, off_scnt, off_spill;
     size_t off_cnt, off_cursor, off_head, off_done, off_qoff, off_item, off_nch, off_qblk, off_itab, off_qlist, off_qt, off_qn,
         off_partial, off_qbound, off_pqn, off_pe, off_qe, off_live, total;
 };
@@ -2046,9 +2162,10 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // 1.50 ms against 0.325 on SIFT1M: removed in round 4)
     pl.pp = pl.split == 3;
     // k_screen_r where it applies (its own preconditions on the scan's flags are in screen_topk)
+    // (with or without the fp32 tiles: the seed then comes from the row-major copy
+    // and the per-pair records from k_pairs -- BIGANN-100M's compact index)
     pl.rs = op.rscreen && pl.split == 3 && idx->metric == LIRA_METRIC_L2 && idx->xadjc && idx->pivot &&
-            rscreen_shape_ok(idx->dpad, k) && !(flags & LIRA_SCAN_PER_PARTITION) && op.seed && idx->X &&
-            idx->lstat;
+            rscreen_shape_ok(idx->dpad, k) && !(flags & LIRA_SCAN_PER_PARTITION) && op.seed && idx->lstat;
     pl.smem = !pl.mfma       ? screen_smem(pl.qr, pl.rl)
               : pl.qr == 128 ? (pl.split == 2 ? SSmem<128, 1, true, true>::total
                                 : pl.rl == 1 ? SSmem<128, 1, true>::total : SSmem<128, 2, true>::total)
@@ -2122,6 +2239,16 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     }
     pl.nch_max = (int)((max_blocks + pl.bpc_near_min - 1) / pl.bpc_near_min) + (pl.near0 > 0 ? 1 : 0);
     pl.max_qblk = npairs / pl.qr + std::min<int64_t>(2 * idx->n_lists, npairs) + 1;
+    // the merge's chunk re-scans through k_rescan: where a chunk is long enough for
+    // one wave per query to be the merge's tail (BIGANN-100M: 32k rows)
+    pl.maxT = std::max(pl.bpc, pl.near0) * kSBT;
+    pl.prescan = !(flags & LIRA_SCAN_PER_PARTITION) &&
+                 (op.rescan == 1 || (op.rescan < 0 && (int64_t)pl.maxT * kTile >= 8192));
+    if (pl.prescan) {
+        pl.rq_cap = (int)std::min<int64_t>(INT32_MAX / 2, 2 * nq + 4096);
+        pl.rcap = (int)std::max<int64_t>(256, (4 * k + 63) / 64 * 64);
+    }
+    pl.scap = pl.rs && !(flags & LIRA_SCAN_PER_PARTITION) ? (op.spill < 0 ? 256 : op.spill) : 0;
     size_t o = 0;
     auto take = [&](size_t bytes) {
         size_t at = o;
@@ -2135,6 +2262,8 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
                                   // [19] group 0's chunk size, [20] the most chunks of a bucket,
                                   // [21] group 0's first chunk size, [64..127] the seed's work estimates
     pl.off_done = take(pl.near0 > 0 ? (size_t)(pl.max_qblk + 1) * 4 : 0);  // per query block: first chunk done
+    pl.off_rst = take(pl.prescan ? (size_t)(2 * nq + 1) * 4 : 0);  // k_rescan: [rq_n, rcnt[nq], rfall[nq]]
+    pl.off_scnt = take(pl.scap ? (size_t)nq * 4 : 0);
     pl.off_qoff = take((nl + 1) * 4);
     pl.off_item = take((nl + 1) * 4);
     pl.off_nch = take(nl * 4);
@@ -2150,6 +2279,9 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     pl.off_qbound = take((size_t)nq * 4);
     pl.off_pqn = take((size_t)npairs * 4);
     pl.off_pe = take((size_t)npairs * pl.nch_max * 4);  // k_screen_m: the error bound of each row list
+    pl.off_rq = take((size_t)pl.rq_cap * 16);
+    pl.off_rbuf = take((size_t)nq * pl.rcap * 8);
+    pl.off_spill = take((size_t)nq * pl.scap * 16);
     pl.total = o;
     return pl;
 }
@@ -2439,7 +2571,8 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     a.nch_max = pl.nch_max;
     a.stats = idx->stats_on ? (unsigned long long *)idx->stats : nullptr;
     hipError_t e;
-    if (pl.rs && fused && centred && qbound && pl.bpc <= 128 && pl.bpc_near <= 128) {
+    bool spilled = false;
+    if (pl.rs && plive && pl.pp && centred && qbound && pl.bpc <= 128 && pl.bpc_near <= 128) {
         RArgs r;
         r.Xb = (const char *)idx->Xb;
         r.xadj = idx->xadjc;
@@ -2471,6 +2604,10 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
         r.invF = std::nextafter((float)((1.0 / (1.0 - g)) * (1.0 + 0x1p-50)), INFINITY);
         r.stats = a.stats;
         r.done0 = groups == 2 && pl.near0 > 0 ? (int32_t *)(w + pl.off_done) : nullptr;
+        r.spill = pl.scap ? (uint4 *)(w + pl.off_spill) : nullptr;
+        r.scnt = pl.scap ? (unsigned *)(w + pl.off_scnt) : nullptr;
+        r.scap = pl.scap;
+        spilled = r.spill != nullptr;
         e = launch_rscreen(r, pl.grid, st);
     } else {
         e = idx->metric == LIRA_METRIC_L2 ? launch_screen_rl<LIRA_METRIC_L2>(a, pl, st)
@@ -2519,6 +2656,51 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     m.stats = a.stats;
     m.split = pl.split;
     m.unsorted = 0;
+    m.rmode = 0;
+    m.spill = spilled ? (const uint4 *)(w + pl.off_spill) : nullptr;
+    m.scnt = spilled ? (const unsigned *)(w + pl.off_scnt) : nullptr;
+    m.scap = pl.scap;
+    if (pl.prescan && qbound) {
+        unsigned *rst = (unsigned *)(w + pl.off_rst);
+        m.rq_n = rst;
+        m.rcnt = rst + 1;
+        m.rfall = rst + 1 + nq;
+        m.rq = (int4 *)(w + pl.off_rq);
+        m.rq_cap = pl.rq_cap;
+        m.rbuf = (const u64 *)(w + pl.off_rbuf);
+        m.rcap = pl.rcap;
+        m.rmode = 1;  // queue the chunks to re-scan
+        if (idx->metric == LIRA_METRIC_L2)
+            launch_smerge<LIRA_METRIC_L2>(Rm, m, st);
+        else
+            launch_smerge<LIRA_METRIC_IP>(Rm, m, st);
+        LIRA_HIP_TRY(hipGetLastError());
+        RescanArgs ra;
+        ra.rq = m.rq;
+        ra.rq_n = m.rq_n;
+        ra.Q = q;
+        ra.Xr = idx->Xr;
+        ra.ids = idx->ids;
+        ra.tile_off = idx->tile_off;
+        ra.head = head;
+        ra.qbound = qbound;
+        ra.rbuf = (u64 *)(w + pl.off_rbuf);
+        ra.rcnt = m.rcnt;
+        ra.rfall = m.rfall;
+        ra.d = idx->d;
+        ra.rq_cap = pl.rq_cap;
+        ra.maxT = pl.maxT;
+        ra.groups = groups;
+        ra.bpc = pl.bpc;
+        ra.rcap = pl.rcap;
+        const dim3 rg((unsigned)(8 * cu_count_s(idx->device)));
+        if (idx->metric == LIRA_METRIC_L2)
+            hipLaunchKernelGGL(k_rescan<LIRA_METRIC_L2>, rg, dim3(256), 0, st, ra);
+        else
+            hipLaunchKernelGGL(k_rescan<LIRA_METRIC_IP>, rg, dim3(256), 0, st, ra);
+        LIRA_HIP_TRY(hipGetLastError());
+        m.rmode = 2;
+    }
     if (idx->metric == LIRA_METRIC_L2)
         launch_smerge<LIRA_METRIC_L2>(Rm, m, st);
     else

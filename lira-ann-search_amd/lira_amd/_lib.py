@@ -26,7 +26,8 @@ LIRA_SCAN_NO_SPLIT = 32
 # lira_index_set_option keys (include/lira_hip.h LIRA_OPT_*)
 OPTIONS = {"keep_tiles": 1, "screen": 2, "split": 3, "qr": 4, "two_phase": 5, "prune": 6, "seed": 7,
            "share": 8, "rounds": 9, "near_rounds": 10, "mfma": 11, "debug": 12, "pipeline": 13, "ring": 14, "probes_hint": 15, "xhi": 16,
-           "order": 17, "wide": 18, "rscreen": 19, "near_first": 20}
+           "order": 17, "wide": 18, "rscreen": 19, "near_first": 20,
+           "rescan": 21, "spill": 22}
 LIRA_PROBE_NEAREST = 0
 LIRA_PROBE_THRESHOLD_GE = 1
 LIRA_PROBE_THRESHOLD_GT = 2

@@ -91,6 +91,13 @@ def check_vs_oracle(x, q, d2b, probe, b, k, metric, dedup=True):
         D, I, nc = run(idx, q, probe, k, dedup=dedup)
         idx.set_option("rscreen", 1)
         assert np.array_equal(I, Io) and np.array_equal(bits(D), bits(Do)), "differ (rscreen=0)"
+    # the merge's chunk re-scans queued for k_rescan (LIRA_OPT_RESCAN = 1) and inline (0);
+    # k_screen_r without its spill lists (its full lists then re-scanned)
+    for name, v in (("rescan", 1), ("rescan", 0), ("spill", 0)):
+        idx.set_option(name, v)
+        D, I, nc = run(idx, q, probe, k, dedup=dedup)
+        idx.set_option(name, -1)
+        assert np.array_equal(I, Io) and np.array_equal(bits(D), bits(Do)), f"differ ({name}={v})"
     if k <= 120:
         # the compact index (no fp32 tiles: row-major + split-bf16 copies only)
         idc = make_index(x, d2b, b, metric, keep_tiles=False)
@@ -337,11 +344,30 @@ def test_screen_duplicate_rows_force_exact_rescan(metric):
     probe = np.tile(np.arange(b, dtype=np.int32), (q.shape[0], 1))
     check_vs_oracle(x, q, d2b, probe, b, 10, metric)
     idx2 = check_vs_oracle(x, q, d2b, probe, b, 10, metric, dedup=False)
+    # (k_screen_m: k_screen_r, the L2 default, spills its full lists' evicted keys instead;
+    # with no spill list (0) or one that overflows (1 record) it re-scans them too)
+    D_, I_, _ = run(idx2, q, probe, 10, dedup=False)
+    for sp in (0, 1):
+        idx2.set_option("spill", sp)
+        D2, I2, _ = run(idx2, q, probe, 10, dedup=False)
+        assert np.array_equal(I2, I_) and np.array_equal(bits(D2), bits(D_)), ("spill", sp)
+    idx2.set_option("spill", -1)
+    idx2.set_option("rscreen", 0)
     idx2.set_stats(True)
-    run(idx2, q, probe, 10)
+    run(idx2, q, probe, 10, dedup=False)
     st = idx2.stats_read()
     idx2.set_stats(False)
     assert st["rescans"] > 0
+    # the same re-scans through k_rescan: same results, same count
+    idx2.set_option("rescan", 1)
+    idx2.set_stats(True)
+    D1, I1, _ = run(idx2, q, probe, 10, dedup=False)
+    st1 = idx2.stats_read()
+    idx2.set_stats(False)
+    idx2.set_option("rescan", 0)
+    D0, I0, _ = run(idx2, q, probe, 10, dedup=False)
+    assert st1["rescans"] == st["rescans"]
+    assert np.array_equal(I1, I0) and np.array_equal(bits(D1), bits(D0))
     off, ids = oracle.build_csr(d2b, b)
     met = oracle.IP if metric == "inner_product" else oracle.L2
     Dq, Iq = oracle.scan_per_partition(q, off, ids, oracle.gather_lists(x, off, ids), probe, 10, met)
@@ -380,7 +406,7 @@ def test_options_do_not_change_results(metric):
     for name, vals in (("qr", (128,)), ("two_phase", (0, 2)), ("seed", (0,)), ("share", (0,)),
                        ("prune", (0,)), ("split", (0,)), ("mfma", (0, 2)), ("rounds", (1, 64)),
                        ("near_rounds", (2, 8)), ("screen", (0,)), ("probes_hint", (1, 4)), ("xhi", (0, 1, 2)),
-                       ("rscreen", (0,))):
+                       ("rscreen", (0,)), ("rescan", (0, 1)), ("spill", (0, 1, 4))):
         old = idx.get_option(name)
         for v in vals:
             idx.set_option(name, v)
