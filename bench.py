@@ -15,6 +15,12 @@ Scaling: ``weak`` (default) gives every rank its own batch of --nq queries;
 .shard_bounds), so at N = 1 it is the same workload and at N = 8 each rank scans
 nq/8 queries.  value = queries of all ranks / max-over-ranks time.
 
+Partition shards (--shard partitions): rank r builds only the lists of the
+buckets partition_owners gives it (B/N of the data), all ranks rank and scan
+the same batch, and a step ends with the all-gather of the N per-rank top-k
+and their k-way merge on the device (lira_merge_shards): value = the batch's
+queries / max-over-ranks time (strong scaling).
+
 Multi-GPU: `python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the
 environment starts N ranks itself (a child `python -m torch.distributed.run
 --nproc-per-node N ... bench.py` process; this parent never touches the GPU and
@@ -80,6 +86,12 @@ def parse():
     ap.add_argument("--no-pipeline", action="store_true", help="skip the MLP-probed pipeline timing")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo only to rehearse N>1 on one GPU")
+    ap.add_argument("--shard", default="queries", choices=["queries", "partitions"],
+                    help="queries (default): every rank holds the whole index and scans its own queries; "
+                         "partitions: rank r holds the lists of its buckets only (lira_amd.distributed."
+                         "partition_owners), every rank scans the whole batch against them, and the ranks' "
+                         "top-k are all-gathered and merged on the device (lira_merge_shards) -- SURVEY 8(e)'s "
+                         "mode for BIGANN's memory; strong scaling by construction")
     return ap.parse_args()
 
 
@@ -592,6 +604,181 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
     return out
 
 
+def run_partition_shard(args, data, rank, world, gpu, dev, dist):
+    """--shard partitions: this rank's buckets only, the whole batch, all-gather +
+    device k-way merge inside the timed step.  Checked after the timed loop: each
+    rank's own result against the oracle on a sample (its own lists), the merge
+    against lira_merge_shards' numpy restatement on that sample, and (configs whose
+    full index fits beside the shard) the whole batch against a full index on rank 0."""
+    from lira_amd import PartitionedIndex, RankWorkspace, rank_nearest
+    from lira_amd.distributed import bucket_sizes, merge_shards, partition_owners, shard_assignment
+    from lira_amd.synthetic import CONFIGS, N_MUL, workload
+    N, d, B, nprobe, k, metric, nq_default = CONFIGS[args.config]
+    n_mul = N_MUL.get(args.config, 1)
+    nq = args.nq or nq_default
+    opts = parse_opts(args.opt, args.config)
+    t0 = time.time()
+    x, centres, assign, make_queries = workload(args.config, args.seed, dev, data)
+    a2 = assign if assign.dim() == 2 else assign[:, None]
+    del assign
+    sizes_all = bucket_sizes(a2, B)
+    owners = partition_owners(sizes_all, world)
+    mine = shard_assignment(a2, owners, rank)
+    if args.config != "bigann100m":
+        a_full = a2
+    else:
+        a_full = None
+        del a2
+    index = PartitionedIndex(d, metric, gpu, **opts).build(mine, x, B)
+    del mine
+    q = make_queries(nq, args.seed + 101)  # the same batch on every rank
+    torch.cuda.synchronize()
+    owned_rows = int(sizes_all[owners == rank].sum())
+    log(f"[rank {rank}] partition shard {args.config}/{data}: {int((owners == rank).sum())} of {B} buckets, "
+        f"{owned_rows} of {int(sizes_all.sum())} list rows, index {index.memory_bytes() / 1e9:.1f} GB, "
+        f"built in {time.time() - t0:.1f}s")
+    gdev = dev if args.backend == "nccl" else torch.device("cpu")
+    ws = RankWorkspace(max(1, nq), B, dev)
+    probe = torch.empty((nq, nprobe), dtype=torch.int32, device=dev)
+    D = torch.empty((nq, k), dtype=torch.float32, device=dev)
+    I = torch.empty((nq, k), dtype=torch.int64, device=dev)
+    ncand = torch.empty(nq, dtype=torch.int64, device=dev)
+    Dall = torch.empty((world, nq, k), dtype=torch.float32, device=gdev)
+    Iall = torch.empty((world, nq, k), dtype=torch.int64, device=gdev)
+    Dm = torch.empty((nq, k), dtype=torch.float32, device=dev)
+    Im = torch.empty((nq, k), dtype=torch.int64, device=dev)
+
+    def local_step():
+        rank_nearest(q, centres, nprobe, out=probe, workspace=ws)
+        index.search(q, probe, k, dedup=True, out=(D, I, ncand))
+
+    graph = None
+    if args.graph:
+        for _ in range(2):
+            local_step()
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            local_step()
+        torch.cuda.synchronize()
+
+    def step():
+        if graph is not None:
+            graph.replay()
+        else:
+            local_step()
+        if world == 1:
+            return D, I
+        if args.backend == "nccl":
+            dist.all_gather_into_tensor(Dall, D)
+            dist.all_gather_into_tensor(Iall, I)
+            merge_shards(Dall, Iall, metric, True, out=(Dm, Im))
+        else:
+            gd = [torch.empty((nq, k), dtype=torch.float32) for _ in range(world)]
+            gi = [torch.empty((nq, k), dtype=torch.int64) for _ in range(world)]
+            dist.all_gather(gd, D.cpu())
+            dist.all_gather(gi, I.cpu())
+            merge_shards(torch.stack(gd).to(dev), torch.stack(gi).to(dev), metric, True, out=(Dm, Im))
+        return Dm, Im
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    index.check()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], device=gdev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    Dr, Ir = step()  # the merged result (world > 1: every rank's shard in it)
+    Dr, Ir = Dr.clone(), Ir.clone()
+    torch.cuda.synchronize()
+    # per-phase kernel times of this rank (the same step launched one by one, untimed)
+    index.set_profiling(True)
+    for _ in range(args.steps):
+        local_step()
+    torch.cuda.synchronize()
+    prof = index.profile_read()
+    index.set_profiling(False)
+    calls = max(1, prof["calls"])
+    merge_ms, Dp, Ip = None, None, None
+    if world > 1:  # every rank's own (nq, k) result, gathered once more for the checks
+        if args.backend == "nccl":
+            dist.all_gather_into_tensor(Dall, D)
+            dist.all_gather_into_tensor(Iall, I)
+            Dst, Ist = Dall, Iall
+        else:
+            gd = [torch.empty((nq, k), dtype=torch.float32) for _ in range(world)]
+            gi = [torch.empty((nq, k), dtype=torch.int64) for _ in range(world)]
+            dist.all_gather(gd, D.cpu())
+            dist.all_gather(gi, I.cpu())
+            Dst, Ist = torch.stack(gd).to(dev), torch.stack(gi).to(dev)
+        s = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(20):
+            merge_shards(Dst, Ist, metric, True, out=(Dm, Im))
+        e1.record(s)
+        torch.cuda.synchronize()
+        merge_ms = e0.elapsed_time(e1) / 20
+        Dp, Ip = Dst.cpu().numpy(), Ist.cpu().numpy()
+
+    # ---- checks (after timing): own shard vs oracle sample, merge restatement, full index
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    ns = min(32 if args.config == "bigann100m" else args.recall_sample, nq)
+    rows = np.r_[0:ns // 2, nq - (ns - ns // 2):nq]
+    cache = {}
+
+    def lists(b):
+        if b not in cache:
+            cache[b] = index.list_ids(b)
+        return cache[b]
+
+    Do, Io = oracle_sample(oracle, index, x, q, probe, rows, k, metric, lists)
+    own_ok = bool(np.array_equal(Io, I.cpu().numpy()[rows]) and
+                  np.array_equal(Do.view(np.uint32), D.cpu().numpy()[rows].view(np.uint32)))
+    merge_ok, full_ok = None, None
+    if world > 1:
+        Dref, Iref = oracle.merge_shards(Dp[:, rows], Ip[:, rows], metric == "inner_product", True, k)
+        merge_ok = bool(np.array_equal(Iref, Ir.cpu().numpy()[rows]) and
+                        np.array_equal(Dref.view(np.uint32), Dr.cpu().numpy()[rows].view(np.uint32)))
+        flags = torch.tensor([int(own_ok), int(merge_ok)], dtype=torch.int32, device=gdev)
+        dist.all_reduce(flags, op=dist.ReduceOp.MIN)
+        own_ok, merge_ok = bool(flags[0].item()), bool(flags[1].item())
+    if rank == 0 and a_full is not None:
+        full = PartitionedIndex(d, metric, gpu, **opts).build(a_full, x, B)
+        Df, If, _ = full.search(q, probe, k, dedup=True)
+        full_ok = bool(torch.equal(If, Ir) and torch.equal(Df.view(torch.int32), Dr.view(torch.int32)))
+        del full
+    out = {"data": data, "value": nq * args.steps / elapsed, "unit": "queries/s", "ms_per_step": elapsed / args.steps * 1e3,
+           "queries_per_rank": nq, "kernel": index.describe(nq, nprobe, k),
+           "launch": "hip_graph" if graph is not None else "stream",
+           "index_bytes": index.memory_bytes(), "n_mul": n_mul, "index_options": opts,
+           "kernels_ms_per_step": {"plan": prof["plan_ms"] / calls, "scan": prof["scan_ms"] / calls,
+                                   "merge": prof["merge_ms"] / calls, "merge_shards": merge_ms},
+           "partition_shard": {"buckets_owned": int((owners == rank).sum()), "rows_owned": owned_rows,
+                               "rows_total": int(sizes_all.sum()),
+                               "rows_per_rank": [int(sizes_all[owners == r].sum()) for r in range(world)],
+                               "own_shard_vs_oracle_sample": own_ok, "merge_vs_restatement_sample": merge_ok,
+                               "merged_equals_full_index": full_ok, "sample_rows": int(len(rows)),
+                               "note": "rank 0's figures; every rank ranks and scans the whole batch against its "
+                                       "own buckets, then all-gather (RCCL) + lira_merge_shards inside the timed "
+                                       "step; merged_equals_full_index: whole batch vs a full index on rank 0 "
+                                       "(None for BIGANN: the full index does not fit beside the shard)"}}
+    del index, x
+    return out
+
+
 def sweep_options(args, index, local_step, D, I, nq, nprobe, k):
     """Per option value: scan/merge/plan ms (HIP events, `args.steps` steps) and
     whether the batch's output is bit-identical to the default run's."""
@@ -787,9 +974,13 @@ def main():
     from lira_amd.synthetic import CONFIGS, LATENT_DIM
 
     N, d, B, nprobe, k, metric, nq_default = CONFIGS[args.config]
-    head = run_workload(args, args.data, rank, world, gpu, dev, dist, primary=True)
+    if args.shard == "partitions":
+        args.scaling = "strong"  # one batch over the ranks' buckets
+        head = run_partition_shard(args, args.data, rank, world, gpu, dev, dist)
+    else:
+        head = run_workload(args, args.data, rank, world, gpu, dev, dist, primary=True)
     contrast = None
-    if args.contrast == "auto" and world == 1 and args.config in ("sift1m", "gist1m"):
+    if args.contrast == "auto" and world == 1 and args.config in ("sift1m", "gist1m") and args.shard == "queries":
         torch.cuda.empty_cache()
         other = "latent" if args.data == "mixture" else "mixture"
         contrast = run_workload(args, other, rank, world, gpu, dev, dist, primary=False)
@@ -820,14 +1011,16 @@ def main():
                        "metric": metric, "n_mul": head["n_mul"],
                        "queries_per_step": nq_job * (world if args.scaling == "weak" else 1),
                        "queries_per_rank": head["queries_per_rank"],
-                       "parallelism": f"query-shard x{world} (index replicated)"},
+                       "parallelism": f"query-shard x{world} (index replicated)" if args.shard == "queries"
+                       else f"partition-shard x{world} (each rank its buckets' lists; all-gather + k-way merge)"},
             "other_scaling": head.get("other_scaling"),
             "allgather_verified": head.get("allgather_verified"),
             "roofline": head.get("roofline"),
             "cpu_baseline": head.get("cpu_baseline"),
             **{key: head[key] for key in ("kernels_ms_per_step", "kernel", "index_bytes", "index_options", "pipeline",
                                           "rank_gemm", "exact_kernel", "candidates_per_query", "parity_sample",
-                                          "parity_bit_exact", "recall_at_k", "recall_gate", "recall_note")
+                                          "parity_bit_exact", "recall_at_k", "recall_gate", "recall_note",
+                                          "partition_shard")
                if key in head},
             "contrast_data": contrast,
         }

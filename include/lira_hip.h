@@ -213,6 +213,24 @@ int lira_index_get_option(const lira_index *idx, int option, int64_t *value);
 /* 1 if the index holds the fp32 tile copy (LIRA_OPT_KEEP_TILES at build time) */
 int lira_index_has_tiles(const lira_index *idx, int *out);
 
+/* ------------------------------------------------- partition shards */
+/*
+ * k-way merge of per-shard top-k results: the exchange step of the
+ * partition-sharded search (each rank holds the lists of its
+ * own buckets, scans them for every query, and the ranks' (nq, k) results are
+ * all-gathered and merged).  Each shard's lists hold a disjoint set of
+ * (bucket, row) entries, so the k smallest keys of the union equal the
+ * single-index result of search.cpp:495-514's top-k over all candidates.
+ *   D, I      device (nparts, nq, k): fp32 / int64, each (nq, k) block in
+ *             lira_scan_topk's output convention (sorted, -1 / +-inf pads)
+ *   nparts    1..64 shards;  metric  LIRA_METRIC_L2 / _IP (the order)
+ *   dedup     1: a gid reached through buckets of two shards is kept once
+ *             (the scan's LIRA_SCAN_DEDUP across shards); 0: both kept
+ *   out_D/I   device (nq, k), same convention.  Stream-ordered, capturable.
+ */
+int lira_merge_shards(const float *D, const int64_t *I, int64_t nparts, int64_t nq, int64_t k, int metric,
+                      int dedup, float *out_D, int64_t *out_I, void *stream);
+
 /* ----------------------------------------------------------- ranking */
 /*
  * Query -> centroid Euclidean distances, exact fp32 in search.cpp's order:

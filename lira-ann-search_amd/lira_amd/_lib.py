@@ -71,6 +71,7 @@ SIGNATURES = {
     "lira_rank_nearest": (_INT, [_P, _I64, _P, _I64, _I64, _I64, _P, _P, _SZ, _P]),
     "lira_select_probes": (_INT, [_P, _I64, _I64, _INT, _F, _I64, _P, _P, _P]),
     "lira_order_probes": (_INT, [_P, _I64, _I64, _P, _I64, _P]),
+    "lira_merge_shards": (_INT, [_P, _P, _I64, _I64, _I64, _INT, _INT, _P, _P, _P]),
     "lira_scan_workspace_size": (_INT, [_P, _I64, _I64, _I64, ctypes.c_uint, ctypes.POINTER(_SZ)]),
     "lira_scan_topk": (_INT, [_P, _P, _I64, _P, _I64, _I64, ctypes.c_uint, _P, _P, _P, _P, _SZ, _P]),
     "lira_scan_describe": (_INT, [_P, _I64, _I64, _I64, ctypes.c_uint, ctypes.c_char_p, _SZ]),

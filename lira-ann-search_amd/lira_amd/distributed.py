@@ -8,11 +8,22 @@ all-gathered so every rank (the caller on rank 0 in particular) sees the whole
 batch's results.  That all-gather is the path's only exchange step: 12 bytes x
 k per query (1.2 MB for 10k queries at k=10), far below xGMI link rates.
 
+Partition sharding (SURVEY.md 8(e)'s alternative for BIGANN's memory): rank r
+holds only the lists of the buckets `partition_owners` gives it (balanced by
+list size), every rank ranks and scans the WHOLE query batch against its own
+lists (a probe into another rank's bucket finds an empty list), and the ranks'
+(nq, k) results are all-gathered and k-way merged on the device
+(lira_merge_shards).  The lists of different ranks are disjoint, so the merge
+of the per-rank exact top-k is the single-index result bit for bit.
+
 The reference has no distributed code (single GPU chosen by
 nvidia-smi, utils.py:90-96); this module is new.
 """
 from __future__ import annotations
 
+import ctypes
+
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -60,3 +71,82 @@ def sharded_search(search_fn, q_all: torch.Tensor, group=None, gather_device=Non
     if gather_device is not None:
         D, I = D.to(gather_device), I.to(gather_device)
     return all_gather_rows(D, n, world, group), all_gather_rows(I, n, world, group)
+
+
+# ---- partition sharding ---------------------------------------------------------
+
+def partition_owners(list_sizes, world: int) -> np.ndarray:
+    """Owner rank of every bucket: largest lists first, each to the least-loaded
+    rank so far (ties -> smaller bucket id, then smaller rank).  Deterministic, so
+    every rank computes the same map from the same sizes."""
+    if world <= 0:
+        raise ValueError("world must be >= 1")
+    sizes = np.asarray(list_sizes, dtype=np.int64)
+    order = np.lexsort((np.arange(sizes.size), -sizes))
+    load = np.zeros(world, dtype=np.int64)
+    owner = np.empty(sizes.size, dtype=np.int32)
+    for b in order:
+        r = int(np.argmin(load))
+        owner[b] = r
+        load[r] += sizes[b]
+    return owner
+
+
+def bucket_sizes(data_2_bkt: torch.Tensor, n_lists: int) -> np.ndarray:
+    """Rows per bucket of an (N,) / (N, n_mul) assignment (-1 = empty slot), on its device."""
+    flat = data_2_bkt.reshape(-1)
+    flat = flat[flat >= 0].to(torch.int64)
+    return torch.bincount(flat, minlength=n_lists).cpu().numpy()
+
+
+def shard_assignment(data_2_bkt: torch.Tensor, owners, rank: int) -> torch.Tensor:
+    """The assignment restricted to this rank's buckets: other buckets' slots -> -1
+    (lira_index_build's empty slot), so the rank's index holds only its own lists."""
+    own = torch.as_tensor(np.asarray(owners) == rank, device=data_2_bkt.device)
+    d2b = data_2_bkt.to(torch.int64)
+    keep = (d2b >= 0) & own[d2b.clamp(min=0)]
+    return torch.where(keep, data_2_bkt, torch.full_like(data_2_bkt, -1))
+
+
+def merge_shards(D_parts: torch.Tensor, I_parts: torch.Tensor, metric: str = "L2", dedup: bool = True,
+                 out=None, stream=None):
+    """k-way merge of (P, nq, k) per-shard top-k results on the device
+    (lira_merge_shards): the k smallest keys of the union in the scan's order."""
+    from . import _lib
+    from .index import METRICS, normalize_metric
+    P, nq, k = D_parts.shape
+    if I_parts.shape != D_parts.shape:
+        raise ValueError("D_parts and I_parts must have the same (P, nq, k) shape")
+    D_parts = D_parts.contiguous()
+    I_parts = I_parts.contiguous()
+    if out is None:
+        out = (torch.empty((nq, k), dtype=torch.float32, device=D_parts.device),
+               torch.empty((nq, k), dtype=torch.int64, device=D_parts.device))
+    with torch.cuda.device(D_parts.device):
+        _lib.call("lira_merge_shards", _lib.ptr(D_parts), _lib.ptr(I_parts), P, nq, k,
+                  METRICS[normalize_metric(metric)], int(bool(dedup)), _lib.ptr(out[0]), _lib.ptr(out[1]),
+                  _lib.stream_ptr(stream))
+    return out
+
+
+def gather_shards(D: torch.Tensor, I: torch.Tensor, world: int, group=None, gather_device=None):
+    """All-gather every rank's (nq, k) result into (world, nq, k) tensors (rank order)."""
+    dev = gather_device or D.device
+    gd = [torch.empty_like(D, device=dev) for _ in range(world)]
+    gi = [torch.empty_like(I, device=dev) for _ in range(world)]
+    dist.all_gather(gd, D.to(dev), group=group)
+    dist.all_gather(gi, I.to(dev), group=group)
+    return torch.stack(gd), torch.stack(gi)
+
+
+def partition_sharded_search(index, q: torch.Tensor, probe: torch.Tensor, k: int, dedup: bool = True,
+                             group=None, gather_device=None):
+    """This rank's index holds its buckets' lists only (shard_assignment): scan the
+    whole batch against them, all-gather the ranks' top-k and merge on q's device.
+    Returns the batch's (D, I) on every rank."""
+    D, I, _ = index.search(q, probe, k, dedup=dedup)
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if world == 1:
+        return D, I
+    Dp, Ip = gather_shards(D, I, world, group, gather_device)
+    return merge_shards(Dp.to(q.device), Ip.to(q.device), index.metric, dedup)

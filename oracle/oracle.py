@@ -236,3 +236,27 @@ def recall_at_k(found_ids, gt_ids, k):
         s = set(int(v) for v in found_ids[i] if v >= 0)
         out[i] = sum(int(g) in s for g in gt_ids[i, :k]) / k
     return out
+
+
+def merge_shards(Dp, Ip, ip, dedup, k):
+    """lira_merge_shards restated (test infrastructure): the k smallest keys of the
+    union of P per-shard (nq, k) top-k lists in search.cpp:495-514's order --
+    ascending (score, gid), score = D for L2 and -D for IP -- equal keys (a row
+    reached through buckets of two shards) kept once with dedup.  Pads: I = -1."""
+    Dp, Ip = np.asarray(Dp), np.asarray(Ip)
+    P, nq = Dp.shape[0], Dp.shape[1]
+    outD = np.full((nq, k), -np.inf if ip else np.inf, dtype=np.float32)
+    outI = np.full((nq, k), -1, dtype=np.int64)
+    for qi in range(nq):
+        keys = sorted((float(-Dp[p, qi, j]) if ip else float(Dp[p, qi, j]), int(Ip[p, qi, j]), Dp[p, qi, j])
+                      for p in range(P) for j in range(Dp.shape[2]) if Ip[p, qi, j] >= 0)
+        out, last = 0, None
+        for sc, gid, dv in keys:
+            if out == k:
+                break
+            if dedup and last == (sc, gid):
+                continue
+            outD[qi, out], outI[qi, out] = dv, gid
+            out += 1
+            last = (sc, gid)
+    return outD, outI
