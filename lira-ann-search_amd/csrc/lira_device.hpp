@@ -431,4 +431,30 @@ __device__ __forceinline__ void emit_list(const u64 (&lst)[R], int k, int dedup,
     for (int e = outpos + lane; e < k; e += 64) emit_key(kEmptyKey, metric, D + e, I + e);
 }
 
+// ---- stream-ordered fill of 32-bit words (instead of hipMemsetAsync) ----
+// The search path's per-call resets (plan counters, flags, the seed bound) are a
+// kernel of our own: a hipMemsetAsync captured into a HIP graph replayed into an
+// illegal-address fault once the same memset had also run eagerly after the
+// capture (graph replay after an eager call of the library faulted on MI355X,
+// ROCm 7.2; replays back to back did not).  A kernel node is ordered and
+// self-contained like every other node of the step.
+static __global__ __launch_bounds__(256) void k_fill32(uint32_t *p, uint32_t v, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * 256 * 4;
+    for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += stride) {
+        if (i + 4 <= n) {
+            *(uint4 *)(p + i) = make_uint4(v, v, v, v);
+        } else {
+            for (int64_t j = i; j < n; ++j) p[j] = v;
+        }
+    }
+}
+// bytes: a multiple of 4, p 16-B aligned (workspace offsets are 256-B aligned)
+static inline hipError_t fill32_async(void *p, uint32_t v, size_t bytes, hipStream_t st) {
+    const int64_t n = (int64_t)(bytes / 4);
+    if (n <= 0) return hipSuccess;
+    const int64_t blocks = (n + 1023) / 1024;
+    hipLaunchKernelGGL(k_fill32, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, st, (uint32_t *)p, v, n);
+    return hipGetLastError();
+}
+
 }  // namespace lira

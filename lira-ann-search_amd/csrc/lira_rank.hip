@@ -668,7 +668,7 @@ int lira_centroid_gemm(const float *q, int64_t nq, const float *centroids, int64
     if (nq == 0) return LIRA_OK;
     if (!q || !centroids || !out_sq) return fail(LIRA_EINVAL, "NULL buffer");
     hipStream_t st = (hipStream_t)stream;
-    if (out_err && n_centroids > 64) LIRA_HIP_TRY(hipMemsetAsync(out_err, 0, nq * 4, st));  // (max over column blocks)
+    if (out_err && n_centroids > 64) LIRA_HIP_TRY(fill32_async(out_err, 0u, nq * 4, st));  // (max over column blocks)
     dim3 grid((unsigned)((nq + 63) / 64), (unsigned)((n_centroids + 63) / 64));
     if (d % 4 == 0 && ((uintptr_t)q & 15) == 0 && ((uintptr_t)centroids & 15) == 0)
         hipLaunchKernelGGL(k_centroid_gemm<true>, grid, dim3(256), 0, st, q, nq, centroids,

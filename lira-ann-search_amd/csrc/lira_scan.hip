@@ -1152,8 +1152,8 @@ static int exact_topk(lira_index *idx, const float *q, int64_t nq, const int32_t
 
     if (ev[0]) LIRA_HIP_TRY(hipEventRecord(ev[0], st));
     // cnt, cursor and head are contiguous at the start of the workspace
-    LIRA_HIP_TRY(hipMemsetAsync(w, 0, pl.off_qoff, st));
-    if (qbound) LIRA_HIP_TRY(hipMemsetAsync(qbound, 0xff, (size_t)nq * 4, st));
+    LIRA_HIP_TRY(fill32_async(w, 0u, pl.off_qoff, st));
+    if (qbound) LIRA_HIP_TRY(fill32_async(qbound, ~0u, (size_t)nq * 4, st));
     const int64_t npairs = nq * nprobe;
     const int nl = (int)idx->n_lists;
     // Two groups when the pruning bound is on and partitions get >= 32 queries:

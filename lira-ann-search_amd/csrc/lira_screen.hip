@@ -2416,7 +2416,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     const int64_t npairs = nq * nprobe;
 
     if (ev[0]) LIRA_HIP_TRY(hipEventRecord(ev[0], st));
-    LIRA_HIP_TRY(hipMemsetAsync(w, 0, pl.off_qoff, st));  // cnt, cursor, head, done flags
+    LIRA_HIP_TRY(fill32_async(w, 0u, pl.off_qoff, st));  // cnt, cursor, head, done flags (not hipMemsetAsync: lira_device.hpp)
     // Two groups (every query's first probe slot -- its nearest partition, where
     // most of its top-k lives -- queued ahead of the rest) when the bound is
     // shared across a query's items: later items then start from tight bounds.
@@ -2448,7 +2448,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     // loads for its nprobe pairs; k_pairs gives every pair its own 16 lanes --
     // measured GIST1M plan 0.160 -> 0.118 ms)
     const bool fused = plive && qbound && o.seed && idx->X && idx->metric == LIRA_METRIC_L2 && k <= 32 && idx->d <= 256;
-    if (qbound && !fused) LIRA_HIP_TRY(hipMemsetAsync(qbound, 0xff, (size_t)nq * 4, st));
+    if (qbound && !fused) LIRA_HIP_TRY(fill32_async(qbound, ~0u, (size_t)nq * 4, st));
     if (fused) {
         SeedPairs sp;
         sp.pivot = idx->pivot;

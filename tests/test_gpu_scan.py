@@ -494,3 +494,45 @@ def test_screen_clustered_filter_and_ties():
         idx.set_stats(False)
         assert st["blocks"] > 0
         assert st["pairs_pruned_plan"] > 0 and st["candidates_pruned_plan"] >= st["pairs_pruned_plan"]
+
+
+def test_graph_replay_after_eager_calls():
+    # a captured step replayed after eager calls of the same search (the per-call
+    # resets are a kernel of the library's own, not hipMemsetAsync: a captured memset
+    # replayed after an eager one faulted, lira_device.hpp fill32_async)
+    import torch
+    from lira_amd import PartitionedIndex, rank_nearest
+    dev = torch.device("cuda", 0)
+    x, q, d2b, probe = random_case(91, 20000, 32, 16, 500, 4, "L2")
+    c = torch.from_numpy(np.stack([x[d2b[:, 0] == b].mean(0) for b in range(16)]).astype(np.float32)).to(dev)
+    xt, qt = torch.from_numpy(x).to(dev), torch.from_numpy(q).to(dev)
+    for keep in (True, False):
+        idx = PartitionedIndex(32, "L2", 0, keep_tiles=int(keep)).build(torch.from_numpy(d2b).to(dev), xt, 16)
+        pr = torch.empty((500, 4), dtype=torch.int32, device=dev)
+        D = torch.empty((500, 10), dtype=torch.float32, device=dev)
+        I = torch.empty((500, 10), dtype=torch.int64, device=dev)
+        nc = torch.empty(500, dtype=torch.int64, device=dev)
+
+        def step():
+            rank_nearest(qt, c, 4, out=pr)
+            idx.search(qt, pr, 10, out=(D, I, nc))
+
+        step()
+        step()
+        torch.cuda.synchronize()
+        I0, D0 = I.clone(), D.clone()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            step()
+        for _ in range(3):
+            g.replay()
+        for prof in (False, True):
+            idx.set_profiling(prof)
+            for _ in range(3):
+                step()
+            idx.set_profiling(False)
+            I.zero_()
+            g.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(I, I0) and torch.equal(D.view(torch.int32), D0.view(torch.int32)), (keep, prof)
+        del g
