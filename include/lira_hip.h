@@ -176,7 +176,8 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *                        the 128-row seed's.  Results never depend on it.
  *   LIRA_OPT_RESCAN      chunks whose screened list may have dropped a candidate (its 32nd key
  *                        within the final bound's reach) are scanned exactly again: -1 (default)
- *                        auto -- 1 where a chunk holds >= 8192 rows (BIGANN-size lists), else 0;
+ *                        auto -- 1 where a chunk holds >= 8192 rows (32768 under k_screen_r, whose
+ *                        spill lists leave few re-scans: BIGANN-size lists), else 0;
  *                        1: a pass that queues them, then k_rescan over all of them at once (a
  *                        wave per 64-row tile), whose exact survivors the merge takes; 0: inside
  *                        the merge, one wave per query.  Results never depend on it.
@@ -185,6 +186,9 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *                        that no full list is re-scanned: -1 (default) 256; 0 none (full lists are
  *                        re-scanned as by k_screen_m); a query that overflows its records has its
  *                        full lists re-scanned instead.  Results never depend on it.
+ *   LIRA_OPT_SEED_TILES  tiles of 64 rows of the nearest list the exact seed bound reads (the
+ *                        unfused seed, fp32 tiles, L2, k <= 32): 0 (default) auto -- 1 for
+ *                        d > 512 (GIST1M), else 2; 1 or 2 fixed.  Results never depend on it.
  */
 #define LIRA_OPT_KEEP_TILES 1
 #define LIRA_OPT_SCREEN 2
@@ -208,6 +212,7 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
 #define LIRA_OPT_NEAR_FIRST 20
 #define LIRA_OPT_RESCAN 21
 #define LIRA_OPT_SPILL 22
+#define LIRA_OPT_SEED_TILES 23
 int lira_index_set_option(lira_index *idx, int option, int64_t value);
 int lira_index_get_option(const lira_index *idx, int option, int64_t *value);
 /* 1 if the index holds the fp32 tile copy (LIRA_OPT_KEEP_TILES at build time) */

@@ -1540,7 +1540,7 @@ __device__ __forceinline__ float seed_bound(const float *Q, const int32_t *probe
         if (nj == 64) {
             // two tiles per packed fp32 op (v_pk_add_f32 / v_pk_mul_f32 round
             // each half like the scalar ops: the same per-lane sums)
-            f2 acc2[NT / 2];
+            f2 acc2[NT / 2 > 0 ? NT / 2 : 1];
 #pragma unroll
             for (int t = 0; t < NT / 2; ++t) acc2[t] = (f2){acc[2 * t], acc[2 * t + 1]};
 #pragma unroll 16
@@ -1561,6 +1561,19 @@ __device__ __forceinline__ float seed_bound(const float *Q, const int32_t *probe
             for (int t = 0; t < NT / 2; ++t) {
                 acc[2 * t] = acc2[t].x;
                 acc[2 * t + 1] = acc2[t].y;
+            }
+            if (NT & 1) {  // (an odd tile: scalar)
+#pragma unroll 16
+                for (int jj = 0; jj < 64; ++jj) {
+                    const float qj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qv), jj));
+                    const float xv = xt[NT - 1][(j0 + jj) * kTile];
+                    if (METRIC == LIRA_METRIC_L2) {
+                        const float df = qj - xv;
+                        acc[NT - 1] = acc[NT - 1] + df * df;
+                    } else {
+                        acc[NT - 1] = acc[NT - 1] + qj * xv;
+                    }
+                }
             }
         } else {
             for (int jj = 0; jj < nj; ++jj) {
@@ -2242,8 +2255,11 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // the merge's chunk re-scans through k_rescan: where a chunk is long enough for
     // one wave per query to be the merge's tail (BIGANN-100M: 32k rows)
     pl.maxT = std::max(pl.bpc, pl.near0) * kSBT;
+    // (k_screen_r's spill lists leave it only the queries whose spill records
+    // overflow: worth the find pass only where a chunk is BIGANN-long; SIFT1M's
+    // 13k-row chunks paid ~7 us of merge for it)
     pl.prescan = !(flags & LIRA_SCAN_PER_PARTITION) &&
-                 (op.rescan == 1 || (op.rescan < 0 && (int64_t)pl.maxT * kTile >= 8192));
+                 (op.rescan == 1 || (op.rescan < 0 && (int64_t)pl.maxT * kTile >= (pl.rs ? 32768 : 8192)));
     if (pl.prescan) {
         pl.rq_cap = (int)std::min<int64_t>(INT32_MAX / 2, 2 * nq + 4096);
         pl.rcap = (int)std::max<int64_t>(256, (4 * k + 63) / 64 * 64);
@@ -2470,7 +2486,12 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
         LIRA_HIP_TRY(hipGetLastError());
     } else if (qbound && o.seed && idx->X) {  // from the fp32 tiles (coalesced)
         const dim3 g((unsigned)((nq + 3) / 4));
-        if (idx->metric == LIRA_METRIC_L2 && k <= 32)
+        // (LIRA_OPT_SEED_TILES: 64 rows instead of 128 where a row is long)
+        const int st_tiles = o.seed_tiles > 0 ? o.seed_tiles : idx->d > 512 ? 1 : 2;
+        if (idx->metric == LIRA_METRIC_L2 && k <= 32 && st_tiles == 1)
+            hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2, 1>), g, dim3(256), 0, st, q, probe, (int)nprobe,
+                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound, SeedPairs());
+        else if (idx->metric == LIRA_METRIC_L2 && k <= 32)
             hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2, 2>), g, dim3(256), 0, st, q, probe, (int)nprobe,
                                (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound, SeedPairs());
         else if (idx->metric == LIRA_METRIC_L2)

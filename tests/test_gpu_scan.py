@@ -406,7 +406,8 @@ def test_options_do_not_change_results(metric):
     for name, vals in (("qr", (128,)), ("two_phase", (0, 2)), ("seed", (0,)), ("share", (0,)),
                        ("prune", (0,)), ("split", (0,)), ("mfma", (0, 2)), ("rounds", (1, 64)),
                        ("near_rounds", (2, 8)), ("screen", (0,)), ("probes_hint", (1, 4)), ("xhi", (0, 1, 2)),
-                       ("rscreen", (0,)), ("rescan", (0, 1)), ("spill", (0, 1, 4))):
+                       ("rscreen", (0,)), ("rescan", (0, 1)), ("spill", (0, 1, 4)),
+                       ("seed_tiles", (1, 2))):
         old = idx.get_option(name)
         for v in vals:
             idx.set_option(name, v)
