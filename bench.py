@@ -1020,7 +1020,7 @@ def main():
             **{key: head[key] for key in ("kernels_ms_per_step", "kernel", "index_bytes", "index_options", "pipeline",
                                           "rank_gemm", "exact_kernel", "candidates_per_query", "parity_sample",
                                           "parity_bit_exact", "recall_at_k", "recall_gate", "recall_note",
-                                          "partition_shard")
+                                          "partition_shard", "sweep")
                if key in head},
             "contrast_data": contrast,
         }

@@ -2240,7 +2240,10 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     const bool two = !(flags & LIRA_SCAN_PER_PARTITION) && op.two_phase && nprobe >= 2 &&
                      (op.two_phase == 2 || nq >= (int64_t)pl.qr * idx->n_lists ||
                       nq * nprobe >= 4 * (int64_t)pl.qr * idx->n_lists);
-    if (two && op.near_rounds <= 0 && pl.mfma) {
+    // (k_screen_r on a full batch keeps its fixed group-0 chunks: the device-side
+    // choice measured SIFT1M mixture 0.242 -> 0.226 ms scan without it at 10 k
+    // queries, latent unchanged, but 2 % better with it at 1 250)
+    if (two && op.near_rounds <= 0 && pl.mfma && !(pl.rs && nq >= 4096)) {
         const int64_t est0 = std::min<int64_t>(nq, (nq + pl.qr - 1) / pl.qr + idx->n_lists);
         const int64_t split6 = std::max<int64_t>(1, ((pl.rs ? 3 : 6) * (int64_t)workers + est0 - 1) / std::max<int64_t>(1, est0));
         pl.bpc_near_min = (int)std::min<int64_t>(pl.bpc_near, std::max<int64_t>(1, (max_blocks + split6 - 1) / split6));
