@@ -1786,6 +1786,9 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
     const bool fall = a.rmode == 2 && a.rfall[q] != 0u;
     // lists + spills hold every key within reach: no list is re-scanned
     const bool sok = a.spill && !a.per_partition && a.scnt[q] <= (unsigned)a.scap;
+    // a list of the query whose last slot is within its limit: only then can an
+    // evicted key be needed (evicted keys lie above their list's final last key)
+    bool any_over = false;
 
     u64 lst[R];
     int pc = 0;  // pending survivors (storage rows) in pend[0..pc)
@@ -1866,10 +1869,12 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
                                       : err_E<METRIC>(qn_s, (double)a.rmax[p], dd, a.split, (double)a.dpad, a.centred);
                 lim = s_lim<METRIC>((double)T, E, dd);
                 const u64 last = src[K2 - 1];
-                over = !sok && last != kEmptyKey && (double)key_score(last) <= lim;  // (kUnsortedMark: a NaN score)
+                over = last != kEmptyKey && (double)key_score(last) <= lim;  // (kUnsortedMark: a NaN score)
                 uns = uns || last == kUnsortedMark;  // an unmerged row buffer (k_screen_m): walk to its first empty key
             }
-            bool active = p >= 0 && !over && a.rmode != 1;
+            // (with spill lists a full list is walked like any other; its evicted keys
+            // are in the spill list, read below only if some list of the query is full)
+            bool active = p >= 0 && (!over || sok) && a.rmode != 1;
             // four keys per round (two 16-B loads; K2 % 4 == 0, lists 32-B aligned):
             // the walk is one dependent load per round
             for (int e0 = 0; __any(active); e0 += 4) {
@@ -1892,6 +1897,8 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
                 }
             }
             u64 ov = __ballot(over);
+            any_over = any_over || ov != 0;
+            if (sok) continue;  // (no re-scans)
             if (a.rmode == 1) {  // queue them for k_rescan
                 if (ov) {
                     unsigned base = 0;
@@ -1960,7 +1967,7 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
         }
         take_lists(0, a.nprobe, T);
         if (a.rmode == 1) return;
-        if (sok) {  // the spilled keys within their lists' limits
+        if (sok && any_over) {  // the spilled keys within their lists' limits
             const int ns = (int)a.scnt[q];
             const uint4 *sp = a.spill + q * (int64_t)a.scap;
             for (int i0 = 0; i0 < ns; i0 += 64) {
