@@ -2225,7 +2225,9 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // per workgroup left the slowest workgroup with two (LIRA_OPT_NEAR_ROUNDS;
     // measured SIFT1M mixture scan 1.08 -> 1.04 ms at 2, slower at 4 and 8:
     // more lists, more survivors)
-    const int near_rounds = op.near_rounds > 0 ? op.near_rounds : pl.rs ? 1 : 2;
+    // (1 since round 4 for k_screen_m too, with its group-0 chunks fixed: DEEP10M scan
+    // 22.2 -> 21.5 ms, merge 0.32 -> 0.26 ms; GIST1M mixture scan -2 %, latent even)
+    const int near_rounds = op.near_rounds > 0 ? op.near_rounds : 1;
     {
         const int64_t est0 = std::min<int64_t>(nq, (nq + pl.qr - 1) / pl.qr + idx->n_lists);
         const int64_t split0 = std::max<int64_t>(1, ((int64_t)near_rounds * workers + est0 - 1) / std::max<int64_t>(1, est0));
@@ -2247,10 +2249,11 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     const bool two = !(flags & LIRA_SCAN_PER_PARTITION) && op.two_phase && nprobe >= 2 &&
                      (op.two_phase == 2 || nq >= (int64_t)pl.qr * idx->n_lists ||
                       nq * nprobe >= 4 * (int64_t)pl.qr * idx->n_lists);
-    // (k_screen_r on a full batch keeps its fixed group-0 chunks: the device-side
-    // choice measured SIFT1M mixture 0.242 -> 0.226 ms scan without it at 10 k
-    // queries, latent unchanged, but 2 % better with it at 1 250)
-    if (two && op.near_rounds <= 0 && pl.mfma && !(pl.rs && nq >= 4096)) {
+    // (only k_screen_r on a small batch: without the device-side choice SIFT1M
+    // mixture scan 0.242 -> 0.226 ms at 10 k queries, latent unchanged, 2 % slower at
+    // 1 250; k_screen_m: GIST1M mixture scan -2 %, DEEP10M scan 22.2 -> 21.5 ms and
+    // merge 0.32 -> 0.26 ms)
+    if (two && op.near_rounds <= 0 && pl.mfma && pl.rs && nq < 4096) {
         const int64_t est0 = std::min<int64_t>(nq, (nq + pl.qr - 1) / pl.qr + idx->n_lists);
         const int64_t split6 = std::max<int64_t>(1, ((pl.rs ? 3 : 6) * (int64_t)workers + est0 - 1) / std::max<int64_t>(1, est0));
         pl.bpc_near_min = (int)std::min<int64_t>(pl.bpc_near, std::max<int64_t>(1, (max_blocks + split6 - 1) / split6));
