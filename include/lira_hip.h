@@ -186,9 +186,11 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *                        that no full list is re-scanned: -1 (default) 256; 0 none (full lists are
  *                        re-scanned as by k_screen_m); a query that overflows its records has its
  *                        full lists re-scanned instead.  Results never depend on it.
- *   LIRA_OPT_SEED_TILES  tiles of 64 rows of the nearest list the exact seed bound reads (the
- *                        unfused seed, fp32 tiles, L2, k <= 32): 0 (default) auto -- 1 for
- *                        d > 512 (GIST1M), else 2; 1 or 2 fixed.  Results never depend on it.
+ *   LIRA_OPT_SEED_TILES  tiles of 64 rows of the nearest list the exact seed bound reads (fp32
+ *                        tiles, L2, k <= 32): 0 (default) auto -- the seed fused with the
+ *                        per-pair records (d <= 256): 4 below 4096 queries, else 2; the unfused
+ *                        one: 1 for d > 512 (GIST1M), else 2; 1, 2 or 4 (fused only) fixed.
+ *                        Results never depend on it.
  */
 #define LIRA_OPT_KEEP_TILES 1
 #define LIRA_OPT_SCREEN 2

@@ -762,7 +762,7 @@ int lira_index_set_option(lira_index *idx, int option, int64_t value) {
         case LIRA_OPT_NEAR_FIRST: if (!in(-1, 128)) break; o.near_first = v; return LIRA_OK;
         case LIRA_OPT_RESCAN: if (!in(-1, 1)) break; o.rescan = v; return LIRA_OK;
         case LIRA_OPT_SPILL: if (!in(-1, 1 << 16)) break; o.spill = v; return LIRA_OK;
-        case LIRA_OPT_SEED_TILES: if (!in(0, 2)) break; o.seed_tiles = v; return LIRA_OK;
+        case LIRA_OPT_SEED_TILES: if (!in(0, 4) || v == 3) break; o.seed_tiles = v; return LIRA_OK;
         default: return fail(LIRA_EINVAL, "unknown option " + std::to_string(option));
     }
     return fail(LIRA_EINVAL, "value " + std::to_string(value) + " out of range for option " + std::to_string(option));

@@ -2493,9 +2493,21 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
         sp.list_size = adapt ? idx->list_size : nullptr;
         sp.lsamp = adapt ? idx->lsamp : nullptr;
         sp.work = adapt ? (unsigned int *)head + 64 : nullptr;
-        hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2, 2, true>), dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, q,
-                           probe, (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad,
-                           nq, (int)k, qbound, sp);
+        // (256 seed rows below 4096 queries: 1 250-query step scan 0.136 -> 0.123 ms for
+        // +0.008 ms of seed; at 10 k queries the seed's +0.043 ms outweighs the scan's gain)
+        const int nt_f = o.seed_tiles > 0 ? o.seed_tiles : nq < 4096 ? 4 : 2;
+        if (nt_f == 4)
+            hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2, 4, true>), dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, q,
+                               probe, (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad,
+                               nq, (int)k, qbound, sp);
+        else if (nt_f == 1)
+            hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2, 1, true>), dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, q,
+                               probe, (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad,
+                               nq, (int)k, qbound, sp);
+        else
+            hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2, 2, true>), dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, q,
+                               probe, (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad,
+                               nq, (int)k, qbound, sp);
         LIRA_HIP_TRY(hipGetLastError());
     } else if (qbound && o.seed && idx->X) {  // from the fp32 tiles (coalesced)
         const dim3 g((unsigned)((nq + 3) / 4));

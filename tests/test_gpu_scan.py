@@ -407,7 +407,7 @@ def test_options_do_not_change_results(metric):
                        ("prune", (0,)), ("split", (0,)), ("mfma", (0, 2)), ("rounds", (1, 64)),
                        ("near_rounds", (2, 8)), ("screen", (0,)), ("probes_hint", (1, 4)), ("xhi", (0, 1, 2)),
                        ("rscreen", (0,)), ("rescan", (0, 1)), ("spill", (0, 1, 4)),
-                       ("seed_tiles", (1, 2))):
+                       ("seed_tiles", (1, 2, 4))):
         old = idx.get_option(name)
         for v in vals:
             idx.set_option(name, v)
