@@ -67,7 +67,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--fma", action="store_true",
                     help="LIRA_SCAN_FMA accumulation (tolerance variant, not the reference's rounding)")
-    ap.add_argument("--data", default="mixture", choices=["latent", "mixture"],
+    ap.add_argument("--data", default="mixture", choices=["latent", "mixture", "uniform"],
                     help="synthetic distribution (lira_amd/synthetic.py): mixture = SURVEY 8(d)'s "
                          "Gaussian mixture (default); latent = low intrinsic dimension + k-means "
                          "partitions, recall near the metric's 0.95 point like real SIFT1M")
@@ -448,7 +448,7 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
                  "pairs_pruned_plan": work["pairs_pruned_plan"],
                  "candidates_pruned_plan": work["candidates_pruned_plan"],
                  "blocks_pruned_plan": work["candidates_pruned_plan"] / (qr * 256.0),
-                 "blocks_unit": "tiles of 64 candidates x 64 rows" if kname == "k_screen_r"
+                 "blocks_unit": f"tiles of 64 candidates x {qr} rows" if kname == "k_screen_r"
                  else "blocks of 256 candidates x qr rows",
                  "blocks_pruned_plan_note": "(query, candidate) pairs the plan's partition filter removed, in "
                                             "units of one screen block (qr query rows x 256 candidates); "
@@ -519,6 +519,9 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
     out["recall_at_k"] = float(np.mean([len(set(Ig[i]) & set(Igt[i])) / k for i in range(len(rows))]))
     out["recall_gate"] = out["recall_at_k"] >= 0.95
     out["recall_note"] = f"{len(rows)} queries vs exhaustive top-{k} (all {B} partitions probed, same kernel)"
+    if data == "uniform":
+        out["recall_note"] += (" -- uniform i.i.d. data has no cluster structure, so nprobe << B cannot reach the "
+                               "0.95 gate (SURVEY.md 7, hard part 7): a throughput and parity workload")
 
     # ---- CPU baseline: the oracle (search.cpp's scan + top-k in its sequential
     # fp32 arithmetic, one query per thread, OpenMP over queries) on the same
@@ -979,11 +982,14 @@ def main():
         head = run_partition_shard(args, args.data, rank, world, gpu, dev, dist)
     else:
         head = run_workload(args, args.data, rank, world, gpu, dev, dist, primary=True)
-    contrast = None
+    contrast = contrast_u = None
     if args.contrast == "auto" and world == 1 and args.config in ("sift1m", "gist1m") and args.shard == "queries":
         torch.cuda.empty_cache()
-        other = "latent" if args.data == "mixture" else "mixture"
+        other = "latent" if args.data != "latent" else "mixture"
         contrast = run_workload(args, other, rank, world, gpu, dev, dist, primary=False)
+        if args.config == "sift1m" and args.data != "uniform":  # north_star's literal random-float vectors
+            torch.cuda.empty_cache()
+            contrast_u = run_workload(args, "uniform", rank, world, gpu, dev, dist, primary=False)
 
     if rank == 0:
         nq_job = args.nq or nq_default
@@ -1006,6 +1012,7 @@ def main():
                  "bound + exact re-check in search.cpp's sequential fp32 sub/mul/add: bit-exact",
             "data": (f"synthetic latent (intrinsic dim {LATENT_DIM[args.config]}, k-means partitions)"
                      if args.data == "latent" else
+                     "synthetic uniform random floats U[0,1)^d (k-means partitions)" if args.data == "uniform" else
                      "synthetic Gaussian mixture (sigma 0.35, separated clusters, nearest-centre partitions)"),
             "config": {"workload": args.config, "N": N, "d": d, "B": B, "nprobe": nprobe, "k": k,
                        "metric": metric, "n_mul": head["n_mul"],
@@ -1023,6 +1030,7 @@ def main():
                                           "partition_shard", "sweep")
                if key in head},
             "contrast_data": contrast,
+            "contrast_uniform": contrast_u,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

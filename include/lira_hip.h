@@ -165,8 +165,8 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *                        each list's rows by ascending distance to the list's pivot, so tile radius
  *                        ranges are narrow and the triangle-inequality skip drops more; 0: list order.
  *                        Results never depend on it.
- *   LIRA_OPT_RSCREEN     1 (default): the wave-streaming screen k_screen_r where it applies (L2 on the
- *                        centred split copy with the hi x hi screen, k <= 24, dpad <= 128, the
+ *   LIRA_OPT_RSCREEN     1 (default): the wave-streaming screen k_screen_r where it applies (L2 or
+ *                        centred IP on the split copy with the hi x hi screen, k <= 120, dpad <= 128, the
  *                        per-query seed on, not PER_PARTITION): query rows' hi parts in LDS, each
  *                        wave streaming its own candidate tiles into registers; 0: k_screen_m
  *   LIRA_OPT_NEAR_FIRST  (k_screen_r) blocks of 256 candidates in the first chunk of every query
@@ -190,7 +190,15 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *                        tiles, L2, k <= 32): 0 (default) auto -- the seed fused with the
  *                        per-pair records (d <= 256): 4 below 4096 queries, else 2; the unfused
  *                        one: 1 for d > 512 (GIST1M), else 2; 1, 2 or 4 (fused only) fixed.
- *                        Results never depend on it.
+ *                        Results never depend on it.  4 returns LIRA_EUNSUPPORTED where the fused
+ *                        seed cannot run (IP, d > 256, or no fp32 tiles).
+ *   LIRA_OPT_IP_CENTRE   (build time, IP indexes) 1 (default): like L2, store each list's rows
+ *                        radius-ordered around its pivot c with the split copy of fl(x - c), so the
+ *                        wave-streaming screen k_screen_r takes IP as q.x = q.fl(x - c) + q.c with a
+ *                        Cauchy-Schwarz block skip (k <= 120, dpad <= 128); needs
+ *                        LIRA_OPT_KEEP_TILES = 1 (the other screens read the fp32 tiles on such an
+ *                        index).  0: the uncentred split copy (round-4 layout).  Results never
+ *                        depend on it.
  */
 #define LIRA_OPT_KEEP_TILES 1
 #define LIRA_OPT_SCREEN 2
@@ -215,6 +223,7 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
 #define LIRA_OPT_RESCAN 21
 #define LIRA_OPT_SPILL 22
 #define LIRA_OPT_SEED_TILES 23
+#define LIRA_OPT_IP_CENTRE 24
 int lira_index_set_option(lira_index *idx, int option, int64_t value);
 int lira_index_get_option(const lira_index *idx, int option, int64_t *value);
 /* 1 if the index holds the fp32 tile copy (LIRA_OPT_KEEP_TILES at build time) */
@@ -320,7 +329,10 @@ int lira_order_probes(int32_t *probe, int64_t n, int64_t max_probe, const float 
  * Order: faiss convention -- L2 ascending squared distance, IP descending
  * inner product; ties -> smaller gid; pads (+inf, -1) for L2, (-inf, -1) IP.
  * workspace: device, >= lira_scan_workspace_size() bytes, or NULL to use a
- * buffer cached in the handle (grown on demand; not graph-capturable).
+ * buffer cached in the handle, grown on demand -- but never while `stream` is
+ * being captured (LIRA_EINVAL: make one eager call of the same shape before the
+ * capture); a cached buffer that a captured graph uses is kept allocated when a
+ * later eager call outgrows it (until lira_index_destroy), so replays stay valid.
  */
 int lira_scan_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe_max, int64_t k,
                              unsigned flags, size_t *bytes);
@@ -365,6 +377,12 @@ int lira_index_profile_read(lira_index *idx, double *plan_ms, double *scan_ms, d
  */
 int lira_index_set_stats(lira_index *idx, int enable);
 int lira_index_stats_read(lira_index *idx, uint64_t *out8);
+/* which scan paths added to the counters since they were enabled or last read (call
+ * it before lira_index_stats_read, which resets it): bit 0 the all-exact scan, bit 1
+ * the screened one -- slots [1] and [3] mean different things on the two paths */
+#define LIRA_STATS_PATH_EXACT 1
+#define LIRA_STATS_PATH_SCREEN 2
+int lira_index_stats_paths(const lira_index *idx, int *out);
 
 /*
  * Device-side error word of the last scan/select on this handle (e.g. a probe

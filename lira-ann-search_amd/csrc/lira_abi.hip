@@ -181,7 +181,7 @@ __global__ __launch_bounds__(64) void k_entry_radius(const float *x, int64_t d, 
 //     >= max ||x|| (atomicMax on the bits of a non-negative float);
 //   (pivot, tstat) the tile's radius range lo <= ||x - c|| <= hi over its real
 //     rows, rounded outward with a 2^-40 margin ((+inf, -inf) without real rows);
-//   (pivot, xadjc) xadjc = fl(||fl(x - c)||^2) / 2 and the list's rmaxc >= max
+//   (pivot, xadjc) xadjc = fl(||fl(x - c)||^2) / 2 (IP: 0) and the list's rmaxc >= max
 //     ||fl(x - c)||, fl(x - c) exactly the values k_split_rows splits;
 //   (tres) the tile's max over real rows of ||v - hi(v)||, v = fl(x - c) (or x
 //     without a pivot), hi(v) the bf16 part k_split_rows stores first.
@@ -223,7 +223,7 @@ __global__ __launch_bounds__(64) void k_row_stats(const float *Xr, const int32_t
         hi = real ? __double2float_ru(R * (1.0 + 0x1p-40)) : -__builtin_inff();
     }
     if (pv && xadjc) {
-        xadjc[t * kTile + lane] = real ? (float)sc * 0.5f : __builtin_inff();
+        xadjc[t * kTile + lane] = !real ? __builtin_inff() : metric == LIRA_METRIC_L2 ? (float)sc * 0.5f : 0.0f;
         rc = real ? __double2float_ru(__builtin_sqrt(sc) * (1.0 + 0x1p-40)) : 0.0f;
     }
     if (tres) m = real ? __double2float_ru(__builtin_sqrt(sh) * (1.0 + 0x1p-40)) : 0.0f;
@@ -358,6 +358,32 @@ static void free_storage(lira_index *idx) {
     idx->h_tile_off.clear();
 }
 
+int cached_workspace(lira_index_impl *idx, size_t need, hipStream_t st, void **out) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    LIRA_HIP_TRY(hipStreamIsCapturing(st, &cs));
+    const bool capturing = cs == hipStreamCaptureStatusActive;
+    if (idx->ws_bytes < need) {
+        if (capturing)
+            return fail(LIRA_EINVAL, "the cached scan workspace must grow to " + std::to_string(need) +
+                                         " bytes while the stream is being captured: make the same call once "
+                                         "before the capture, or pass a workspace");
+        if (idx->ws) {
+            if (idx->ws_in_graph)
+                idx->ws_retired.push_back(idx->ws);
+            else
+                hipFree(idx->ws);
+        }
+        idx->ws = nullptr;
+        idx->ws_bytes = 0;
+        idx->ws_in_graph = false;
+        LIRA_HIP_TRY(hipMalloc(&idx->ws, need));
+        idx->ws_bytes = need;
+    }
+    if (capturing) idx->ws_in_graph = true;
+    *out = idx->ws;
+    return LIRA_OK;
+}
+
 struct DeviceGuard {
     int prev = -1;
     explicit DeviceGuard(int dev) {
@@ -419,6 +445,7 @@ int lira_index_destroy(lira_index *idx) {
     free_storage(idx);
     if (idx->err) hipFree(idx->err);
     if (idx->ws) hipFree(idx->ws);
+    for (void *w : idx->ws_retired) hipFree(w);
     for (hipEvent_t e : idx->ev_pool) hipEventDestroy(e);
     if (idx->stats) hipFree(idx->stats);
     delete idx;
@@ -482,10 +509,14 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
     uint32_t *d_key = nullptr, *d_key2 = nullptr;
     void *d_tmp = nullptr;
     double *d_psum = nullptr;
-    const bool l2 = idx->metric == LIRA_METRIC_L2 && tiles > 0;
-    // radius-ordered lists (LIRA_OPT_ORDER, L2): a list's rows stored by
-    // ascending ||x - pivot||, so a tile's radius range is narrow and the
-    // triangle-inequality skip can drop it (results do not depend on the order)
+    // pivots, tile radius ranges and the centred split copy: L2 always; IP where
+    // LIRA_OPT_IP_CENTRE asks (with the fp32 tiles kept, which the screens other
+    // than k_screen_r then read: they have no centred IP form)
+    const bool ipc = idx->metric == LIRA_METRIC_IP && idx->opt.ip_centre && idx->opt.keep_tiles && tiles > 0;
+    const bool l2 = (idx->metric == LIRA_METRIC_L2 || ipc) && tiles > 0;
+    // radius-ordered lists (LIRA_OPT_ORDER): a list's rows stored by ascending
+    // ||x - pivot||, so a tile's radius range is narrow and the triangle /
+    // Cauchy-Schwarz skip can drop it (results do not depend on the order)
     const bool order = l2 && idx->opt.order && total > 0;
     const unsigned dy = (unsigned)((d + 255) / 256);
     int rc = LIRA_OK;
@@ -685,6 +716,7 @@ int lira_index_add_partitions(lira_index *idx, int64_t n_lists, const int64_t *l
     idx->max_list = mx;
     idx->max_list_tiles = mxt;
     idx->max_replicas = std::max<int32_t>(1, max_replicas);
+    idx->ipc = ipc && idx->xadjc != nullptr;
     idx->h_list_size = size;
     idx->h_tile_off = toff;
     return LIRA_OK;
@@ -762,7 +794,15 @@ int lira_index_set_option(lira_index *idx, int option, int64_t value) {
         case LIRA_OPT_NEAR_FIRST: if (!in(-1, 128)) break; o.near_first = v; return LIRA_OK;
         case LIRA_OPT_RESCAN: if (!in(-1, 1)) break; o.rescan = v; return LIRA_OK;
         case LIRA_OPT_SPILL: if (!in(-1, 1 << 16)) break; o.spill = v; return LIRA_OK;
-        case LIRA_OPT_SEED_TILES: if (!in(0, 4) || v == 3) break; o.seed_tiles = v; return LIRA_OK;
+        case LIRA_OPT_IP_CENTRE: if (!in(0, 1)) break; o.ip_centre = v; return LIRA_OK;
+        case LIRA_OPT_SEED_TILES:
+            if (!in(0, 4) || v == 3) break;
+            // 4 tiles exist only in the seed fused with the per-pair records (L2, d <= 256,
+            // fp32 tiles kept); the unfused seed reads 1 or 2
+            if (v == 4 && (idx->metric != LIRA_METRIC_L2 || idx->d > 256 || !o.keep_tiles))
+                return fail(LIRA_EUNSUPPORTED, "LIRA_OPT_SEED_TILES 4 needs the fused seed (L2, d <= 256, fp32 tiles)");
+            o.seed_tiles = v;
+            return LIRA_OK;
         default: return fail(LIRA_EINVAL, "unknown option " + std::to_string(option));
     }
     return fail(LIRA_EINVAL, "value " + std::to_string(value) + " out of range for option " + std::to_string(option));
@@ -795,6 +835,7 @@ int lira_index_get_option(const lira_index *idx, int option, int64_t *value) {
         case LIRA_OPT_RESCAN: *value = o.rescan; break;
         case LIRA_OPT_SPILL: *value = o.spill; break;
         case LIRA_OPT_SEED_TILES: *value = o.seed_tiles; break;
+        case LIRA_OPT_IP_CENTRE: *value = o.ip_centre; break;
         default: return fail(LIRA_EINVAL, "unknown option " + std::to_string(option));
     }
     return LIRA_OK;
@@ -856,6 +897,13 @@ int lira_index_set_stats(lira_index *idx, int enable) {
         LIRA_HIP_TRY(hipMemset(idx->stats, 0, 8 * sizeof(uint64_t)));
     }
     idx->stats_on = enable != 0;
+    if (enable) idx->stats_paths = 0;
+    return LIRA_OK;
+}
+
+int lira_index_stats_paths(const lira_index *idx, int *out) {
+    if (!idx || !out) return fail(LIRA_EINVAL, "index or out is NULL");
+    *out = idx->stats_paths;
     return LIRA_OK;
 }
 
@@ -867,6 +915,7 @@ int lira_index_stats_read(lira_index *idx, uint64_t *out8) {
     LIRA_HIP_TRY(hipDeviceSynchronize());
     LIRA_HIP_TRY(hipMemcpy(out8, idx->stats, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     LIRA_HIP_TRY(hipMemset(idx->stats, 0, 8 * sizeof(uint64_t)));
+    idx->stats_paths = 0;
     return LIRA_OK;
 }
 

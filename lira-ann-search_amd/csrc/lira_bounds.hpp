@@ -116,11 +116,20 @@ __device__ __forceinline__ float row_h(double lim, double qn, double qnorm, doub
 // radius range meets the query's triangle interval under the seed bound -- the
 // plan sizes the nearest-probe group's items from the batch's total (0 for an
 // invalid or filtered pair)
+//
+// centred == 2 (IP on a centred copy, k_screen_r): q is NOT centred (q' = q); the
+// record carries qc = fl(q.c) instead of qn and dq (QN = (qc, ||q|| up, pair,
+// qc)), and the filter is Cauchy-Schwarz: -q.x >= -q.c - ||q|| ||x - c|| -
+// slack, slack = 1.01 u |qc| + (d + 2) u ||q|| rmx[p] (search.cpp's own rounding
+// of the exact sum, rmx the list's max ||x||), so a list whose largest radius
+// lies below (-qc - slack - T) / ||q|| holds no candidate with exact score <= T.
 __device__ __forceinline__ int pair_record(const float *Q, int64_t d, int64_t pair, bool valid, int praw,
                                            int nprobe, int n_lists, const float *pivot, int centred,
                                            const float2 *lstat, uint32_t qb, int32_t *probe_live, float4 *QN,
                                            float *QE, float *pqn, uint16_t *QH, int64_t dpad,
-                                           const int32_t *est_size = nullptr, const float2 *est_samp = nullptr) {
+                                           const int32_t *est_size = nullptr, const float2 *est_samp = nullptr,
+                                           const float *rmx = nullptr) {
+    const bool ipm = centred == 2;
     const int sub = threadIdx.x & 15;
     const int p = praw < n_lists ? praw : -1;  // (an id >= n_lists passes through: k_count reports it)
     const int64_t q = valid ? pair / nprobe : 0;
@@ -137,7 +146,7 @@ __device__ __forceinline__ int pair_record(const float *Q, int64_t d, int64_t pa
 #pragma unroll 8
         for (int64_t j = sub; j < d; j += 16) {
             const float x = qr[j], cv = pv ? pv[j] : 0.0f;
-            const float sv = centred && pv ? x - cv : x;
+            const float sv = centred == 1 && pv ? x - cv : x;
             if (qh) qh[j] = (uint16_t)bf16_rne_sat(sv);
             const double xc = (double)sv;
             s = __builtin_fma(xc, xc, s);
@@ -146,8 +155,12 @@ __device__ __forceinline__ int pair_record(const float *Q, int64_t d, int64_t pa
                 e = __builtin_fma(rr, rr, e);
             }
             if (pv) {
-                const double df = (double)x - (double)cv;
-                t = __builtin_fma(df, df, t);
+                if (ipm) {  // q.c
+                    t = __builtin_fma((double)x, (double)cv, t);
+                } else {
+                    const double df = (double)x - (double)cv;
+                    t = __builtin_fma(df, df, t);
+                }
             }
         }
         if (qh)
@@ -162,9 +175,21 @@ __device__ __forceinline__ int pair_record(const float *Q, int64_t d, int64_t pa
     // (the interval math runs in lane 0 of the pair only, unless the estimate needs it in all 16)
     if (!est_size && (sub != 0 || !valid)) return 0;
     int live = p;
-    const float dq = (float)__builtin_sqrt(t);
-    float fa = -__builtin_inff(), fb = __builtin_inff();  // the triangle interval
-    if (p >= 0 && lstat && (int)(pair % nprobe) >= 1) {
+    const float dq = ipm ? (float)t : (float)__builtin_sqrt(t);  // (IP: qc = fl(q.c))
+    const double qnd = __builtin_sqrt(s);
+    float fa = -__builtin_inff(), fb = __builtin_inff();  // the triangle (IP: Cauchy-Schwarz) interval
+    if (ipm && p >= 0 && lstat && rmx && (int)(pair % nprobe) >= 1 && qb != ~0u && qnd > 0.0) {
+        const double dd = (double)d, T = (double)ord2f(qb);
+        if (T < 1e300) {
+            const double qnu = qnd * (1.0 + 0x1p-40);
+            const double slack = (1.01 * __builtin_fabs(t) + (dd + 2.0) * qnu * (double)rmx[p]) * kU * 1.01 + 0x1p-120;
+            double A = (-t - slack - T) / qnu;
+            A -= __builtin_fabs(A) * 0x1p-40 + 0x1p-120;
+            fa = __double2float_rd(A);
+            const float2 ls = lstat[p];
+            if (ls.y < fa) live = -1;
+        }
+    } else if (!ipm && p >= 0 && lstat && (int)(pair % nprobe) >= 1) {
         const double dd = (double)d, F = 1.0 - (dd + 4.0) * kU;
         if (qb != ~0u && F > 0.5) {
             const double T = (double)ord2f(qb);
@@ -190,8 +215,8 @@ __device__ __forceinline__ int pair_record(const float *Q, int64_t d, int64_t pa
     if (sub != 0 || !valid) return est;
     probe_live[pair] = praw >= n_lists ? praw : live;
     if (live < 0) return est;
-    const float qnu = __double2float_ru(__builtin_sqrt(s) * (1.0 + 0x1p-40));
-    if (QN) QN[pair] = make_float4((float)s, qnu, __int_as_float((int)pair), dq);
+    const float qnu = __double2float_ru(qnd * (1.0 + 0x1p-40));
+    if (QN) QN[pair] = make_float4(ipm ? dq : (float)s, qnu, __int_as_float((int)pair), dq);
     if (QE) QE[pair] = __double2float_ru(__builtin_sqrt(e) * (1.0 + 0x1p-40));
     if (pqn) pqn[pair] = qnu;
     return est;

@@ -438,22 +438,32 @@ __device__ __forceinline__ void emit_list(const u64 (&lst)[R], int k, int dedup,
 // capture (graph replay after an eager call of the library faulted on MI355X,
 // ROCm 7.2; replays back to back did not).  A kernel node is ordered and
 // self-contained like every other node of the step.
+// (VEC: 16-B stores, p 16-B aligned; else one 4-B store per word, any 4-B aligned p)
+template <bool VEC>
 static __global__ __launch_bounds__(256) void k_fill32(uint32_t *p, uint32_t v, int64_t n) {
-    const int64_t stride = (int64_t)gridDim.x * 256 * 4;
-    for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += stride) {
-        if (i + 4 <= n) {
+    const int64_t stride = (int64_t)gridDim.x * 256 * (VEC ? 4 : 1);
+    for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * (VEC ? 4 : 1); i < n; i += stride) {
+        if (!VEC) {
+            p[i] = v;
+        } else if (i + 4 <= n) {
             *(uint4 *)(p + i) = make_uint4(v, v, v, v);
         } else {
             for (int64_t j = i; j < n; ++j) p[j] = v;
         }
     }
 }
-// bytes: a multiple of 4, p 16-B aligned (workspace offsets are 256-B aligned)
+// bytes: a multiple of 4; p 4-B aligned (16-B stores where p is 16-B aligned, as every
+// workspace offset is; a caller's buffer, e.g. lira_centroid_gemm's out_err, may not be)
 static inline hipError_t fill32_async(void *p, uint32_t v, size_t bytes, hipStream_t st) {
     const int64_t n = (int64_t)(bytes / 4);
     if (n <= 0) return hipSuccess;
-    const int64_t blocks = (n + 1023) / 1024;
-    hipLaunchKernelGGL(k_fill32, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, st, (uint32_t *)p, v, n);
+    const bool vec = ((uintptr_t)p & 15) == 0;
+    const int64_t blocks = (n + (vec ? 1023 : 255)) / (vec ? 1024 : 256);
+    const dim3 g((unsigned)(blocks < 4096 ? blocks : 4096));
+    if (vec)
+        hipLaunchKernelGGL(k_fill32<true>, g, dim3(256), 0, st, (uint32_t *)p, v, n);
+    else
+        hipLaunchKernelGGL(k_fill32<false>, g, dim3(256), 0, st, (uint32_t *)p, v, n);
     return hipGetLastError();
 }
 

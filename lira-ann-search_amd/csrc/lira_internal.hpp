@@ -56,6 +56,7 @@ struct lira_opts {
     int rescan = -1;      // LIRA_OPT_RESCAN (-1: auto)
     int spill = -1;       // LIRA_OPT_SPILL (-1: 256 records per query)
     int seed_tiles = 0;   // LIRA_OPT_SEED_TILES (0: auto)
+    int ip_centre = 1;    // LIRA_OPT_IP_CENTRE (build time): IP lists centred on their pivots like L2's
 };
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device):
@@ -74,9 +75,10 @@ struct lira_index_impl {
     int32_t *ids = nullptr;
     int32_t *tile_off = nullptr;   // n_lists+1 (int32: < 2^31 tiles)
     int32_t *list_size = nullptr;  // n_lists
-    // L2 only, for the scan's triangle-inequality block skip: per-list pivot
-    // (mean of its rows, fp32, n_lists x d) and per-tile radius bounds
-    // (lo, hi) with lo <= ||x - pivot|| <= hi for every real row of the tile.
+    // For the scan's block skips (L2: triangle inequality; IP: Cauchy-Schwarz on
+    // the centred copy): per-list pivot (mean of its rows, fp32, n_lists x d) and
+    // per-tile radius bounds (lo, hi) with lo <= ||x - pivot|| <= hi for every
+    // real row of the tile.  L2 always; IP where the index is centred (ipc).
     float *pivot = nullptr;
     float2 *tstat = nullptr;
     // per list: (min, max) of its tiles' radius ranges (the scan's pair filter)
@@ -90,9 +92,12 @@ struct lira_index_impl {
     // The same for the split-bf16 copy, which holds x - pivot of its list (L2:
     // the screen works on centred vectors, whose norms and hence error bounds
     // are smaller): xadjc = ||fl(x - c)||^2 / 2, rmaxc >= max ||fl(x - c)||.
-    // NULL for IP (no centring) -- the split screen then uses xadj / rmax.
+    // IP centred (ipc): the copy holds fl(x - c) too, xadjc = 0 (+inf padding)
+    // and q.x = q.fl(x - c) + q.c is screened by k_screen_r only (the other
+    // screens then take the fp32 tiles); NULL for an uncentred IP index.
     float *xadjc = nullptr;
     float *rmaxc = nullptr;
+    bool ipc = false;
     // Row-major copy of the tiles, [n_tiles*64][d] fp32 by storage row: the
     // screened path's exact re-check reads one candidate's d values
     // contiguously (a tile column would cost one cache line per value).
@@ -106,6 +111,8 @@ struct lira_index_impl {
     int32_t *err = nullptr;        // device error word
     void *ws = nullptr;            // cached scan workspace
     size_t ws_bytes = 0;
+    bool ws_in_graph = false;      // a stream capture recorded kernels that use ws
+    std::vector<void *> ws_retired;  // outgrown workspaces a captured graph may still use (freed at destroy)
     // profiling: 4 events per recorded call (start, after plan, after scan, after merge)
     bool profiling = false;
     std::vector<hipEvent_t> ev_pool;
@@ -113,9 +120,17 @@ struct lira_index_impl {
     // scan work counters (lira_index_set_stats): 8 u64 on the device
     bool stats_on = false;
     uint64_t *stats = nullptr;
+    int stats_paths = 0;  // scan paths counted since the last read: 1 all-exact, 2 screened
 };
 
 int64_t round_up(int64_t x, int64_t m);
+
+// The handle's cached scan workspace, at least `need` bytes, for a call on `st`.
+// Growing it while `st` is being captured is refused (LIRA_EINVAL: the graph would
+// bake in an allocation made mid-capture); a workspace that a captured graph uses
+// is never freed when a later eager call outgrows it (retired until destroy), so a
+// replay after such a call reads valid memory.
+int cached_workspace(lira_index_impl *idx, size_t need, hipStream_t st, void **out);
 
 }  // namespace lira
 

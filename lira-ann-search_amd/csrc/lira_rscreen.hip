@@ -1,33 +1,38 @@
 // lira_rscreen.hip -- k_screen_r, the wave-streaming screen (gfx950): the
-// default screen of lira_scan_topk for L2, k <= 24, dpad <= 128.  Replaces
-// search.cpp:468-493 (the per-query loop over the candidates of the probed
-// buckets) with results identical to the all-exact scan: it screens every
+// default screen of lira_scan_topk for L2 and for IP on a centred index
+// (lira_index::ipc), k <= 120, dpad <= 128.  Replaces search.cpp:468-493 (the
+// per-query loop over the candidates of the probed buckets, l2_sq :253-260 /
+// -ip :263-269) with results identical to the all-exact scan: it screens every
 // (query, candidate) pair with a rigorous bound and leaves the exact re-check
-// and the top-k to k_smerge (lira_screen.hip), exactly as k_screen_m does.
-// The error model is k_screen_m<..., 3>'s (hi x hi, lira_bounds.hpp err_E,
-// split = 3), evaluated in fp32 with explicit outward rounding.
+// and the top-k to k_smerge (lira_screen.hip), exactly as k_screen_m does.  The
+// error model is k_screen_m<..., 3>'s (hi x hi, lira_bounds.hpp err_E, split =
+// 3), evaluated in fp32 with explicit outward rounding.
 //
-// Why a second screen.  k_screen_m stages each candidate block through LDS
-// once for its 64 query rows: per 32 dims of a 256-candidate block every wave
-// issues 5 LDS-DMA pieces and 17 fragment reads and meets the other three
-// waves at a barrier, so the slowest wave's selection gates the next chunk
-// (0.18 of HBM peak, MFMA busy 5-11 %, 46-55 % of wave
-// cycles parked).  Here:
-//   * the item's 64 query rows' hi parts live in registers for the whole item
-//     (A operands: dpad / 32 x 4 row groups x 8 bf16 per lane, 64 VGPRs at
-//     d = 128), loaded once per item from the per-pair records (k_seed_t);
-//   * each wave streams its OWN candidate tiles (64 rows each; tiles u, u + 4,
-//     ... of the item): B fragments straight from HBM/L2 into registers, one
-//     16-B load per lane feeding 4 MFMAs, the next tile's loads issued under
-//     the current tile's MFMAs -- no LDS staging of candidates, no DMA issue,
-//     no barrier inside an item;
-//   * the four waves share the item's 64 row lists (LDS, sorted, 32 keys);
-//     each wave appends survivors to its own per-row buffers (16 keys) and
-//     merges a full buffer into the shared list under a per-row LDS lock;
-//     thresholds are refreshed per tile from the shared lists, the per-row
-//     running error bound and the query's published bound.
-// Per tile and wave: 4 x dpad/32 x 4 v_mfma_f32_16x16x32_bf16 (64 at d = 128:
-// 64 rows x 64 candidates), 4 dpad/32 + 1 loads, ~100 VALU of selection.
+// Work split.  An item is (bucket, block of QR query rows, chunk of the bucket):
+//   * the item's QR query rows' hi parts live in LDS in MFMA-fragment order (the
+//     A operands, loaded once per item from the per-pair records of k_seed_t /
+//     k_pairs);
+//   * each of the 4 waves streams its OWN candidate tiles (64 rows each; tiles
+//     u, u + 4, ... of the item): B fragments straight from HBM/L2 into
+//     registers, one 16-B load per lane feeding QR/16 MFMAs, the next tile's
+//     loads issued under the current tile's MFMAs -- no LDS staging of
+//     candidates, no barrier inside an item;
+//   * the four waves share the item's QR row lists (LDS, sorted, K2 = 32 RL
+//     keys); each wave appends survivors to its own per-row buffers (16 keys)
+//     and merges a full buffer into the shared list under a per-row LDS lock;
+//     thresholds follow the shared lists, the per-row error bound and the
+//     query's published bound.
+// RL = 1 (k <= 24): 64 query rows per item, 32-key lists.  RL = 2 / 4 (k <= 56 /
+// 120, DEEP10M's k = 100): 32 rows per item, 64 / 128-key lists, so that the
+// lists, buffers and A operands stay within 80 KB of LDS (two workgroups per
+// CU; the MFMA count per pair is the same, each candidate byte feeds 32 rows
+// instead of 64).
+//
+// Metrics.  L2: x' = fl(x - c), q' = fl(q - c) for the list pivot c; score s~ =
+// fl(qn - 2 fl(dot' - xadj)), qn = fl(||q'||^2), xadj = fl(||x'||^2)/2; block skip
+// by the triangle inequality.  IP (centred): q stays, x' = fl(x - c), and q.x
+// = q.x' + q.c, so s~ = -fl(dot' + qc), qc = fl(q.c) per (query, list) pair;
+// block skip by Cauchy-Schwarz, -q.x >= -q.c - ||q|| ||x - c||.
 //
 // MFMA layout (cdna_hip_programming.md, 16x16x32 bf16): A = 16 query rows x
 // 32 dims (lane l: row l & 15, dims 8 (l >> 4) ..), B = 32 dims x 16
@@ -46,44 +51,36 @@ namespace lira {
 typedef __bf16 rbf16x8 __attribute__((ext_vector_type(8)));
 typedef float rf4 __attribute__((ext_vector_type(4)));
 
-static constexpr int kRQ = 64;          // query rows per item
 static constexpr int kRW = 4;           // waves per workgroup
-static constexpr int kRK2 = 32;         // row list keys (k <= 24)
 static constexpr int kRBC = 16;         // survivor buffer keys per (wave, row)
 static constexpr int kRMaxTiles = 512;  // tiles per item (the plan caps a chunk at 128 blocks)
 static constexpr int kROCap = 128;      // survivor queue entries per wave (>= two candidate masks)
 
+template <int RL>
 struct RSmem {
-    static constexpr int aq = 0;                                    // [4 chunks][4 row groups][64 lanes] 16 B: A operands
-    static constexpr int lists = aq + 4 * 4 * 64 * 16;              // [64][32] u64
-    static constexpr int bufs = lists + kRQ * kRK2 * 8;              // [4][64][16] u64
-    static constexpr int bufc = bufs + kRW * kRQ * kRBC * 8;         // [4][64] int
-    static constexpr int hs = bufc + kRW * kRQ * 4;                  // [4][64] float: the wave's thresholds
-    static constexpr int tst = hs + kRW * kRQ * 4;                   // [512] float2: tile radius ranges
-    static constexpr int trs = tst + kRMaxTiles * 8;                 // [512] float: tile hi residuals
-    static constexpr int pair = trs + kRMaxTiles * 4;                // [64] int
-    static constexpr int qn = pair + kRQ * 4;                        // [64] float4: qn, ||q'|| (up), qres, ||q - c||
-    static constexpr int erun = qn + kRQ * 16;                       // [64] float bits: running error bound
-    static constexpr int lock = erun + kRQ * 4;                      // [64] int
-    static constexpr int opub = lock + kRQ * 4;                      // [64] uint: bound last published
-    static constexpr int oqk = opub + kRQ * 4;                       // [4][kROCap] u64: survivor queue keys
-    static constexpr int kth = oqk + kRW * kROCap * 8;               // [64] u64: each list's k-th key
-    static constexpr int meta = kth + kRQ * 8;                       // [16] int
+    static constexpr int QR = RL == 1 ? 64 : 32;                   // query rows per item
+    static constexpr int K2 = 32 * RL;                             // row list keys
+    static constexpr int NRG = QR / 16;                            // MFMA row groups
+    static constexpr int aq = 0;                                   // [4 chunks][NRG][64 lanes] 16 B: A operands
+    static constexpr int lists = aq + 4 * NRG * 64 * 16;           // [QR][K2] u64
+    static constexpr int bufs = lists + QR * K2 * 8;               // [4][QR][16] u64
+    static constexpr int bufc = bufs + kRW * QR * kRBC * 8;        // [4][64] int (lane = row)
+    static constexpr int hs = bufc + kRW * 64 * 4;                 // [4][64] float: the wave's thresholds
+    static constexpr int tst = hs + kRW * 64 * 4;                  // [512] float2: tile radius ranges
+    static constexpr int trs = tst + kRMaxTiles * 8;               // [512] float: tile hi residuals
+    static constexpr int pair = trs + kRMaxTiles * 4;              // [64] int
+    static constexpr int qn = pair + 64 * 4;                       // [64] float4: qn (IP qc), ||q'|| (up), qres, dq (IP qc)
+    static constexpr int erun = qn + 64 * 16;                      // [64] float bits: running error bound
+    static constexpr int lock = erun + 64 * 4;                     // [64] int
+    static constexpr int opub = lock + 64 * 4;                     // [64] uint: bound last published
+    static constexpr int oqk = opub + 64 * 4;                      // [4][kROCap] u64: survivor queue keys
+    static constexpr int kth = oqk + kRW * kROCap * 8;             // [64] u64: each list's k-th key
+    static constexpr int meta = kth + 64 * 8;                      // [16] int
     static constexpr int total = meta + 64;
 };
-static_assert(RSmem::total <= 80 * 1024, "k_screen_r: two workgroups per CU");
+static_assert(RSmem<1>::total <= 80 * 1024 && RSmem<2>::total <= 80 * 1024 && RSmem<4>::total <= 80 * 1024,
+              "k_screen_r: two workgroups per CU");
 static_assert(kROCap >= 128, "a drained queue takes two full candidate masks");
-
-// Timing experiment (-DRS_CLOCKS builds only): per-wave cycle split of the
-// kernel, summed over waves, read by lira_debug_rs_clocks
-#ifdef RS_CLOCKS
-__device__ unsigned long long g_rs_clk[16];
-#define RCLK(v) const long long v = clock64()
-#define RACC(slot, a, b) (clk[slot] += (unsigned long long)((b) - (a)))
-#else
-#define RCLK(v)
-#define RACC(slot, a, b)
-#endif
 
 // a value the compiler must treat as produced here (keeps per-lane address
 // arithmetic from being hoisted out of the loops: hipcc otherwise precomputed
@@ -97,48 +94,87 @@ __device__ __forceinline__ int opaque(int x) {
 __device__ __forceinline__ float rup(float x) { return __builtin_fmaf(__builtin_fabsf(x), 0x1p-20f, x) + 0x1p-125f; }
 __device__ __forceinline__ float rdn(float x) { return __builtin_fmaf(-__builtin_fabsf(x), 0x1p-20f, x) - 0x1p-125f; }
 
-// err_E<L2>(qnorm, Rb, d, split = 3, dpad, centred = 1, hres, qres) in fp32:
-// every term is >= 0, so the ~16 roundings stay below 2^-20 relative and the
-// final factor covers them; + 2^-125 >= d 2^-140 (lira_bounds.hpp).
-// The MFMA chain here starts from C = -xadj (no separate fl(dot - xadj)): one
-// more add, and every partial sum is bounded by xadj + ||q'|| (R + rho), xadj <=
-// fl(Rb^2) / 2, so the accumulation term counts dpad + 1 adds at 2^-22 of that
-// (lira_bounds.hpp's model: any order or rounding mode at <= 2^-22 per add)
-__device__ __forceinline__ float errE_r(float qnorm, float Rb, float hres, float qres, float dp) {
+// err_E(qnorm, Rb, d, split = 3, dpad, centred, hres, qres) in fp32: every term is
+// >= 0, so the ~16 roundings stay below 2^-20 relative and the final factor covers
+// them; + 2^-125 >= d 2^-140 (lira_bounds.hpp).
+// The MFMA chain starts from C = -xadj (no separate fl(dot - xadj)): one more
+// add, and every partial sum is bounded by xadj + ||q'|| (R + rho), xadj <=
+// fl(Rb^2) / 2 (L2; 0 for IP), so the accumulation term counts dpad + 1 adds at
+// 2^-22 of that (lira_bounds.hpp's model: any order or rounding mode at <= 2^-22
+// per add).
+// L2: E = 2 ed + (8.4 + 2.01 + 2) u (||q'|| + Rb)^2 (the centred copy's 2.01 u s^2,
+// s~ = fl(qn - 2 wv)'s extra rounding 2 u s^2).
+// IP (centred): s~ = -fl(wv + qc) against search.cpp's s = -fl_seq(q.x):
+//   |q.x' - wv| <= ed;  |q.(x - c - x')| <= 1.01 u ||q|| Rb (x' = fl(x - c));
+//   |qc - q.c| <= 1.01 u |qc|;  the add: u (||q|| (Rb + rho) + |qc|);
+//   search.cpp's own sum: (d + 2) u ||q|| Rx, Rx >= ||x|| (the list's rmax).
+template <int M>
+__device__ __forceinline__ float errE_r(float qnorm, float Rb, float hres, float qres, float dp, float qc, float Rx,
+                                        float dd) {
     const float ex = hres >= 0.0f ? hres * 1.0001f : 0x1p-8f * 1.02f * Rb;
-    const float ed = ex * qnorm + qres * (Rb + ex) * 1.0001f +
-                     2.0f * (dp + 1.0f) * 0x1p-22f * 1.02f * (qnorm * (Rb + ex) + 0.5001f * Rb * Rb) +
+    const float xa = M == LIRA_METRIC_L2 ? 0.5001f * Rb * Rb : 0.0f;
+    const float ed = ex * qnorm + qres * (Rb + ex) * 1.0001f + 2.0f * (dp + 1.0f) * 0x1p-22f * 1.02f * (qnorm * (Rb + ex) + xa) +
                      2.0f * dp * 0x1p-96f * (qnorm + Rb + ex + 1.0f);
-    const float s = qnorm + Rb;
-    return (2.0f * ed + (1.05f * 8.0f + 2.01f + 2.0f) * 0x1p-24f * s * s) * (1.0f + 0x1p-18f) + 0x1p-125f;
+    if (M == LIRA_METRIC_L2) {
+        const float s = qnorm + Rb;
+        return (2.0f * ed + (1.05f * 8.0f + 2.01f + 2.0f) * 0x1p-24f * s * s) * (1.0f + 0x1p-18f) + 0x1p-125f;
+    }
+    const float aq = __builtin_fabsf(qc);
+    return (ed + (1.01f * qnorm * Rb + 2.02f * aq + qnorm * (Rb + ex) + (dd + 2.0f) * qnorm * Rx) * 0x1p-24f) * 1.05f +
+           0x1p-125f;
 }
 
-// L2 screened score of a candidate from wv = fl(dot - xadj): s~ = fl(qn - 2 wv)
-// (k_screen_m: fma(-2, dot, fl(qn + 2 xadj)); this form's extra rounding is in
-// errE_r's 2 u s^2)
-__device__ __forceinline__ u64 rkey(float wv, float qn, uint32_t pos) {
-    const float s = qn - 2.0f * wv;
+// the screened score of a candidate from wv = fl(dot - xadj), per row qv = qn (L2)
+// or qc (IP): L2 s~ = fl(qn - 2 wv) (k_screen_m: fma(-2, dot, fl(qn + 2 xadj));
+// this form's extra rounding is in errE_r's 2 u s^2); IP s~ = -fl(wv + qc)
+template <int M>
+__device__ __forceinline__ u64 rkey(float wv, float qv, uint32_t pos) {
+    const float s = M == LIRA_METRIC_L2 ? qv - 2.0f * wv : -(wv + qv);
     return ((u64)f2ord(s) << 32) | pos;
 }
 
 // Buffered survivors carry fl(dot - xadj) instead of the score: wkey = (f2ord(-wv),
-// storage position), ascending in the score for a fixed row; converted to the
-// list key (rkey, the same arithmetic) when merged, where the row's qn is one
-// broadcast read (the selection then needs no LDS read)
+// storage position), ascending in the score for a fixed row (both metrics); converted
+// to the list key (rkey, the same arithmetic) when merged, where the row's qn / qc is
+// one broadcast read (the selection then needs no LDS read)
 __device__ __forceinline__ u64 wkey(float wv, uint32_t pos) { return ((u64)f2ord(-wv) << 32) | pos; }
-__device__ __forceinline__ u64 wkey_to_key(u64 wk, float qn) {
-    return rkey(-ord2f((uint32_t)(wk >> 32)), qn, (uint32_t)wk);
+template <int M>
+__device__ __forceinline__ u64 wkey_to_key(u64 wk, float qv) {
+    return rkey<M>(-ord2f((uint32_t)(wk >> 32)), qv, (uint32_t)wk);
+}
+
+// the bound on the final k-th exact score from a list's k-th screened key (bound_P)
+__device__ __forceinline__ float bound_of(u64 kk, float er, float gP) {
+    return kk != kEmptyKey ? rup(rup(key_score(kk) + er) * gP) + 0x1p-125f : __builtin_inff();
+}
+// s_lim's T part: L2 (T + d 2^-140) / (1 - g), IP T (the error is all in E)
+template <int M>
+__device__ __forceinline__ float lim_of(float T, float invF) {
+    if (!(T < 3e38f)) return __builtin_inff();
+    return M == LIRA_METRIC_L2 ? rup(rup(fmaxf(T, 0.0f) + 0x1p-125f) * invF) : T;
+}
+
+// key e (runtime, < 32 RL) of a half-wave list, broadcast to the lane's half
+template <int RL>
+__device__ __forceinline__ u64 list_at(const u64 (&lst)[RL], int e) {
+    u64 x = lst[0];
+#pragma unroll
+    for (int r = 1; r < RL; ++r)
+        if ((e >> 5) == r) x = lst[r];
+    return shfl64(x, (lane_id() & 32) + (e & 31));
 }
 
 // A row list's merge with the keys it evicts (spill lists on): per half, lst <- the
-// 32 smallest of lst U batch, and ev = the 32 largest (what half_merge_batch1 drops)
-__device__ __forceinline__ u64 merge_evict(u64 (&lst)[1], u64 batch) {
+// 32 RL smallest of lst U batch, and ev = the 32 largest (what half_merge_batch1 drops:
+// the list's first 32 (RL - 1) keys are below its last 32)
+template <int RL>
+__device__ __forceinline__ u64 merge_evict(u64 (&lst)[RL], u64 batch) {
     u64 b[1] = {batch};
     half_sort<1>(b);
     const u64 rev = rev32_u64(b[0]);
-    const u64 ev = kmax(lst[0], rev);
-    lst[0] = kmin(lst[0], rev);
-    half_bitonic_merge<1>(lst);
+    const u64 ev = kmax(lst[RL - 1], rev);
+    lst[RL - 1] = kmin(lst[RL - 1], rev);
+    half_bitonic_merge<RL>(lst);
     return ev;
 }
 
@@ -149,11 +185,10 @@ __device__ __forceinline__ u64 merge_evict(u64 (&lst)[1], u64 batch) {
 // rounding, which is above k_smerge's s_lim(T, E) (lira_bounds.hpp).  Per half-wave
 // (hv: this lane's half holds the row).  Past scap records the query's count shows
 // the overflow and k_smerge re-scans its full lists instead.
+template <int M>
 __device__ __forceinline__ void spill_evicted(const RArgs &a, u64 ev, bool hv, u64 kth, float er, float Tc, int pr) {
-    float T = kth != kEmptyKey ? rup(rup(key_score(kth) + er) * a.gP) + 0x1p-125f : __builtin_inff();
-    T = fminf(T, Tc);
-    const float Ac = T < 3e38f ? rup(rup(fmaxf(T, 0.0f) + 0x1p-125f) * a.invF) : __builtin_inff();
-    const float lim = rup(Ac + er);
+    const float T = fminf(bound_of(kth, er, a.gP), Tc);
+    const float lim = rup(lim_of<M>(T, a.invF) + er);
     const bool sp = hv && pr >= 0 && ev != kEmptyKey && key_score(ev) <= lim;
     const u64 m = __ballot(sp);
     if (!m) return;
@@ -174,36 +209,41 @@ __device__ __forceinline__ void spill_evicted(const RArgs &a, u64 ev, bool hv, u
 // row's LDS lock: raise the row's running error bound to the wave's first
 // (readers take the list's k-th key, then the bound: program order in both),
 // half-wave merge, publish the query's bound if the list's k-th improved.
+template <int M, int RL>
 __device__ __forceinline__ void flush_row(u64 *lists, u64 *kth_s, const u64 *mybuf, int *lock_s, uint32_t *erun_s,
-                                       uint32_t *opub_s, const int *pair_s, int row, int n, int ew_bits, int k,
-                                       uint32_t *qbound, int nprobe, float gP, float qn_row, const RArgs &a,
-                                       float Tc_row) {
+                                          uint32_t *opub_s, const int *pair_s, int row, int n, int ew_bits, int k,
+                                          float qv_row, const RArgs &a, float Tc_row) {
+    constexpr int K2 = 32 * RL;
     const int lane = opaque(lane_id()), hl = lane & 31;  // (opaque: addresses computed here, not hoisted)
-#ifdef RS_CLOCKS
-    if (lane == 0) atomicAdd(&g_rs_clk[12], 1ull);
-#endif
     if (lane == 0) {
         while (atomicCAS(lock_s + row, 0, 1) != 0) __builtin_amdgcn_s_sleep(1);
         atomicMax(erun_s + row, (uint32_t)ew_bits);
     }
     asm volatile("" ::: "memory");
-    u64 lst[1] = {lists[row * kRK2 + hl]};
-    const u64 b = hl < n ? wkey_to_key(mybuf[row * kRBC + hl], qn_row) : kEmptyKey;
+    u64 lst[RL];
+#pragma unroll
+    for (int r = 0; r < RL; ++r) lst[r] = lists[row * K2 + r * 32 + hl];
+    const u64 b = hl < n ? wkey_to_key<M>(mybuf[row * kRBC + hl], qv_row) : kEmptyKey;
     u64 ev = kEmptyKey;
     if (a.spill)
-        ev = merge_evict(lst, b);
+        ev = merge_evict<RL>(lst, b);
     else
-        half_merge_batch1<1>(lst, b);
-    if (lane < 32) lists[row * kRK2 + hl] = lst[0];
-    if (lane == k - 1) kth_s[row] = lst[0];
-    if (lane == k - 1 && lst[0] != kEmptyKey && qbound) {
-        const int pr = pair_s[row];
-        if (pr >= 0) {
-            const float er = __uint_as_float(erun_s[row]);
-            const uint32_t P = f2ord(rup(rup(key_score(lst[0]) + er) * gP) + 0x1p-125f);
-            if (P < opub_s[row]) {
-                opub_s[row] = P;
-                atomicMin(qbound + pr / nprobe, P);
+        half_merge_batch1<RL>(lst, b);
+    if (lane < 32) {
+#pragma unroll
+        for (int r = 0; r < RL; ++r) lists[row * K2 + r * 32 + hl] = lst[r];
+    }
+    const u64 kk = list_at<RL>(lst, k - 1);
+    if (lane == 0) {
+        kth_s[row] = kk;
+        if (kk != kEmptyKey && a.qbound) {
+            const int pr = pair_s[row];
+            if (pr >= 0) {
+                const uint32_t P = f2ord(bound_of(kk, __uint_as_float(erun_s[row]), a.gP));
+                if (P < opub_s[row]) {
+                    opub_s[row] = P;
+                    atomicMin(a.qbound + pr / a.nprobe, P);
+                }
             }
         }
     }
@@ -211,26 +251,26 @@ __device__ __forceinline__ void flush_row(u64 *lists, u64 *kth_s, const u64 *myb
     if (lane == 0) *(volatile int *)(lock_s + row) = 0;
     __builtin_amdgcn_wave_barrier();
     if (a.spill)  // (after the unlock: the atomic's round trip holds no other wave)
-        spill_evicted(a, ev, lane < 32, shfl64(lst[0], k - 1), __uint_as_float(erun_s[row]), Tc_row, pair_s[row]);
+        spill_evicted<M>(a, ev, lane < 32, kk, __uint_as_float(erun_s[row]), Tc_row, pair_s[row]);
 }
 
 // Merge this wave's full row buffers into the lists, then move the survivor
 // queue into the buffers (LDS atomic slots), merging every buffer that fills,
 // until the queue is empty.
+template <int M, int RL>
 __device__ __forceinline__ void drain_buffers(u64 *lists, u64 *kth_s, u64 *mybuf, int *mybufc, int *lock_s,
-                                           uint32_t *erun_s, uint32_t *opub_s, const int *pair_s,
-                                           const float4 *rec_s, const u64 *oq_key, uint32_t pos_base, int nq,
-                                           float Ew, int k, uint32_t *qbound, int nprobe, float gP, const RArgs &a,
-                                           float Tc) {
+                                              uint32_t *erun_s, uint32_t *opub_s, const int *pair_s,
+                                              const float4 *rec_s, const u64 *oq_key, uint32_t pos_base, int nq,
+                                              float Ew, int k, const RArgs &a, float Tc) {
     const int lane = opaque(lane_id());
     auto flush_full = [&]() {
         u64 full = __ballot(mybufc[lane] >= kRBC);  // lane = row
         while (full) {
             const int row = __builtin_ctzll(full);
             full &= full - 1;
-            flush_row(lists, kth_s, mybuf, lock_s, erun_s, opub_s, pair_s, row, kRBC,
-                      __builtin_amdgcn_readlane(__float_as_int(Ew), row), k, qbound, nprobe, gP, rec_s[row].x, a,
-                      __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Tc), row)));
+            flush_row<M, RL>(lists, kth_s, mybuf, lock_s, erun_s, opub_s, pair_s, row, kRBC,
+                             __builtin_amdgcn_readlane(__float_as_int(Ew), row), k, rec_s[row].x, a,
+                             __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Tc), row)));
             if (lane == 0) mybufc[row] = 0;
             __builtin_amdgcn_wave_barrier();
         }
@@ -254,50 +294,49 @@ __device__ __forceinline__ void drain_buffers(u64 *lists, u64 *kth_s, u64 *mybuf
             }
             __builtin_amdgcn_wave_barrier();
             // rows the round filled (a lane that overflowed left its row's count above kRBC)
-            if (lane < kRQ && mybufc[lane] > kRBC) mybufc[lane] = kRBC;
+            if (mybufc[lane] > kRBC) mybufc[lane] = kRBC;
             __builtin_amdgcn_wave_barrier();
             flush_full();
         }
     }
 }
 
-template <int NC>  // 32-dim chunks: dpad = 32 NC
+template <int NC, int M, int RL>  // NC: 32-dim chunks (dpad = 32 NC); M: metric; RL: list registers
 __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
+    typedef RSmem<RL> S;
+    constexpr int QR = S::QR, K2 = S::K2, NRG = S::NRG;
+    constexpr int NSTEP = 8 * NRG;  // selection steps per tile: (row group, register, candidate pair)
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    u64 *lists = (u64 *)(smem + RSmem::lists);
-    u64 *bufs = (u64 *)(smem + RSmem::bufs);
-    int *bufc = (int *)(smem + RSmem::bufc);
-    float *hs = (float *)(smem + RSmem::hs);
-    float2 *tst = (float2 *)(smem + RSmem::tst);
-    float *trs = (float *)(smem + RSmem::trs);
-    int *pair_s = (int *)(smem + RSmem::pair);
-    float4 *rec_s = (float4 *)(smem + RSmem::qn);
-    const uint4 *aq_s = (const uint4 *)(smem + RSmem::aq);
-    uint32_t *erun_s = (uint32_t *)(smem + RSmem::erun);
-    int *lock_s = (int *)(smem + RSmem::lock);
-    uint32_t *opub_s = (uint32_t *)(smem + RSmem::opub);
-    int *meta = (int *)(smem + RSmem::meta);
-    u64 *kth_s = (u64 *)(smem + RSmem::kth);
+    u64 *lists = (u64 *)(smem + S::lists);
+    u64 *bufs = (u64 *)(smem + S::bufs);
+    int *bufc = (int *)(smem + S::bufc);
+    float *hs = (float *)(smem + S::hs);
+    float2 *tst = (float2 *)(smem + S::tst);
+    float *trs = (float *)(smem + S::trs);
+    int *pair_s = (int *)(smem + S::pair);
+    float4 *rec_s = (float4 *)(smem + S::qn);
+    const uint4 *aq_s = (const uint4 *)(smem + S::aq);
+    uint32_t *erun_s = (uint32_t *)(smem + S::erun);
+    int *lock_s = (int *)(smem + S::lock);
+    uint32_t *opub_s = (uint32_t *)(smem + S::opub);
+    int *meta = (int *)(smem + S::meta);
+    u64 *kth_s = (u64 *)(smem + S::kth);
     __shared__ int xq[9];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, cj = lane & 15;
     const int k = a.k;
-    const float dp = (float)a.dpad;
-    u64 *mybuf = bufs + wave * kRQ * kRBC;
-    int *mybufc = bufc + wave * kRQ;
-    float *myh = hs + wave * kRQ;
-    u64 *oq_key = (u64 *)(smem + RSmem::oqk) + wave * kROCap;
+    const float dp = (float)a.dpad, dd = (float)a.d;
+    u64 *mybuf = bufs + wave * QR * kRBC;
+    int *mybufc = bufc + wave * 64;
+    float *myh = hs + wave * 64;
+    u64 *oq_key = (u64 *)(smem + S::oqk) + wave * kROCap;
     const bool TRI = a.tstat != nullptr;
     // B fragment: the lane's byte offset inside a tile's 32-dim chunk
     const uint32_t lane_off = (uint32_t)((g >> 1) * 4096 + (g & 1) * 1024 + cj * 16);
     const int64_t tile_bytes = a.dpad * 64 * 4;
     unsigned long long n_tiles = 0, n_skip = 0, n_surv = 0;
-#ifdef RS_CLOCKS
-    unsigned long long clk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long surv_g0 = 0, tiles_g0 = 0;
-#endif
 
     const int bpc_near_d = __builtin_amdgcn_readfirstlane(a.head[19]);
     // Items are claimed by the last wave's lane 0 (its tiles are u = 3, 7, ...: the
@@ -324,7 +363,6 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
     }
     __syncthreads();
     for (;;) {
-        RCLK(t_item);
         if (!meta[0]) break;
         const int vp = __builtin_amdgcn_readfirstlane(meta[1]);
         const int qb = __builtin_amdgcn_readfirstlane(meta[2]);
@@ -343,6 +381,7 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
         const int qblk = __builtin_amdgcn_readfirstlane(meta[6]);
         const int tbase = tile0 + tb_begin;
         const float R = a.rmax[p];
+        const float Rx = M == LIRA_METRIC_IP ? a.rmaxx[p] : 0.0f;
         int u = wave;
         // B operands: a ring of RS chunks of [candidate group]; chunk s (of the
         // wave's chunk sequence: tile after tile) sits in slot s mod RS, and its
@@ -364,8 +403,8 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
         if (u < nt) load_first();
 
         // ---- item prologue: row records, lists, tile statistics
-        const int nval = a.cnt[vp] - qb * kRQ;
-        const int my_pair = lane < nval ? a.qlist[a.qoff[vp] + qb * kRQ + lane] : -1;  // lane = row
+        const int nval = a.cnt[vp] - qb * QR;
+        const int my_pair = lane < QR && lane < nval ? a.qlist[a.qoff[vp] + qb * QR + lane] : -1;  // lane = row
         const float4 qrec = my_pair >= 0 ? a.QN[my_pair] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         const float my_qres = my_pair >= 0 ? a.QE[my_pair] : 0.0f;
         const int my_q = my_pair >= 0 ? my_pair / a.nprobe : -1;
@@ -390,7 +429,7 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
         {
             uint4 *l4 = (uint4 *)lists;
             const uint4 e4 = make_uint4(~0u, ~0u, ~0u, ~0u);
-            for (int i = tid; i < kRQ * kRK2 / 2; i += 256) l4[i] = e4;
+            for (int i = tid; i < QR * K2 / 2; i += 256) l4[i] = e4;
         }
         if (TRI) {
             float rb = 0.0f, hr = 0.0f;
@@ -411,26 +450,30 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
 
         // A operands into LDS, in fragment order: [chunk c][row group rg][lane (g, j)]
         // = row 16 rg + j, dims 32 c + 8 g .. + 7 (each wave reads 1 KiB per (c, rg))
-        for (int e = tid; e < NC * 4 * 64; e += 256) {
-            const int l = e & 63, rg = (e >> 6) & 3, c = e >> 8;
+        for (int e = tid; e < NC * NRG * 64; e += 256) {
+            const int l = e & 63, rg = (e >> 6) % NRG, c = e / (64 * NRG);
             const int pr = pair_s[16 * rg + (l & 15)];
             uint4 v = make_uint4(0u, 0u, 0u, 0u);
             if (pr >= 0) v = *(const uint4 *)(a.QH + (int64_t)pr * a.dpad + 32 * c + 8 * (l >> 4));
-            ((uint4 *)(smem + RSmem::aq))[e] = v;
+            ((uint4 *)(smem + S::aq))[e] = v;
         }
         __syncthreads();
 
         // ---- per-row bound state (lane = row; qbound is always set here)
-        const float my_qn = qrec.x, my_qnorm = qrec.y, my_dq = qrec.w;
+        // my_qv: L2 qn = fl(||q'||^2), IP qc = fl(q.c); my_dq: L2 fl(||q - c||)
+        const float my_qv = qrec.x, my_qnorm = qrec.y, my_dq = qrec.w;
         const uint32_t *pub_at = a.qbound + (my_q >= 0 ? my_q : 0);  // (a padding row reads query 0's: unused)
         uint32_t pub = __hip_atomic_load(pub_at, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        float Tc = -1.0f, Ac = __builtin_inff(), triA = -__builtin_inff(), triB = __builtin_inff();
+        float Tc = -1.0f, triA = -__builtin_inff(), triB = __builtin_inff();
         // The screening error bound is the item's (its largest tile radius and hi
         // residual: err_E is monotone in both), so a row's threshold changes only
         // when its T does; Ew = the bound of every key this item lists (lane = row)
         const float Rb_item = TRI ? fminf(R, rup(__uint_as_float((uint32_t)meta[4]))) : R;
         const float hres_item = TRI && a.tres ? __uint_as_float((uint32_t)meta[5]) : -1.0f;
-        const float Ew = my_pair >= 0 ? errE_r(my_qnorm, Rb_item, hres_item, my_qres, dp) : 0.0f;
+        const float Ew = my_pair >= 0 ? errE_r<M>(my_qnorm, Rb_item, hres_item, my_qres, dp, my_qv, Rx, dd) : 0.0f;
+        // (IP) the Cauchy-Schwarz skip's slack: qc's rounding, search.cpp's exact sum
+        const float slk = M == LIRA_METRIC_IP && my_pair >= 0
+            ? (1.01f * __builtin_fabsf(my_qv) + (dd + 2.0f) * my_qnorm * Rx) * 0x1p-24f * 1.02f + 0x1p-120f : 0.0f;
         const int g4 = opaque(4 * g);  // (selection rows: 16 rg + g4 + reg)
         // T: the row's bound on its final k-th exact score (shared list, published bound).
         // No divergent branch (the published bound's load stays countable for the
@@ -439,25 +482,38 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
             const u64 kk = kth_s[lane];
             asm volatile("" ::: "memory");  // (the list's key first, then its bound: see flush_row)
             const float er = __uint_as_float(erun_s[lane]);
-            float T = kk != kEmptyKey ? rup(rup(key_score(kk) + er) * a.gP) + 0x1p-125f : __builtin_inff();
+            float T = bound_of(kk, er, a.gP);
             T = fminf(T, ord2f(pub));  // (~0u, nothing published: a NaN, which fminf ignores)
             pub = __hip_atomic_load(pub_at, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (__any(T != Tc)) {  // (recomputed for every lane: an unchanged T gives the same values)
                 Tc = T;
                 const bool fin = T < 3e38f;
-                Ac = fin ? rup(rup(fmaxf(T, 0.0f) + 0x1p-125f) * a.invF) : __builtin_inff();
-                // (v_sqrt_f32, <= 1 ulp: inside rup's 2^-20 margin)
-                const float rad = rup(__builtin_amdgcn_sqrtf(Ac));
-                triA = my_pair < 0 ? __builtin_inff() : fin ? rdn(rdn(my_dq) - rad) : -__builtin_inff();
-                triB = my_pair < 0 ? -__builtin_inff() : fin ? rup(rup(my_dq) + rad) : __builtin_inff();
+                const float Ac = lim_of<M>(T, a.invF);
+                if (M == LIRA_METRIC_L2) {
+                    // (v_sqrt_f32, <= 1 ulp: inside rup's 2^-20 margin)
+                    const float rad = rup(__builtin_amdgcn_sqrtf(Ac));
+                    triA = my_pair < 0 ? __builtin_inff() : fin ? rdn(rdn(my_dq) - rad) : -__builtin_inff();
+                    triB = my_pair < 0 ? -__builtin_inff() : fin ? rup(rup(my_dq) + rad) : __builtin_inff();
+                } else {
+                    // a tile can hold a candidate of exact score <= T only if its largest
+                    // radius reaches (-qc - slack - T) / ||q|| (||q|| rounded up)
+                    triA = my_pair < 0 ? __builtin_inff()
+                           : fin && my_qnorm > 0.0f ? rdn(rdn(rdn(-my_qv - slk) - Ac) / my_qnorm) : -__builtin_inff();
+                    triB = my_pair < 0 ? -__builtin_inff() : __builtin_inff();
+                }
                 // pass iff fl(-xadj + dot) >= h (lane = row), then the rows in selection order
                 float h = __builtin_inff();
                 if (my_pair >= 0) {
                     h = -__builtin_inff();
                     if (fin) {
-                        const float lim = rup(Ac + Ew), sq = my_qnorm + Rb_item;
-                        h = rdn(0.5f * (my_qn - lim) - (__builtin_fabsf(my_qn) + __builtin_fabsf(lim)) * 0x1p-22f -
-                                1.06f * 0x1p-24f * sq * sq);
+                        const float lim = rup(Ac + Ew);
+                        if (M == LIRA_METRIC_L2) {
+                            const float sq = my_qnorm + Rb_item;
+                            h = rdn(0.5f * (my_qv - lim) - (__builtin_fabsf(my_qv) + __builtin_fabsf(lim)) * 0x1p-22f -
+                                    1.06f * 0x1p-24f * sq * sq);
+                        } else {  // s~ = -fl(wv + qc) <= lim  =>  wv >= -lim - qc - (|lim| + |qc|) 2^-22
+                            h = rdn(rdn(-lim - my_qv) - (__builtin_fabsf(my_qv) + __builtin_fabsf(lim)) * 0x1p-22f);
+                        }
                     }
                     h = fmaxf(h, -3.40282347e38f);  // (padding, xadj = +inf, never passes)
                 }
@@ -472,8 +528,6 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
             return __all(r.y < triA || r.x > triB) != 0;
         };
 
-        RCLK(t_pro);
-        RACC(0, t_item, t_pro);
         update_T();
         if (u < nt && skip(u)) {
             do {
@@ -485,19 +539,12 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
         int ovf = 0;  // survivor queue fill (wave-uniform)
         // survivor queue -> this wave's row buffers (full ones merged into the lists)
         auto drain = [&]() {
-#ifdef RS_NODRAIN  // timing experiment: the queue is discarded (results invalid)
-            ovf = 0;
-            return;
-#endif
-            drain_buffers(lists, kth_s, mybuf, mybufc, lock_s, erun_s, opub_s, pair_s, rec_s, oq_key,
-                          (uint32_t)tbase * 64u, ovf, Ew, k, a.qbound, a.nprobe, a.gP, a, Tc);
+            drain_buffers<M, RL>(lists, kth_s, mybuf, mybufc, lock_s, erun_s, opub_s, pair_s, rec_s, oq_key,
+                                 (uint32_t)tbase * 64u, ovf, Ew, k, a, Tc);
             ovf = 0;
         };
 
-        RCLK(t_loop0);
-        RACC(1, t_pro, t_loop0);
         while (u < nt) {
-            RCLK(t_a);
             const rf4 xa = xa_n;
             // ---- the row bounds (thresholds rewritten where one changed)
             update_T();
@@ -509,92 +556,64 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
                 un += kRW;
             }
             const int ul = un < nt ? un : u;  // (the last tile's loads repeat the current tile)
-#ifdef RS_SAMETILE  // timing experiment: every load reads the item's first tile (L2-resident)
-            const char *cbase = a.Xb + (int64_t)tbase * tile_bytes + lane_off, *nbase = cbase;
-#else
             const char *cbase = a.Xb + (int64_t)(tbase + u) * tile_bytes + lane_off;
             const char *nbase = a.Xb + (int64_t)(tbase + ul) * tile_bytes + lane_off;
-#endif
             xa_n = *(const rf4 *)(a.xadj + (int64_t)(tbase + ul) * 64 + 4 * cj);
             // the rows' thresholds in selection order (read under the MFMAs)
-            rf4 hv[4];
+            rf4 hv[NRG];
 #pragma unroll
-            for (int rg = 0; rg < 4; ++rg) hv[rg] = *(const rf4 *)(myh + 16 * rg + g4);
-            RCLK(t_b);
-            RACC(2, t_a, t_b);
+            for (int rg = 0; rg < NRG; ++rg) hv[rg] = *(const rf4 *)(myh + 16 * rg + g4);
 
-            // ---- 64 rows x 64 candidates: acc = -xadj + dot (the first chunk's MFMAs
+            // ---- QR rows x 64 candidates: acc = -xadj + dot (the first chunk's MFMAs
             // take C = -xadj of their candidate; lane (g, j) holds candidates 4 j + i
             // of rows 4 g + reg, so C is the same for every row group); each B
-            // fragment's slot reloaded after its 4 MFMAs
-            rf4 acc[4][4];
-            // per chunk: the A fragments (LDS), this chunk's 16 MFMAs, the slot's
+            // fragment's slot reloaded after its NRG MFMAs
+            rf4 acc[NRG][4];
+            // per chunk: the A fragments (LDS), this chunk's MFMAs, the slot's
             // reloads; a scheduling barrier per chunk keeps the reloads where they are
             // (left alone, hipcc sank them next to their consumers)
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
                 const int sl = c % RS, cn = c + RS;  // slot; the chunk that goes into it next
-                rbf16x8 Acur[4];
+                rbf16x8 Acur[NRG];
 #pragma unroll
-                for (int rg = 0; rg < 4; ++rg) Acur[rg] = __builtin_bit_cast(rbf16x8, aq_s[(c * 4 + rg) * 64 + lane]);
+                for (int rg = 0; rg < NRG; ++rg) Acur[rg] = __builtin_bit_cast(rbf16x8, aq_s[(c * NRG + rg) * 64 + lane]);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const rf4 cx = (rf4)(-xa[i]);
 #pragma unroll
-                    for (int rg = 0; rg < 4; ++rg)
-#ifdef RS_NOMFMA  // timing experiment: no MFMAs (results invalid)
-                        acc[rg][i] = c == 0 ? cx : acc[rg][i] + (rf4)((float)Acur[rg][0] * (float)B[sl][i][0] * 0.0f);
-#else
+                    for (int rg = 0; rg < NRG; ++rg)
                         acc[rg][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Acur[rg], B[sl][i], c == 0 ? cx : acc[rg][i],
                                                                              0, 0, 0);
-#endif
                     B[sl][i] = cn < NC ? *(const rbf16x8 *)(cbase + cn * 8192 + i * 256)
                                        : *(const rbf16x8 *)(nbase + (cn - NC) * 8192 + i * 256);
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
             ++n_tiles;
-#ifdef RS_CLOCKS
-            if (vp < a.n_lists && a.n_virt > a.n_lists) ++tiles_g0;
-#endif
-            RCLK(t_c);
-            RACC(3, t_b, t_c);
 
             // ---- selection: pass iff acc = -xadj + dot >= h.  Per (row group, register)
             // entry e = 4 rg + reg, lane group g holds row 16 rg + 4 g + reg: four
             // compares into wave masks (one per candidate slot i), skipped together
             // when all are empty; each non-empty mask's lanes append (wv, position,
-            // row) to the wave's survivor queue at slots from the mask's prefix count,
-            // a mask that would overflow the queue draining it first
-            RCLK(t_d);
-            RACC(4, t_c, t_d);
-            const uint32_t lpos0 = (uint32_t)(u * 64 + 4 * cj);
+            // row) to the wave's survivor queue at slots from the mask's prefix count.
             // The pass runs over (entry, half) steps h = 2 e + (i >> 1); a step that
             // would overflow the queue stops it there, the queue is drained (one
             // inlined call site) and the pass resumes at that step (rare)
-#ifdef RS_NOSEL  // timing experiment: no selection (results invalid)
-            if (__builtin_amdgcn_readfirstlane(lane) == 0) {
-                float z = 0.0f;
-#pragma unroll
-                for (int rg = 0; rg < 4; ++rg)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) z += acc[rg][i][0];
-                if (z == 12345.0f) n_surv += 1;
-            } else
-#endif
+            const uint32_t lpos0 = (uint32_t)(u * 64 + 4 * cj);
             for (int s0 = 0;;) {
                 // (the accumulators as if redefined: keeps the compares from being
                 // hoisted out of this loop, which cost 64 masks held in SGPRs)
 #pragma unroll
-                for (int rg = 0; rg < 4; ++rg)
+                for (int rg = 0; rg < NRG; ++rg)
 #pragma unroll
                     for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(acc[rg][i]));
                 // (likewise the entries' low words: row << 16 | position, from one value
                 // per pass -- hoisted, the 32 precomputed words were spilled)
                 const uint32_t low0 = (uint32_t)opaque((int)(((uint32_t)g4 << 16) | lpos0));
-                int stop = 32;
+                int stop = NSTEP;
 #pragma unroll
-                for (int rg = 0; rg < 4; ++rg) {
+                for (int rg = 0; rg < NRG; ++rg) {
 #pragma unroll
                     for (int reg = 0; reg < 4; ++reg) {
                         const int e = 4 * rg + reg;
@@ -604,9 +623,6 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
 #pragma unroll
                         for (int i = 0; i < 4; ++i) m[i] = __ballot(acc[rg][i][reg] >= hp);
                         if (!(m[0] | m[1] | m[2] | m[3])) continue;
-#ifdef RS_CLOCKS
-                        clk[7] += 1ull << 32;  // (entries with survivors, high half)
-#endif
                         const uint32_t low = low0 + ((uint32_t)(16 * rg + reg) << 16);
 #pragma unroll
                         for (int hf = 0; hf < 2; ++hf) {
@@ -620,12 +636,6 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
                                 continue;
                             }
                             n_surv += (unsigned long long)n;
-#ifdef RS_CLOCKS
-                            if (vp < a.n_lists && a.n_virt > a.n_lists) surv_g0 += (unsigned long long)n;
-#endif
-#ifdef RS_NOSURV  // timing experiment: survivors dropped (results invalid)
-                            continue;
-#endif
                             // queue entry: fl(-xadj + dot) bits | row << 16 | position in the item
                             if ((ma >> lane) & 1ull)
                                 oq_key[ovf + mbcnt64(ma)] = ((u64)__float_as_uint(acc[rg][2 * hf][reg]) << 32) | (low + 2u * hf);
@@ -636,54 +646,49 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
                         }
                     }
                 }
-                if (stop == 32) break;
-#ifdef RS_CLOCKS
-                n_skip += 1ull << 32;  // (mid-selection drains, high half)
-#endif
+                if (stop == NSTEP) break;
                 drain();
                 s0 = stop;
             }
-            RCLK(t_e);
-            RACC(5, t_d, t_e);
             u = un;
         }
         if (ovf) drain();
         if (wave == kRW - 1 && lane == 0) claim_into_meta();  // (the next item; read after the barriers below)
-        RCLK(t_epi);
 
         // ---- item epilogue: every wave's buffers into the lists (rows split over
         // the waves, two per pass: one per half-wave), then the lists out
         if (mybufc[lane] > 0) atomicMax(erun_s + lane, __float_as_uint(Ew));
         __syncthreads();
         const int ln = opaque(lane);  // (lane-derived addresses computed here, not hoisted)
+        constexpr int RPW = QR / kRW;  // rows per wave
 #pragma unroll 1
-        for (int j = 0; j < 16; j += 2) {
-            const int hl = ln & 31, row = wave * 16 + j + (ln >> 5);
-            const int c0 = bufc[0 * kRQ + row], c1 = bufc[1 * kRQ + row], c2 = bufc[2 * kRQ + row],
-                      c3 = bufc[3 * kRQ + row];
+        for (int j = 0; j < RPW; j += 2) {
+            const int hl = ln & 31, row = wave * RPW + j + (ln >> 5);
+            const int c0 = bufc[0 * 64 + row], c1 = bufc[1 * 64 + row], c2 = bufc[2 * 64 + row], c3 = bufc[3 * 64 + row];
             const int n = c0 + c1 + c2 + c3;
             if (!__any(n > 0)) continue;
-#ifdef RS_NOEPI  // timing experiment: buffers not merged at the item's end (results invalid)
-            continue;
-#endif
-            const float qn_r = rec_s[row].x;
+            const float qv_r = rec_s[row].x;
             for (int r0 = 0; __any(n > r0); r0 += 32) {
                 const int e = r0 + hl;
                 u64 b = kEmptyKey;
                 if (e < n) {
                     const int w = e < c0 ? 0 : e < c0 + c1 ? 1 : e < c0 + c1 + c2 ? 2 : 3;
                     const int off = e - (w == 0 ? 0 : w == 1 ? c0 : w == 2 ? c0 + c1 : c0 + c1 + c2);
-                    b = wkey_to_key(bufs[(w * kRQ + row) * kRBC + off], qn_r);
+                    b = wkey_to_key<M>(bufs[(w * QR + row) * kRBC + off], qv_r);
                 }
-                u64 lst[1] = {lists[row * kRK2 + hl]};
+                u64 lst[RL];
+#pragma unroll
+                for (int r = 0; r < RL; ++r) lst[r] = lists[row * K2 + r * 32 + hl];
                 if (a.spill) {
-                    const u64 ev = merge_evict(lst, b);
-                    lists[row * kRK2 + hl] = lst[0];
-                    spill_evicted(a, ev, true, shfl64(lst[0], (ln & 32) + k - 1), __uint_as_float(erun_s[row]),
-                                  __shfl(Tc, row, 64), pair_s[row]);
+                    const u64 ev = merge_evict<RL>(lst, b);
+#pragma unroll
+                    for (int r = 0; r < RL; ++r) lists[row * K2 + r * 32 + hl] = lst[r];
+                    spill_evicted<M>(a, ev, true, list_at<RL>(lst, k - 1), __uint_as_float(erun_s[row]),
+                                     __shfl(Tc, row, 64), pair_s[row]);
                 } else {
-                    half_merge_batch1<1>(lst, b);
-                    lists[row * kRK2 + hl] = lst[0];
+                    half_merge_batch1<RL>(lst, b);
+#pragma unroll
+                    for (int r = 0; r < RL; ++r) lists[row * K2 + r * 32 + hl] = lst[r];
                 }
                 __builtin_amdgcn_wave_barrier();
             }
@@ -692,89 +697,82 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
         // (sorted lists: the keys, the first empty one and the last slot are all
         // k_smerge reads -- its walk stops at the first key beyond its limit)
 #pragma unroll 1
-        for (int j = 0; j < 16; j += 2) {
-            const int hl = ln & 31, row = wave * 16 + j + (ln >> 5);
+        for (int j = 0; j < RPW; j += 2) {
+            const int hl = ln & 31, row = wave * RPW + j + (ln >> 5);
             const int pr = pair_s[row];
-            const u64 key = lists[row * kRK2 + hl];
-            const u64 full = __ballot(key != kEmptyKey);
-            const int nv = __builtin_popcount((uint32_t)(ln >> 5 ? full >> 32 : full));
-            if (pr >= 0 && (hl <= nv || hl == kRK2 - 1)) a.partial[((int64_t)pr * a.nch_max + ch) * kRK2 + hl] = key;
+            u64 key[RL];
+            int nv = 0;
+#pragma unroll
+            for (int r = 0; r < RL; ++r) {
+                key[r] = lists[row * K2 + r * 32 + hl];
+                const u64 full = __ballot(key[r] != kEmptyKey);
+                nv += __builtin_popcount((uint32_t)(ln >> 5 ? full >> 32 : full));
+            }
+            if (pr >= 0) {
+                u64 *dst = a.partial + ((int64_t)pr * a.nch_max + ch) * K2;
+#pragma unroll
+                for (int r = 0; r < RL; ++r) {
+                    const int e = r * 32 + hl;
+                    if (e <= nv || e == K2 - 1) dst[e] = key[r];
+                }
+            }
         }
         if (my_pair >= 0) {
             const float er = __uint_as_float(erun_s[lane]);
             a.pE[(int64_t)my_pair * a.nch_max + ch] = fmaxf(er, 0x1p-126f);  // (>= every listed key's bound)
-            const u64 kk = lists[lane * kRK2 + k - 1];
-            if (a.qbound && kk != kEmptyKey)
-                atomicMin(a.qbound + my_q, f2ord(rup(rup(key_score(kk) + er) * a.gP) + 0x1p-125f));
+            const u64 kk = lists[lane * K2 + k - 1];
+            if (a.qbound && kk != kEmptyKey) atomicMin(a.qbound + my_q, f2ord(bound_of(kk, er, a.gP)));
         }
         if (g0 && ch == 0 && a.done0) {  // the query block's later chunks may start
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this wave's published bounds landed)
             __syncthreads();
             if (tid == 0) atomicAdd(a.done0 + qblk, 1);
         }
-        RCLK(t_end);
-        RACC(6, t_epi, t_end);
-#ifdef RS_CLOCKS
-        clk[7] += 1;
-#endif
     }
-#ifdef RS_CLOCKS
-    if (lane == 0) {
-        for (int i = 0; i < 8; ++i) atomicAdd(&g_rs_clk[i], clk[i]);
-        atomicAdd(&g_rs_clk[8], n_tiles);
-        atomicAdd(&g_rs_clk[9], n_skip);
-        atomicAdd(&g_rs_clk[10], 1ull);
-        atomicAdd(&g_rs_clk[11], n_surv);
-        atomicAdd(&g_rs_clk[13], surv_g0);
-        atomicAdd(&g_rs_clk[14], tiles_g0);
-    }
-#endif
     if (a.stats && lane == 0) {
-        atomicAdd(a.stats + 0, n_tiles * 64ull * 64ull);  // (row, candidate) pairs screened
-        atomicAdd(a.stats + 2, n_tiles);                   // tiles computed (of 64 candidates)
-        atomicAdd(a.stats + 4, n_skip);                    // tiles skipped by the triangle test
-        atomicAdd(a.stats + 7, n_surv);                    // survivors appended
+        atomicAdd(a.stats + 0, n_tiles * (unsigned long long)QR * 64ull);  // (row, candidate) pairs screened
+        atomicAdd(a.stats + 2, n_tiles);                                   // tiles computed (of 64 candidates)
+        atomicAdd(a.stats + 4, n_skip);                                    // tiles skipped by the triangle test
+        atomicAdd(a.stats + 7, n_surv);                                    // survivors appended
     }
 }
 
-}  // namespace lira
+bool rscreen_shape_ok(int64_t dpad, int64_t k) {
+    return k >= 1 && k <= 120 && dpad >= 32 && dpad <= 128 && dpad % 32 == 0;
+}
+int rscreen_smem(int rl) { return rl == 1 ? RSmem<1>::total : rl == 2 ? RSmem<2>::total : RSmem<4>::total; }
 
-namespace lira {
-
-bool rscreen_shape_ok(int64_t dpad, int64_t k) { return k >= 1 && k <= 24 && dpad >= 32 && dpad <= 128 && dpad % 32 == 0; }
-int rscreen_smem() { return RSmem::total; }
-
-template <int NC>
+template <int NC, int M, int RL>
 static hipError_t launch_r(const RArgs &a, int grid, hipStream_t st) {
     static std::atomic<uint64_t> attr{0};
-    hipError_t e = set_smem_attr_once(attr, (const void *)k_screen_r<NC>, RSmem::total);
+    hipError_t e = set_smem_attr_once(attr, (const void *)k_screen_r<NC, M, RL>, RSmem<RL>::total);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_screen_r<NC>), dim3(grid), dim3(256), RSmem::total, st, a);
+    hipLaunchKernelGGL((k_screen_r<NC, M, RL>), dim3(grid), dim3(256), RSmem<RL>::total, st, a);
     return hipGetLastError();
 }
 
-#ifdef RS_CLOCKS
-}  // namespace lira
-// slots: 0 item prologue, 1 first tile setup, 2 thresholds, 3 MFMA loop (+ its loads' waits),
-// 4 pass masks, 5 survivor queue (+ drains), 6 epilogue, 7 items; 8 tiles, 9 skipped tiles, 10 waves
-extern "C" int lira_debug_rs_clocks(unsigned long long *out16) {
-    hipDeviceSynchronize();
-    hipMemcpyFromSymbol(out16, HIP_SYMBOL(lira::g_rs_clk), 16 * 8);
-    unsigned long long z[16] = {0};
-    hipMemcpyToSymbol(HIP_SYMBOL(lira::g_rs_clk), z, 16 * 8);
-    return 0;
-}
-namespace lira {
-#endif
-
-hipError_t launch_rscreen(const RArgs &a, int grid, hipStream_t st) {
+template <int M, int RL>
+static hipError_t launch_rm(const RArgs &a, int grid, hipStream_t st) {
     switch (a.dpad / 32) {
-        case 1: return launch_r<1>(a, grid, st);
-        case 2: return launch_r<2>(a, grid, st);
-        case 3: return launch_r<3>(a, grid, st);
-        case 4: return launch_r<4>(a, grid, st);
+        case 1: return launch_r<1, M, RL>(a, grid, st);
+        case 2: return launch_r<2, M, RL>(a, grid, st);
+        case 3: return launch_r<3, M, RL>(a, grid, st);
+        case 4: return launch_r<4, M, RL>(a, grid, st);
         default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_rscreen(const RArgs &a, int rl, int grid, hipStream_t st) {
+    if (a.metric == LIRA_METRIC_L2) {
+        if (rl == 1) return launch_rm<LIRA_METRIC_L2, 1>(a, grid, st);
+        if (rl == 2) return launch_rm<LIRA_METRIC_L2, 2>(a, grid, st);
+        if (rl == 4) return launch_rm<LIRA_METRIC_L2, 4>(a, grid, st);
+    } else {
+        if (rl == 1) return launch_rm<LIRA_METRIC_IP, 1>(a, grid, st);
+        if (rl == 2) return launch_rm<LIRA_METRIC_IP, 2>(a, grid, st);
+        if (rl == 4) return launch_rm<LIRA_METRIC_IP, 4>(a, grid, st);
+    }
+    return hipErrorInvalidValue;
 }
 
 }  // namespace lira

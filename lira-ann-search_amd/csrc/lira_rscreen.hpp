@@ -6,18 +6,20 @@
 namespace lira {
 
 struct RArgs {
-    const char *Xb;          // split-bf16 copy (bytes): per tile and 16-dim chunk 4 KiB [g 4][p 64][8 bf16]
-    const float *xadj;       // centred fl(||x'||^2)/2 per storage row (+inf: padding)
+    int metric;              // LIRA_METRIC_L2, or LIRA_METRIC_IP on a centred index (lira_index::ipc)
+    const char *Xb;          // split-bf16 copy (bytes) of x' = fl(x - c): per tile and 16-dim chunk 4 KiB [g 4][p 64][8 bf16]
+    const float *xadj;       // per storage row: L2 fl(||x'||^2)/2, IP 0 (+inf: padding)
     const float *rmax;       // per list: max ||x'|| (centred)
-    const float2 *tstat;     // per tile: lo <= ||x - c|| <= hi (NULL: no triangle skip)
+    const float *rmaxx;      // per list: max ||x|| (IP: the exact sum's rounding term)
+    const float2 *tstat;     // per tile: lo <= ||x - c|| <= hi (NULL: no triangle / Cauchy-Schwarz skip)
     const float *tres;       // per tile: max ||x' - hi(x')||
     const int32_t *tile_off, *cnt, *qoff, *qlist;
     const int4 *itab;        // item -> (virtual partition, query block, chunk, -)
     int32_t *head;           // plan counters / XCD queue bounds (k_plan)
-    const float4 *QN;        // per pair: qn = fl(||q'||^2), ||q'|| (up), pair, fl(||q - c||)
+    const float4 *QN;        // per pair: qn = fl(||q'||^2), ||q'|| (up), pair, fl(||q - c||); IP: qc = fl(q.c), ||q|| (up), pair, qc
     const float *QE;         // per pair: ||q' - hi(q')|| (up)
     const uint16_t *QH;      // per pair: hi(q') as bf16, dpad dims
-    u64 *partial;            // [pair][nch_max][32] row lists (k_smerge's input)
+    u64 *partial;            // [pair][nch_max][32 RL] row lists (k_smerge's input)
     float *pE;               // [pair][nch_max] each list's screening-error bound
     uint32_t *qbound;        // [nq] f2ord(bound on the final k-th exact score)
     int64_t d, dpad;
@@ -31,10 +33,11 @@ struct RArgs {
     int scap;
 };
 
-// the shapes k_screen_r implements: L2 on the centred split copy, hi x hi,
-// k <= 24 (32-key row lists), dpad <= 128 (the queries' hi parts in registers)
+// the shapes k_screen_r implements: L2 or IP on the centred split copy, hi x hi,
+// k <= 120 (row lists of 32 RL keys, RL = 1 / 2 / 4 for k <= 24 / 56 / 120; 64
+// query rows per item at RL 1, else 32), dpad <= 128 (the rows' hi parts in LDS)
 bool rscreen_shape_ok(int64_t dpad, int64_t k);
-int rscreen_smem();
-hipError_t launch_rscreen(const RArgs &a, int grid, hipStream_t st);
+int rscreen_smem(int rl);
+hipError_t launch_rscreen(const RArgs &a, int rl, int grid, hipStream_t st);
 
 }  // namespace lira

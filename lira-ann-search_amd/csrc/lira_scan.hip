@@ -1128,14 +1128,8 @@ static int exact_topk(lira_index *idx, const float *q, int64_t nq, const int32_t
     const int RL = scan_rl(k);
     ScanPlan pl = make_plan(idx, nq, nprobe, k);
     if (!ws) {
-        if (idx->ws_bytes < pl.total) {
-            if (idx->ws) hipFree(idx->ws);
-            idx->ws = nullptr;
-            idx->ws_bytes = 0;
-            LIRA_HIP_TRY(hipMalloc(&idx->ws, pl.total));
-            idx->ws_bytes = pl.total;
-        }
-        ws = idx->ws;
+        const int rc = cached_workspace(idx, pl.total, st, &ws);
+        if (rc != LIRA_OK) return rc;
     } else if (ws_bytes < pl.total) {
         return fail(LIRA_EINVAL, "workspace too small: need " + std::to_string(pl.total) + " bytes");
     }
@@ -1285,6 +1279,7 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
         for (int i = 0; i < 4; ++i) ev[i] = idx->ev_pool[idx->ev_used + i];
         idx->ev_used += 4;
     }
+    if (idx->stats_on) idx->stats_paths |= scr ? 2 : 1;
     const int rc = scr ? screen_topk(idx, q, nq, probe, nprobe, k, flags, Rm, out_D, out_I, out_ncand, ws, ws_bytes,
                                      st, ev)
                        : exact_topk(idx, q, nq, probe, nprobe, k, flags, Rm, out_D, out_I, out_ncand, ws, ws_bytes,

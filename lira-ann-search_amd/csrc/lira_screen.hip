@@ -2059,13 +2059,14 @@ __global__ __launch_bounds__(256) void k_rescan(RescanArgs a) {
 __global__ __launch_bounds__(256) void k_pairs(const float *Q, int64_t d, const int32_t *probe, int64_t npairs,
                                                int nprobe, int n_lists, const float *pivot, int centred,
                                                const float2 *lstat, const uint32_t *qbound, int32_t *probe_live,
-                                               float4 *QN, float *QE, float *pqn, uint16_t *QH, int64_t dpad) {
+                                               float4 *QN, float *QE, float *pqn, uint16_t *QH, int64_t dpad,
+                                               const float *rmx) {
     const int64_t pair = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
     const bool valid = pair < npairs;
     const int praw = valid ? probe[pair] : -1;
     const uint32_t qb = valid && lstat && qbound ? qbound[pair / nprobe] : ~0u;
     pair_record(Q, d, pair, valid, praw, nprobe, n_lists, pivot, centred, lstat && qbound ? lstat : nullptr, qb,
-                probe_live, QN, QE, pqn, QH, dpad);
+                probe_live, QN, QE, pqn, QH, dpad, nullptr, nullptr, rmx);
 }
 
 // (stats on) what the plan's partition filter removed: pairs whose probe slot
@@ -2090,11 +2091,11 @@ __global__ __launch_bounds__(256) void k_prune_stats(const int32_t *probe, const
 static hipError_t launch_pairs(const float *Q, int64_t d, const int32_t *probe, int64_t npairs, int nprobe,
                                int n_lists, const float *pivot, int centred, const float2 *lstat,
                                const uint32_t *qbound, int32_t *probe_live, float4 *QN, float *QE, float *pqn,
-                               uint16_t *QH, int64_t dpad, hipStream_t st) {
+                               uint16_t *QH, int64_t dpad, const float *rmx, hipStream_t st) {
     const unsigned g = (unsigned)((npairs * 16 + 255) / 256);
     if (g == 0) return hipSuccess;
     hipLaunchKernelGGL(k_pairs, dim3(g), dim3(256), 0, st, Q, d, probe, npairs, nprobe, n_lists, pivot, centred, lstat,
-                       qbound, probe_live, QN, QE, pqn, QH, dpad);
+                       qbound, probe_live, QN, QE, pqn, QH, dpad, rmx);
     return hipGetLastError();
 }
 
@@ -2137,8 +2138,17 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     SPlan pl;
     const lira_opts &op = idx->opt;
     pl.rl = screen_rl(k);
-    // the split-bf16 screen unless asked off (it is the only one without the fp32 tiles)
-    const bool split_wanted = (op.split && !(flags & LIRA_SCAN_NO_SPLIT)) || !idx->X;
+    const int xhi = op.xhi >= 0 ? op.xhi : idx->pivot != nullptr && (idx->metric == LIRA_METRIC_L2 || idx->ipc) ? 2 : 0;
+    // k_screen_r (lira_rscreen.hip): the hi x hi screen on the centred split copy, L2
+    // or centred IP (q.x = q.fl(x - c) + q.c), k <= 120 (RL 1: 64 queries per item;
+    // RL 2, 4: 32), dpad <= 128, with the per-query seed, not PER_PARTITION
+    const int rs_qr = pl.rl == 1 ? 64 : 32;
+    const bool rs = op.rscreen && (op.split || !idx->X) && (op.mfma || !idx->X) && op.seed && !(flags & (LIRA_SCAN_NO_SPLIT | LIRA_SCAN_PER_PARTITION)) &&
+                    idx->Xb && idx->xadjc && idx->pivot && idx->lstat && rscreen_shape_ok(idx->dpad, k) && xhi == 2 &&
+                    (op.qr == 0 || op.qr == rs_qr) && (idx->metric == LIRA_METRIC_L2 || idx->ipc);
+    // the split-bf16 screen unless asked off (it is the only one without the fp32
+    // tiles); a centred IP copy has no k_screen_m form: the fp32 tiles there
+    const bool split_wanted = idx->ipc ? rs : (op.split && !(flags & LIRA_SCAN_NO_SPLIT)) || !idx->X;
     // MFMA screen up to RL 4 (k <= 120) on the split-bf16 copy (DEEP10M's k =
     // 100: 24.1 ms against 33.3 ms on the VALU screen); the fp32 MFMA form
     // (no split copy or LIRA_OPT_SPLIT = 0) only while its LDS fits 2
@@ -2172,7 +2182,6 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // 1.44 ms latent, 0.47 -> 0.41 mixture; GIST1M 1.03 -> 0.77 latent, 0.84 ->
     // 0.67 mixture (survivors +4 %: the bound's extra ||q - qh|| R is small
     // against the score spread)
-    const int xhi = op.xhi >= 0 ? op.xhi : idx->metric == LIRA_METRIC_L2 && idx->pivot != nullptr ? 2 : 0;
     if (pl.split && xhi && pl.qr != 32 && pl.rl <= (pl.qr == 64 ? 4 : 1)) pl.split = 2;
     if (pl.split == 2 && xhi == 2 && pl.qr == 64 && pl.rl == 1) pl.split = 3;
     // (round 3 measured a pipelined NS-slot ring screen, k_screen_s, slower on
@@ -2184,9 +2193,15 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // k_screen_r where it applies (its own preconditions on the scan's flags are in screen_topk)
     // (with or without the fp32 tiles: the seed then comes from the row-major copy
     // and the per-pair records from k_pairs -- BIGANN-100M's compact index)
-    pl.rs = op.rscreen && pl.split == 3 && idx->metric == LIRA_METRIC_L2 && idx->xadjc && idx->pivot &&
-            rscreen_shape_ok(idx->dpad, k) && !(flags & LIRA_SCAN_PER_PARTITION) && op.seed && idx->lstat;
-    pl.smem = !pl.mfma       ? screen_smem(pl.qr, pl.rl)
+    pl.rs = rs;
+    if (rs) {
+        pl.mfma = 1;
+        pl.split = 3;
+        pl.qr = rs_qr;
+        pl.pp = 1;
+    }
+    pl.smem = pl.rs          ? rscreen_smem(pl.rl)
+              : !pl.mfma     ? screen_smem(pl.qr, pl.rl)
               : pl.qr == 128 ? (pl.split == 2 ? SSmem<128, 1, true, true>::total
                                 : pl.rl == 1 ? SSmem<128, 1, true>::total : SSmem<128, 2, true>::total)
               : pl.split == 3 ? SSmem<64, 1, true, false, true>::total
@@ -2236,7 +2251,7 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // k_screen_m stages the radius ranges of an item's first kBR blocks in LDS; a
     // longer item would read them from global memory inside the ring (whose
     // compiler-inserted waits drain it): cap the chunk at kBR blocks
-    if (pl.mfma && idx->metric == LIRA_METRIC_L2 && idx->pivot) {
+    if (pl.mfma && idx->pivot && (idx->metric == LIRA_METRIC_L2 || pl.rs)) {
         pl.bpc = std::min(pl.bpc, SSmem<64, 1, true>::kBR);
         pl.bpc_near = std::min(pl.bpc_near, pl.bpc);
     }
@@ -2277,7 +2292,7 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
         pl.rq_cap = (int)std::min<int64_t>(INT32_MAX / 2, 2 * nq + 4096);
         pl.rcap = (int)std::max<int64_t>(256, (4 * k + 63) / 64 * 64);
     }
-    pl.scap = pl.rs && !(flags & LIRA_SCAN_PER_PARTITION) ? (op.spill < 0 ? 256 : op.spill) : 0;
+    pl.scap = pl.rs && !(flags & LIRA_SCAN_PER_PARTITION) ? (op.spill < 0 ? 256 * pl.rl : op.spill) : 0;
     size_t o = 0;
     auto take = [&](size_t bytes) {
         size_t at = o;
@@ -2337,6 +2352,22 @@ std::string screen_describe(const lira_index *idx, int64_t nq, int64_t nprobe, i
                             : "k_screen VALU v_pk_fma_f32";
     s += " RL=" + std::to_string(pl.rl) + " QR=" + std::to_string(pl.qr) + " K2=" + std::to_string(pl.K2) +
          " grid=" + std::to_string(pl.grid) + " smem=" + std::to_string(pl.smem);
+    // the plan (chunking, groups, seed, spill / re-scan): a PMC record of another plan
+    // does not describe this launch's traffic (bench.py matches the whole string)
+    const lira_opts &o = idx->opt;
+    const bool per_part = (flags & LIRA_SCAN_PER_PARTITION) != 0;
+    const bool fill = nq >= (int64_t)pl.qr * idx->n_lists || nq * nprobe >= 4 * (int64_t)pl.qr * idx->n_lists;
+    const int groups = !per_part && o.two_phase && nprobe >= 2 && (o.two_phase == 2 || fill) ? 2 : 1;
+    const bool fused = pl.pp && o.seed && idx->X && idx->metric == LIRA_METRIC_L2 && k <= 32 && idx->d <= 256;
+    const int seed_t = !o.seed ? 0 : fused ? (o.seed_tiles > 0 ? o.seed_tiles : nq < 4096 ? 4 : 2)
+                       : idx->X && k <= 32 ? (idx->metric != LIRA_METRIC_L2 ? 2 : o.seed_tiles > 0 ? o.seed_tiles
+                                                                                   : idx->d > 512 ? 1 : 2)
+                       : 4;
+    s += " plan: groups=" + std::to_string(groups) + " bpc=" + std::to_string(pl.bpc) +
+         " near=" + std::to_string(groups == 2 ? pl.bpc_near_min : pl.bpc) + ".." +
+         std::to_string(groups == 2 ? pl.bpc_near : pl.bpc) + " near0=" + std::to_string(groups == 2 ? pl.near0 : 0) +
+         " seed=" + std::to_string(seed_t) + (fused ? "f" : "") + " spill=" + std::to_string(pl.scap) +
+         " rescan=" + std::to_string(pl.prescan);
     return s;
 }
 
@@ -2416,14 +2447,8 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     const bool per_part = (flags & LIRA_SCAN_PER_PARTITION) != 0;
     SPlan pl = make_splan(idx, nq, nprobe, k, flags);
     if (!ws) {
-        if (idx->ws_bytes < pl.total) {
-            if (idx->ws) hipFree(idx->ws);
-            idx->ws = nullptr;
-            idx->ws_bytes = 0;
-            LIRA_HIP_TRY(hipMalloc(&idx->ws, pl.total));
-            idx->ws_bytes = pl.total;
-        }
-        ws = idx->ws;
+        const int rc = cached_workspace(idx, pl.total, st, &ws);
+        if (rc != LIRA_OK) return rc;
     } else if (ws_bytes < pl.total) {
         return fail(LIRA_EINVAL, "workspace too small: need " + std::to_string(pl.total) + " bytes");
     }
@@ -2542,9 +2567,9 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     }
     if (plive && !fused)
         LIRA_HIP_TRY(launch_pairs(q, idx->d, probe, npairs, (int)nprobe, (int)idx->n_lists, idx->pivot,
-                                  centred ? 1 : 0, filter ? idx->lstat : nullptr, filter ? qbound : nullptr, plive,
-                                  pl.pp ? QN : nullptr, pl.pp ? QE : nullptr, pl.pp ? pqn : nullptr, QH, idx->dpad,
-                                  st));
+                                  idx->ipc ? 2 : centred ? 1 : 0, filter ? idx->lstat : nullptr, filter ? qbound : nullptr,
+                                  plive, pl.pp ? QN : nullptr, pl.pp ? QE : nullptr, pl.pp ? pqn : nullptr, QH, idx->dpad,
+                                  idx->rmax, st));
     const int32_t *pprobe = plive ? plive : probe;  // the pairs that become work
     const int nvirt = groups * (int)idx->n_lists;
     LIRA_HIP_TRY(launch_plan(idx, pprobe, npairs, (int)nprobe, pl.bpc, groups == 2 ? pl.bpc_near : pl.bpc, pl.qr, groups, cnt, cursor, qoff, item_off,
@@ -2618,8 +2643,13 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     a.stats = idx->stats_on ? (unsigned long long *)idx->stats : nullptr;
     hipError_t e;
     bool spilled = false;
-    if (pl.rs && plive && pl.pp && centred && qbound && pl.bpc <= 128 && pl.bpc_near <= 128) {
+    const bool rs_go = pl.rs && plive && pl.pp && centred && qbound && pl.bpc <= 128 && pl.bpc_near <= 128;
+    if (idx->ipc && pl.split && !rs_go)  // (make_splan takes the split copy of a centred IP index only for k_screen_r)
+        return fail(LIRA_EHIP, "internal: centred IP split plan without k_screen_r");
+    if (rs_go) {
         RArgs r;
+        r.metric = idx->metric;
+        r.rmaxx = idx->rmax;
         r.Xb = (const char *)idx->Xb;
         r.xadj = idx->xadjc;
         r.rmax = idx->rmaxc;
@@ -2645,16 +2675,17 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
         r.k = (int)k;
         r.bpc = pl.bpc;
         r.nch_max = pl.nch_max;
-        const double g = ((double)idx->d + 4.0) * 0x1p-24;
-        r.gP = std::nextafter((float)((1.0 + g) * (1.0 + 0x1p-50)), INFINITY);
-        r.invF = std::nextafter((float)((1.0 / (1.0 - g)) * (1.0 + 0x1p-50)), INFINITY);
+        // (IP: bound_P / s_lim carry no (1 +- g) factor, err_E covers the exact sum's rounding)
+        const double g = idx->metric == LIRA_METRIC_L2 ? ((double)idx->d + 4.0) * 0x1p-24 : 0.0;
+        r.gP = g > 0.0 ? std::nextafter((float)((1.0 + g) * (1.0 + 0x1p-50)), INFINITY) : 1.0f;
+        r.invF = g > 0.0 ? std::nextafter((float)((1.0 / (1.0 - g)) * (1.0 + 0x1p-50)), INFINITY) : 1.0f;
         r.stats = a.stats;
         r.done0 = groups == 2 && pl.near0 > 0 ? (int32_t *)(w + pl.off_done) : nullptr;
         r.spill = pl.scap ? (uint4 *)(w + pl.off_spill) : nullptr;
         r.scnt = pl.scap ? (unsigned *)(w + pl.off_scnt) : nullptr;
         r.scap = pl.scap;
         spilled = r.spill != nullptr;
-        e = launch_rscreen(r, pl.grid, st);
+        e = launch_rscreen(r, pl.rl, pl.grid, st);
     } else {
         e = idx->metric == LIRA_METRIC_L2 ? launch_screen_rl<LIRA_METRIC_L2>(a, pl, st)
                                           : launch_screen_rl<LIRA_METRIC_IP>(a, pl, st);
@@ -2679,7 +2710,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     m.Q = q;
     m.Xr = idx->Xr;
     m.rmax = centred ? idx->rmaxc : idx->rmax;
-    m.centred = centred;
+    m.centred = centred && !idx->ipc;  // (centred IP lists always carry their pE)
     m.pqn = pqn;
     m.qbound = qbound;
     m.D = out_D;

@@ -21,8 +21,6 @@ nvidia-smi, utils.py:90-96); this module is new.
 """
 from __future__ import annotations
 
-import ctypes
-
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -114,14 +112,25 @@ def merge_shards(D_parts: torch.Tensor, I_parts: torch.Tensor, metric: str = "L2
     (lira_merge_shards): the k smallest keys of the union in the scan's order."""
     from . import _lib
     from .index import METRICS, normalize_metric
+    if D_parts.dim() != 3 or I_parts.dim() != 3:
+        raise ValueError("D_parts and I_parts must be (P, nq, k)")
     P, nq, k = D_parts.shape
     if I_parts.shape != D_parts.shape:
         raise ValueError("D_parts and I_parts must have the same (P, nq, k) shape")
+    if D_parts.dtype != torch.float32 or I_parts.dtype != torch.int64:
+        raise ValueError(f"D_parts must be float32 and I_parts int64 (got {D_parts.dtype}, {I_parts.dtype})")
+    if D_parts.device != I_parts.device or D_parts.device.type != "cuda":
+        raise ValueError("D_parts and I_parts must be on the same GPU")
     D_parts = D_parts.contiguous()
     I_parts = I_parts.contiguous()
     if out is None:
         out = (torch.empty((nq, k), dtype=torch.float32, device=D_parts.device),
                torch.empty((nq, k), dtype=torch.int64, device=D_parts.device))
+    else:
+        Do, Io = out
+        for t, dt, name in ((Do, torch.float32, "out[0]"), (Io, torch.int64, "out[1]")):
+            if tuple(t.shape) != (nq, k) or t.dtype != dt or t.device != D_parts.device or not t.is_contiguous():
+                raise ValueError(f"{name} must be a contiguous ({nq}, {k}) {dt} tensor on {D_parts.device}")
     with torch.cuda.device(D_parts.device):
         _lib.call("lira_merge_shards", _lib.ptr(D_parts), _lib.ptr(I_parts), P, nq, k,
                   METRICS[normalize_metric(metric)], int(bool(dedup)), _lib.ptr(out[0]), _lib.ptr(out[1]),

@@ -238,8 +238,8 @@ class PartitionedIndex:
     def describe(self, nq: int, nprobe: int, k: int, dedup: bool = True, exact: bool = False) -> str:
         """The scan kernel a search of this shape runs (lira_scan_describe)."""
         flags = (_lib.LIRA_SCAN_DEDUP if dedup else 0) | (_lib.LIRA_SCAN_EXACT if exact else 0)
-        buf = ctypes.create_string_buffer(256)
-        _lib.call("lira_scan_describe", self._h, int(nq), int(nprobe), int(k), flags, buf, 256)
+        buf = ctypes.create_string_buffer(512)
+        _lib.call("lira_scan_describe", self._h, int(nq), int(nprobe), int(k), flags, buf, 512)
         return buf.value.decode()
 
     def check(self, stream=None):
@@ -269,13 +269,22 @@ class PartitionedIndex:
         candidate blocks entered, dropped by the L2 early abandon, skipped by
         the triangle-inequality test (include/lira_hip.h)."""
         v = (ctypes.c_uint64 * 8)()
+        paths = ctypes.c_int()
         with torch.cuda.device(self.device):
+            _lib.call("lira_index_stats_paths", self._h, ctypes.byref(paths))
             _lib.call("lira_index_stats_read", self._h, v)
-        # ([1] / [3] mean chunks_nominal / blocks_dropped on the all-exact scan and the
-        # plan filter's removed pairs / their (query, candidate) pairs on the screened one)
-        return {"chunks_computed": v[0], "chunks_nominal": v[1], "blocks": v[2], "blocks_dropped": v[3],
-                "blocks_skipped": v[4], "rechecked": v[5], "rescans": v[6], "survivors": v[7],
-                "pairs_pruned_plan": v[1], "candidates_pruned_plan": v[3]}
+        out = {"chunks_computed": v[0], "blocks": v[2], "blocks_skipped": v[4], "rechecked": v[5],
+               "rescans": v[6], "survivors": v[7],
+               "paths": {1: "exact", 2: "screen", 3: "exact+screen"}.get(paths.value, "none")}
+        # slots [1] / [3]: chunks_nominal / blocks_dropped on the all-exact scan, the plan
+        # filter's removed pairs / their (query, candidate) pairs on the screened one
+        if paths.value == 1:
+            out.update(chunks_nominal=v[1], blocks_dropped=v[3])
+        elif paths.value == 2:
+            out.update(pairs_pruned_plan=v[1], candidates_pruned_plan=v[3])
+        else:  # (both paths, or none: the two meanings are summed)
+            out.update(slot1=v[1], slot3=v[3])
+        return out
 
     def set_option(self, name: str, value) -> None:
         """Set one LIRA_OPT_* knob by name (see include/lira_hip.h)."""

@@ -11,6 +11,10 @@ Two distributions, both fp32:
   nprobe (nearest centroids) lands near the metric's 0.95 operating point
   (measured: SIFT1M m=12 -> 0.97, GIST1M m=16 -> 0.96, DEEP10M m=20 -> 0.985),
   as it does on the real datasets.  deep10m rows are L2-normalised (DEEP1B is).
+* ``uniform``: x ~ U[0, 1)^d i.i.d. (north_star's literal "synthetic random-float
+  vectors"), k-means partitions like ``latent``.  No cluster structure: recall@k at
+  nprobe << B is low against global ground truth (hard part 7), so
+  it is a throughput and parity workload -- both sides scan identical probe lists.
 * ``mixture``: B centres ~ N(0,1)^d, point = centre[uniform label] +
   sigma * N(0,1)^d (sigma = 0.35), nearest-centre partitions.  In high d these
   clusters are perfectly separated (recall 1.0 at any nprobe >= 1), so exact
@@ -62,6 +66,17 @@ def mixture_torch(n, d, n_centres, seed, device, sigma=0.35, centres=None, chunk
     return x, centres
 
 
+def uniform_torch(n, d, seed, device, chunk=1 << 20):
+    """n rows of U[0, 1)^d (torch Philox on ``device``), in chunks."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    x = torch.empty((n, d), device=device, dtype=torch.float32)
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        x[s:e] = torch.rand((e - s, d), generator=g, device=device)
+    return x
+
+
 def nearest_centre(x: torch.Tensor, centres: torch.Tensor, chunk=1 << 18) -> torch.Tensor:
     """argmin_c ||x - c||^2 per row (offline assignment; int32)."""
     cn = (centres * centres).sum(1)
@@ -110,8 +125,8 @@ def workload(config: str, seed: int, device, data: str = "latent", n_override=No
     """(x, centroids, assignment, make_queries(nq, seed)) for a config.
 
     assignment: (N,) int32, or (N, n_mul) for the configs of N_MUL.
-    ``latent``: k-means centroids (lira_amd.knn.Kmeans, subsample of 256 points
-    per centroid as faiss) and exact nearest-centroid assignment.
+    ``latent`` / ``uniform``: k-means centroids (lira_amd.knn.Kmeans, subsample of
+    256 points per centroid as faiss) and exact nearest-centroid assignment.
     ``mixture``: generating centres and nearest-centre assignment."""
     N, d, B, _, _, _, _ = CONFIGS[config]
     N = n_override or N
@@ -120,16 +135,21 @@ def workload(config: str, seed: int, device, data: str = "latent", n_override=No
         x, c = mixture_torch(N, d, B, seed, device)
         assign = nearest_centre(x, c) if n_mul == 1 else nearest_m(x, c, n_mul)
         return x, c, assign, lambda nq, s: mixture_torch(nq, d, B, s, device, centres=c)[0]
-    if data != "latent":
+    if data not in ("latent", "uniform"):
         raise ValueError(f"unknown synthetic distribution {data!r}")
     from .knn import Kmeans
-    basis = latent_basis(d, LATENT_DIM[config], seed, device)
-    norm = config in NORMALISED
-    x = latent_torch(N, basis, seed + 1, device, normalise=norm)
+    if data == "uniform":
+        x = uniform_torch(N, d, seed + 1, device)
+        make_q = lambda nq, s: uniform_torch(nq, d, s, device)  # noqa: E731
+    else:
+        basis = latent_basis(d, LATENT_DIM[config], seed, device)
+        norm = config in NORMALISED
+        x = latent_torch(N, basis, seed + 1, device, normalise=norm)
+        make_q = lambda nq, s: latent_torch(nq, basis, s, device, normalise=norm)  # noqa: E731
     km = Kmeans(d, B, niter=kmeans_iter, seed=seed, device=device.index)
     km.train(x)
     c = torch.from_numpy(km.centroids).to(device)
     assign = nearest_m(x, c, n_mul)
     if n_mul == 1:
         assign = assign[:, 0]
-    return x, c, assign, lambda nq, s: latent_torch(nq, basis, s, device, normalise=norm)
+    return x, c, assign, make_q

@@ -406,8 +406,8 @@ def test_options_do_not_change_results(metric):
     for name, vals in (("qr", (128,)), ("two_phase", (0, 2)), ("seed", (0,)), ("share", (0,)),
                        ("prune", (0,)), ("split", (0,)), ("mfma", (0, 2)), ("rounds", (1, 64)),
                        ("near_rounds", (2, 8)), ("screen", (0,)), ("probes_hint", (1, 4)), ("xhi", (0, 1, 2)),
-                       ("rscreen", (0,)), ("rescan", (0, 1)), ("spill", (0, 1, 4)),
-                       ("seed_tiles", (1, 2, 4))):
+                       ("rscreen", (0,)), ("rescan", (0, 1)), ("spill", (0, 1, 4)), ("near_first", (0, 1, 4)),
+                       ("seed_tiles", (1, 2, 4) if metric == "L2" else (1, 2))):
         old = idx.get_option(name)
         for v in vals:
             idx.set_option(name, v)
@@ -424,8 +424,18 @@ def test_options_do_not_change_results(metric):
         D3, I3, _ = run(idx, q, probe, k)
         idx.set_option("qr", 0)
         assert np.array_equal(I3, I1) and np.array_equal(bits(D3), bits(D1)), ("qr32", k)
+    # IP: the uncentred split copy (LIRA_OPT_IP_CENTRE = 0, round 4's layout, k_screen_m)
+    if metric == "inner_product":
+        idu = make_index(x, d2b, 8, metric, ip_centre=0)
+        for k in (10, 100):
+            D0, I0, _ = run(idu, q, probe, k)
+            D1, I1, _ = run(idx, q, probe, k)
+            assert np.array_equal(I0, I1) and np.array_equal(bits(D0), bits(D1)), ("ip_centre", k)
     # the removed screen variants (k_screen_s / _w / _v, k_seed_b): 0 still reads back, others refused
     from lira_amd import LiraError
+    if metric == "inner_product":  # (4 seed tiles exist only in the fused L2 seed)
+        with pytest.raises(LiraError, match="EUNSUPPORTED"):
+            idx.set_option("seed_tiles", 4)
     for name, bad in (("pipeline", 1), ("ring", 3), ("wide", 1), ("seed", 2)):
         with pytest.raises(LiraError, match="EUNSUPPORTED"):
             idx.set_option(name, bad)
@@ -537,3 +547,116 @@ def test_graph_replay_after_eager_calls():
             torch.cuda.synchronize()
             assert torch.equal(I, I0) and torch.equal(D.view(torch.int32), D0.view(torch.int32)), (keep, prof)
         del g
+
+
+def unit_case(seed, n, d, b, nq, nprobe, sigma=0.5):
+    # L2-normalised rows around b random directions (DEEP1B-like: search.cpp's IP on unit vectors)
+    rng = np.random.default_rng(seed)
+    c = rng.standard_normal((b, d), dtype=np.float32)
+    c /= np.linalg.norm(c, axis=1, keepdims=True)
+    lab = rng.integers(0, b, n)
+    x = c[lab] + sigma / np.sqrt(d) * rng.standard_normal((n, d), dtype=np.float32)
+    x = (x / np.linalg.norm(x, axis=1, keepdims=True)).astype(np.float32)
+    q = c[rng.integers(0, b, nq)] + sigma / np.sqrt(d) * rng.standard_normal((nq, d), dtype=np.float32)
+    q = (q / np.linalg.norm(q, axis=1, keepdims=True)).astype(np.float32)
+    d2b = oracle.centroid_dist(x, c).argmin(1).astype(np.int32)[:, None]
+    probe = oracle.probe_nearest(oracle.centroid_dist(q, c), nprobe)
+    return x, q, d2b, probe
+
+
+@pytest.mark.parametrize("k", [10, 40, 100])
+@pytest.mark.parametrize("data", ["clustered", "unit"])
+def test_rscreen_ip_centred(k, data):
+    # k_screen_r on a centred IP index (q.x = q.fl(x - c) + q.c, Cauchy-Schwarz block
+    # skip and plan filter; 32-, 64- and 128-key row lists): bit-exact against the
+    # oracle, the uncentred index (LIRA_OPT_IP_CENTRE = 0: k_screen_m) and the options
+    n, d, b, nq, nprobe = 40000, 96, 16, 700, 5
+    if data == "clustered":
+        x, q, d2b, probe = clustered_case(800 + k, n, d, b, nq, nprobe)
+    else:
+        x, q, d2b, probe = unit_case(900 + k, n, d, b, nq, nprobe)
+    idx = make_index(x, d2b, b, "inner_product")
+    assert idx.describe(nq, nprobe, k).startswith("k_screen_r"), idx.describe(nq, nprobe, k)
+    off, ids = oracle.build_csr(d2b, b)
+    vecs = oracle.gather_lists(x, off, ids)
+    for dedup in (True, False):
+        Do, Io, nco = oracle.scan_topk(q, off, ids, vecs, probe, k, oracle.IP, idx.max_replicas if dedup else 0)
+        D, I, nc = run(idx, q, probe, k, dedup=dedup)
+        assert np.array_equal(I, Io) and np.array_equal(bits(D), bits(Do)), dedup
+        assert np.array_equal(nc, nco)
+    idx.set_stats(True)
+    run(idx, q, probe, k)
+    st = idx.stats_read()
+    idx.set_stats(False)
+    assert st["survivors"] > 0
+    if data == "clustered":  # far clusters: whole lists or tiles dropped by Cauchy-Schwarz
+        assert st["blocks_skipped"] + st["pairs_pruned_plan"] > 0, st
+    ref = run(idx, q, probe, k)
+    for name, v in (("spill", 0), ("spill", 1), ("near_first", 0), ("rescan", 1), ("prune", 0), ("rounds", 64)):
+        old = idx.get_option(name)
+        idx.set_option(name, v)
+        D, I, _ = run(idx, q, probe, k)
+        idx.set_option(name, old)
+        assert np.array_equal(I, ref[1]) and np.array_equal(bits(D), bits(ref[0])), (name, v)
+    idu = make_index(x, d2b, b, "inner_product", ip_centre=0)
+    assert not idu.describe(nq, nprobe, k).startswith("k_screen_r")
+    D, I, _ = run(idu, q, probe, k)
+    assert np.array_equal(I, ref[1]) and np.array_equal(bits(D), bits(ref[0])), "uncentred"
+    # per-partition lists on the centred index run the fp32-tile screen
+    Dp, Ip, _ = run(idx, q, probe, k, per_partition=True, dedup=False)
+    Dq, Iq = oracle.scan_per_partition(q, off, ids, vecs, probe, k, oracle.IP)
+    assert np.array_equal(Ip, Iq) and np.array_equal(bits(Dp), bits(Dq))
+
+
+@pytest.mark.parametrize("k", [25, 64, 100])
+def test_rscreen_l2_long_lists(k):
+    # L2 at k > 24: k_screen_r with 32 query rows per item and 64 / 128-key row lists
+    x, q, d2b, probe = clustered_case(1000 + k, 40000, 64, 16, 700, 5, spread=0.6)
+    idx = make_index(x, d2b, 16, "L2")
+    assert idx.describe(700, 5, k).startswith("k_screen_r")
+    off, ids = oracle.build_csr(d2b, 16)
+    Do, Io, nco = oracle.scan_topk(q, off, ids, oracle.gather_lists(x, off, ids), probe, k, oracle.L2,
+                                   idx.max_replicas)
+    D, I, nc = run(idx, q, probe, k)
+    assert np.array_equal(I, Io) and np.array_equal(bits(D), bits(Do))
+    idx.set_option("rscreen", 0)
+    D2, I2, _ = run(idx, q, probe, k)
+    assert np.array_equal(I2, Io) and np.array_equal(bits(D2), bits(Do))
+
+
+def test_graph_capture_workspace_growth():
+    # the handle's cached workspace (lira_hip.h lira_scan_topk): growing it while the
+    # stream is captured is refused (EINVAL); an eager call that outgrows a buffer a
+    # captured graph uses leaves that buffer allocated, so the replay stays valid
+    import torch
+    from lira_amd import LiraError
+    dev = torch.device("cuda", 0)
+    x, q, d2b, probe = random_case(93, 20000, 32, 16, 3000, 4, "L2")
+    qt, pt = torch.from_numpy(q).to(dev), torch.from_numpy(probe).to(dev)
+    idx = make_index(x, d2b, 16, "L2")
+    D = torch.empty((200, 10), dtype=torch.float32, device=dev)
+    I = torch.empty((200, 10), dtype=torch.int64, device=dev)
+    nc = torch.empty(200, dtype=torch.int64, device=dev)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        idx.search(qt[:200], pt[:200], 10, out=(D, I, nc))  # sizes the cached workspace
+        torch.cuda.synchronize()
+        I0, D0 = I.clone(), D.clone()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            idx.search(qt[:200], pt[:200], 10, out=(D, I, nc))
+        run(idx, q, probe, 10)  # 3000 queries: a larger workspace (the captured one retired)
+        I.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+    assert torch.equal(I, I0) and torch.equal(D.view(torch.int32), D0.view(torch.int32))
+    del g
+    # a fresh handle: its first call would allocate under capture
+    idx2 = make_index(x, d2b, 16, "L2")
+    g2 = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with pytest.raises(LiraError, match="EINVAL"):
+            with torch.cuda.graph(g2, stream=s):
+                idx2.search(qt[:200], pt[:200], 10, out=(D, I, nc))
+    torch.cuda.synchronize()
+    del g2
