@@ -155,12 +155,14 @@ __device__ __forceinline__ float lim_of(float T, float invF) {
 }
 
 // key e (runtime, < 32 RL) of a half-wave list, broadcast to the lane's half
+// (masks, not a select chain: hipcc turned the chain into a scratch array indexed
+// by e >> 5)
 template <int RL>
 __device__ __forceinline__ u64 list_at(const u64 (&lst)[RL], int e) {
-    u64 x = lst[0];
+    const int r = __builtin_amdgcn_readfirstlane(e >> 5);
+    u64 x = 0;
 #pragma unroll
-    for (int r = 1; r < RL; ++r)
-        if ((e >> 5) == r) x = lst[r];
+    for (int i = 0; i < RL; ++i) x |= lst[i] & (0ull - (u64)(r == i));
     return shfl64(x, (lane_id() & 32) + (e & 31));
 }
 
