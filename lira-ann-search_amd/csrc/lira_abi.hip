@@ -795,6 +795,7 @@ int lira_index_set_option(lira_index *idx, int option, int64_t value) {
         case LIRA_OPT_RESCAN: if (!in(-1, 1)) break; o.rescan = v; return LIRA_OK;
         case LIRA_OPT_SPILL: if (!in(-1, 1 << 16)) break; o.spill = v; return LIRA_OK;
         case LIRA_OPT_IP_CENTRE: if (!in(0, 1)) break; o.ip_centre = v; return LIRA_OK;
+        case LIRA_OPT_CHUNK: if (!in(0, 1 << 20)) break; o.chunk = v; return LIRA_OK;
         case LIRA_OPT_SEED_TILES:
             if (!in(0, 4) || v == 3) break;
             // 4 tiles exist only in the seed fused with the per-pair records (L2, d <= 256,
@@ -836,6 +837,7 @@ int lira_index_get_option(const lira_index *idx, int option, int64_t *value) {
         case LIRA_OPT_SPILL: *value = o.spill; break;
         case LIRA_OPT_SEED_TILES: *value = o.seed_tiles; break;
         case LIRA_OPT_IP_CENTRE: *value = o.ip_centre; break;
+        case LIRA_OPT_CHUNK: *value = o.chunk; break;
         default: return fail(LIRA_EINVAL, "unknown option " + std::to_string(option));
     }
     return LIRA_OK;

@@ -56,6 +56,7 @@ struct lira_opts {
     int rescan = -1;      // LIRA_OPT_RESCAN (-1: auto)
     int spill = -1;       // LIRA_OPT_SPILL (-1: 256 records per query)
     int seed_tiles = 0;   // LIRA_OPT_SEED_TILES (0: auto)
+    int chunk = 0;        // LIRA_OPT_CHUNK (0: auto)
     int ip_centre = 1;    // LIRA_OPT_IP_CENTRE (build time): IP lists centred on their pivots like L2's
 };
 

@@ -51,35 +51,37 @@ namespace lira {
 typedef __bf16 rbf16x8 __attribute__((ext_vector_type(8)));
 typedef float rf4 __attribute__((ext_vector_type(4)));
 
-static constexpr int kRW = 4;           // waves per workgroup
-static constexpr int kRBC = 16;         // survivor buffer keys per (wave, row)
 static constexpr int kRMaxTiles = 512;  // tiles per item (the plan caps a chunk at 128 blocks)
 static constexpr int kROCap = 128;      // survivor queue entries per wave (>= two candidate masks)
 
-template <int RL>
+// W waves per workgroup (an item): 4 (two workgroups per CU) or 8 (one, with QR = 64
+// rows at RL 4: the 128-key lists of 64 rows and 8 waves' buffers in one CU's LDS)
+template <int RL, int W>
 struct RSmem {
-    static constexpr int QR = RL == 1 ? 64 : 32;                   // query rows per item
+    static constexpr int QR = RL == 1 || W == 8 ? 64 : 32;         // query rows per item
     static constexpr int K2 = 32 * RL;                             // row list keys
     static constexpr int NRG = QR / 16;                            // MFMA row groups
+    static constexpr int BC = W == 8 ? 8 : 16;                     // survivor buffer keys per (wave, row)
     static constexpr int aq = 0;                                   // [4 chunks][NRG][64 lanes] 16 B: A operands
     static constexpr int lists = aq + 4 * NRG * 64 * 16;           // [QR][K2] u64
-    static constexpr int bufs = lists + QR * K2 * 8;               // [4][QR][16] u64
-    static constexpr int bufc = bufs + kRW * QR * kRBC * 8;        // [4][64] int (lane = row)
-    static constexpr int hs = bufc + kRW * 64 * 4;                 // [4][64] float: the wave's thresholds
-    static constexpr int tst = hs + kRW * 64 * 4;                  // [512] float2: tile radius ranges
+    static constexpr int bufs = lists + QR * K2 * 8;               // [W][QR][BC] u64
+    static constexpr int bufc = bufs + W * QR * BC * 8;            // [W][64] int (lane = row)
+    static constexpr int hs = bufc + W * 64 * 4;                   // [W][64] float: the wave's thresholds
+    static constexpr int tst = hs + W * 64 * 4;                    // [512] float2: tile radius ranges
     static constexpr int trs = tst + kRMaxTiles * 8;               // [512] float: tile hi residuals
     static constexpr int pair = trs + kRMaxTiles * 4;              // [64] int
     static constexpr int qn = pair + 64 * 4;                       // [64] float4: qn (IP qc), ||q'|| (up), qres, dq (IP qc)
     static constexpr int erun = qn + 64 * 16;                      // [64] float bits: running error bound
     static constexpr int lock = erun + 64 * 4;                     // [64] int
     static constexpr int opub = lock + 64 * 4;                     // [64] uint: bound last published
-    static constexpr int oqk = opub + 64 * 4;                      // [4][kROCap] u64: survivor queue keys
-    static constexpr int kth = oqk + kRW * kROCap * 8;             // [64] u64: each list's k-th key
+    static constexpr int oqk = opub + 64 * 4;                      // [W][kROCap] u64: survivor queue keys
+    static constexpr int kth = oqk + W * kROCap * 8;               // [64] u64: each list's k-th key
     static constexpr int meta = kth + 64 * 8;                      // [16] int
     static constexpr int total = meta + 64;
 };
-static_assert(RSmem<1>::total <= 80 * 1024 && RSmem<2>::total <= 80 * 1024 && RSmem<4>::total <= 80 * 1024,
-              "k_screen_r: two workgroups per CU");
+static_assert(RSmem<1, 4>::total <= 80 * 1024 && RSmem<2, 4>::total <= 80 * 1024 && RSmem<4, 4>::total <= 80 * 1024,
+              "k_screen_r: two 4-wave workgroups per CU");
+static_assert(RSmem<4, 8>::total <= 160 * 1024, "k_screen_r: one 8-wave workgroup per CU");
 static_assert(kROCap >= 128, "a drained queue takes two full candidate masks");
 
 // a value the compiler must treat as produced here (keeps per-lane address
@@ -211,7 +213,7 @@ __device__ __forceinline__ void spill_evicted(const RArgs &a, u64 ev, bool hv, u
 // row's LDS lock: raise the row's running error bound to the wave's first
 // (readers take the list's k-th key, then the bound: program order in both),
 // half-wave merge, publish the query's bound if the list's k-th improved.
-template <int M, int RL>
+template <int M, int RL, int BC>
 __device__ __forceinline__ void flush_row(u64 *lists, u64 *kth_s, const u64 *mybuf, int *lock_s, uint32_t *erun_s,
                                           uint32_t *opub_s, const int *pair_s, int row, int n, int ew_bits, int k,
                                           float qv_row, const RArgs &a, float Tc_row) {
@@ -225,7 +227,7 @@ __device__ __forceinline__ void flush_row(u64 *lists, u64 *kth_s, const u64 *myb
     u64 lst[RL];
 #pragma unroll
     for (int r = 0; r < RL; ++r) lst[r] = lists[row * K2 + r * 32 + hl];
-    const u64 b = hl < n ? wkey_to_key<M>(mybuf[row * kRBC + hl], qv_row) : kEmptyKey;
+    const u64 b = hl < n ? wkey_to_key<M>(mybuf[row * BC + hl], qv_row) : kEmptyKey;
     u64 ev = kEmptyKey;
     if (a.spill)
         ev = merge_evict<RL>(lst, b);
@@ -259,18 +261,18 @@ __device__ __forceinline__ void flush_row(u64 *lists, u64 *kth_s, const u64 *myb
 // Merge this wave's full row buffers into the lists, then move the survivor
 // queue into the buffers (LDS atomic slots), merging every buffer that fills,
 // until the queue is empty.
-template <int M, int RL>
+template <int M, int RL, int BC>
 __device__ __forceinline__ void drain_buffers(u64 *lists, u64 *kth_s, u64 *mybuf, int *mybufc, int *lock_s,
                                               uint32_t *erun_s, uint32_t *opub_s, const int *pair_s,
                                               const float4 *rec_s, const u64 *oq_key, uint32_t pos_base, int nq,
                                               float Ew, int k, const RArgs &a, float Tc) {
     const int lane = opaque(lane_id());
     auto flush_full = [&]() {
-        u64 full = __ballot(mybufc[lane] >= kRBC);  // lane = row
+        u64 full = __ballot(mybufc[lane] >= BC);  // lane = row
         while (full) {
             const int row = __builtin_ctzll(full);
             full &= full - 1;
-            flush_row<M, RL>(lists, kth_s, mybuf, lock_s, erun_s, opub_s, pair_s, row, kRBC,
+            flush_row<M, RL, BC>(lists, kth_s, mybuf, lock_s, erun_s, opub_s, pair_s, row, BC,
                              __builtin_amdgcn_readlane(__float_as_int(Ew), row), k, rec_s[row].x, a,
                              __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Tc), row)));
             if (lane == 0) mybufc[row] = 0;
@@ -289,24 +291,24 @@ __device__ __forceinline__ void drain_buffers(u64 *lists, u64 *kth_s, u64 *mybuf
         while (__any(pend)) {
             if (pend) {
                 const int slot = atomicAdd(mybufc + row, 1);
-                if (slot < kRBC) {
-                    mybuf[row * kRBC + slot] = key;
+                if (slot < BC) {
+                    mybuf[row * BC + slot] = key;
                     pend = false;
                 }
             }
             __builtin_amdgcn_wave_barrier();
-            // rows the round filled (a lane that overflowed left its row's count above kRBC)
-            if (mybufc[lane] > kRBC) mybufc[lane] = kRBC;
+            // rows the round filled (a lane that overflowed left its row's count above BC)
+            if (mybufc[lane] > BC) mybufc[lane] = BC;
             __builtin_amdgcn_wave_barrier();
             flush_full();
         }
     }
 }
 
-template <int NC, int M, int RL>  // NC: 32-dim chunks (dpad = 32 NC); M: metric; RL: list registers
-__global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
-    typedef RSmem<RL> S;
-    constexpr int QR = S::QR, K2 = S::K2, NRG = S::NRG;
+template <int NC, int M, int RL, int W>  // NC: 32-dim chunks (dpad = 32 NC); M: metric; RL: list registers; W: waves
+__global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void k_screen_r(RArgs a) {
+    typedef RSmem<RL, W> S;
+    constexpr int QR = S::QR, K2 = S::K2, NRG = S::NRG, BC = S::BC, NT = 64 * W;
     constexpr int NSTEP = 8 * NRG;  // selection steps per tile: (row group, register, candidate pair)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     u64 *lists = (u64 *)(smem + S::lists);
@@ -330,7 +332,7 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
     const int g = lane >> 4, cj = lane & 15;
     const int k = a.k;
     const float dp = (float)a.dpad, dd = (float)a.d;
-    u64 *mybuf = bufs + wave * QR * kRBC;
+    u64 *mybuf = bufs + wave * QR * BC;
     int *mybufc = bufc + wave * 64;
     float *myh = hs + wave * 64;
     u64 *oq_key = (u64 *)(smem + S::oqk) + wave * kROCap;
@@ -359,7 +361,7 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
     };
     if (tid < 9) xq[tid] = a.head[10 + tid];
     __syncthreads();
-    if (wave == kRW - 1 && lane == 0) {
+    if (wave == W - 1 && lane == 0) {
         qx = xcd_id();
         claim_into_meta();
     }
@@ -385,22 +387,24 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
         const float R = a.rmax[p];
         const float Rx = M == LIRA_METRIC_IP ? a.rmaxx[p] : 0.0f;
         int u = wave;
-        // B operands: a ring of RS chunks of [candidate group]; chunk s (of the
-        // wave's chunk sequence: tile after tile) sits in slot s mod RS, and its
-        // slot is reloaded with chunk s + RS as soon as its MFMAs have issued
-        // (RS = NC: the next tile's chunk; RS = 2 at d = 128: two chunks ahead,
-        // 32 VGPRs instead of 64).  The wave's first tile is requested before the
+        // B operands: a ring of NC chunks of [candidate group] -- the whole next
+        // tile: chunk c's slot is reloaded with the next tile's chunk c as soon as its
+        // MFMAs have issued, so a tile's loads have a whole tile (MFMAs + selection)
+        // to land (two chunks ahead, round 4's ring at d = 128, left chunks 2-3 of
+        // every tile waiting on HBM).  The wave's first tile is requested before the
         // prologue (under its loads and barriers), and again only if skipped.
-        constexpr int RS = NC % 2 == 0 && NC >= 4 ? 2 : NC;
+        constexpr int RS = NC;
         rbf16x8 B[RS][4];
         rf4 xa_n = (rf4)(0.0f);  // the next tile's xadj (candidates 4 cj .. + 3)
+        // (xadj first, then B: the loop's first use is xa, so on every path into
+        // the tile loop the compiler's wait for it leaves the B loads in flight)
         auto load_first = [&]() {
             const char *base = a.Xb + (int64_t)(tbase + u) * tile_bytes + lane_off;
+            xa_n = *(const rf4 *)(a.xadj + (int64_t)(tbase + u) * 64 + 4 * cj);
 #pragma unroll
             for (int c = 0; c < RS; ++c)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) B[c][i] = *(const rbf16x8 *)(base + c * 8192 + i * 256);
-            xa_n = *(const rf4 *)(a.xadj + (int64_t)(tbase + u) * 64 + 4 * cj);
         };
         if (u < nt) load_first();
 
@@ -431,11 +435,11 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
         {
             uint4 *l4 = (uint4 *)lists;
             const uint4 e4 = make_uint4(~0u, ~0u, ~0u, ~0u);
-            for (int i = tid; i < QR * K2 / 2; i += 256) l4[i] = e4;
+            for (int i = tid; i < QR * K2 / 2; i += NT) l4[i] = e4;
         }
         if (TRI) {
             float rb = 0.0f, hr = 0.0f;
-            for (int i = tid; i < nt; i += 256) {
+            for (int i = tid; i < nt; i += NT) {
                 const float2 t2 = a.tstat[tbase + i];
                 tst[i] = t2;
                 rb = fmaxf(rb, t2.y);
@@ -452,7 +456,7 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
 
         // A operands into LDS, in fragment order: [chunk c][row group rg][lane (g, j)]
         // = row 16 rg + j, dims 32 c + 8 g .. + 7 (each wave reads 1 KiB per (c, rg))
-        for (int e = tid; e < NC * NRG * 64; e += 256) {
+        for (int e = tid; e < NC * NRG * 64; e += NT) {
             const int l = e & 63, rg = (e >> 6) % NRG, c = e / (64 * NRG);
             const int pr = pair_s[16 * rg + (l & 15)];
             uint4 v = make_uint4(0u, 0u, 0u, 0u);
@@ -479,14 +483,17 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
         const int g4 = opaque(4 * g);  // (selection rows: 16 rg + g4 + reg)
         // T: the row's bound on its final k-th exact score (shared list, published bound).
         // No divergent branch (the published bound's load stays countable for the
-        // compiler's waits: a conditional one cost a vmcnt(0) per tile)
-        auto update_T = [&]() {
+        // compiler's waits: a conditional one cost a vmcnt(0) per tile).  The next
+        // published bound is requested only inside the tile loop (refresh), ahead of
+        // the tile's other loads: on every path into the loop the outstanding loads
+        // are then the pub load followed by the tile's, and its wait leaves them in flight
+        auto update_T = [&](bool refresh) {
             const u64 kk = kth_s[lane];
             asm volatile("" ::: "memory");  // (the list's key first, then its bound: see flush_row)
             const float er = __uint_as_float(erun_s[lane]);
             float T = bound_of(kk, er, a.gP);
             T = fminf(T, ord2f(pub));  // (~0u, nothing published: a NaN, which fminf ignores)
-            pub = __hip_atomic_load(pub_at, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (refresh) pub = __hip_atomic_load(pub_at, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (__any(T != Tc)) {  // (recomputed for every lane: an unchanged T gives the same values)
                 Tc = T;
                 const bool fin = T < 3e38f;
@@ -530,18 +537,18 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
             return __all(r.y < triA || r.x > triB) != 0;
         };
 
-        update_T();
+        update_T(false);
         if (u < nt && skip(u)) {
             do {
                 ++n_skip;
-                u += kRW;
+                u += W;
             } while (u < nt && skip(u));
             if (u < nt) load_first();
         }
         int ovf = 0;  // survivor queue fill (wave-uniform)
         // survivor queue -> this wave's row buffers (full ones merged into the lists)
         auto drain = [&]() {
-            drain_buffers<M, RL>(lists, kth_s, mybuf, mybufc, lock_s, erun_s, opub_s, pair_s, rec_s, oq_key,
+            drain_buffers<M, RL, BC>(lists, kth_s, mybuf, mybufc, lock_s, erun_s, opub_s, pair_s, rec_s, oq_key,
                                  (uint32_t)tbase * 64u, ovf, Ew, k, a, Tc);
             ovf = 0;
         };
@@ -549,13 +556,13 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
         while (u < nt) {
             const rf4 xa = xa_n;
             // ---- the row bounds (thresholds rewritten where one changed)
-            update_T();
+            update_T(true);
 
             // ---- the next tile of this wave (skip test with the current intervals)
-            int un = u + kRW;
+            int un = u + W;
             while (un < nt && skip(un)) {
                 ++n_skip;
-                un += kRW;
+                un += W;
             }
             const int ul = un < nt ? un : u;  // (the last tile's loads repeat the current tile)
             const char *cbase = a.Xb + (int64_t)(tbase + u) * tile_bytes + lane_off;
@@ -655,28 +662,29 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
             u = un;
         }
         if (ovf) drain();
-        if (wave == kRW - 1 && lane == 0) claim_into_meta();  // (the next item; read after the barriers below)
+        if (wave == W - 1 && lane == 0) claim_into_meta();  // (the next item; read after the barriers below)
 
         // ---- item epilogue: every wave's buffers into the lists (rows split over
         // the waves, two per pass: one per half-wave), then the lists out
         if (mybufc[lane] > 0) atomicMax(erun_s + lane, __float_as_uint(Ew));
         __syncthreads();
         const int ln = opaque(lane);  // (lane-derived addresses computed here, not hoisted)
-        constexpr int RPW = QR / kRW;  // rows per wave
+        constexpr int RPW = QR / W;  // rows per wave
 #pragma unroll 1
         for (int j = 0; j < RPW; j += 2) {
             const int hl = ln & 31, row = wave * RPW + j + (ln >> 5);
-            const int c0 = bufc[0 * 64 + row], c1 = bufc[1 * 64 + row], c2 = bufc[2 * 64 + row], c3 = bufc[3 * 64 + row];
-            const int n = c0 + c1 + c2 + c3;
+            int n = 0;
+#pragma unroll
+            for (int w = 0; w < W; ++w) n += bufc[w * 64 + row];
             if (!__any(n > 0)) continue;
             const float qv_r = rec_s[row].x;
             for (int r0 = 0; __any(n > r0); r0 += 32) {
                 const int e = r0 + hl;
                 u64 b = kEmptyKey;
                 if (e < n) {
-                    const int w = e < c0 ? 0 : e < c0 + c1 ? 1 : e < c0 + c1 + c2 ? 2 : 3;
-                    const int off = e - (w == 0 ? 0 : w == 1 ? c0 : w == 2 ? c0 + c1 : c0 + c1 + c2);
-                    b = wkey_to_key<M>(bufs[(w * QR + row) * kRBC + off], qv_r);
+                    int w = 0, off = e;  // (the wave buffer holding key e of the row's concatenation)
+                    while (off >= bufc[w * 64 + row]) off -= bufc[w++ * 64 + row];
+                    b = wkey_to_key<M>(bufs[(w * QR + row) * BC + off], qv_r);
                 }
                 u64 lst[RL];
 #pragma unroll
@@ -742,39 +750,44 @@ __global__ __launch_bounds__(256, 2) void k_screen_r(RArgs a) {
 bool rscreen_shape_ok(int64_t dpad, int64_t k) {
     return k >= 1 && k <= 120 && dpad >= 32 && dpad <= 128 && dpad % 32 == 0;
 }
-int rscreen_smem(int rl) { return rl == 1 ? RSmem<1>::total : rl == 2 ? RSmem<2>::total : RSmem<4>::total; }
+int rscreen_smem(int rl, int waves) {
+    return rl == 1 ? RSmem<1, 4>::total : rl == 2 ? RSmem<2, 4>::total : waves == 8 ? RSmem<4, 8>::total : RSmem<4, 4>::total;
+}
+int rscreen_qr(int rl, int waves) {
+    return rl == 1 ? RSmem<1, 4>::QR : rl == 2 ? RSmem<2, 4>::QR : waves == 8 ? RSmem<4, 8>::QR : RSmem<4, 4>::QR;
+}
 
-template <int NC, int M, int RL>
+template <int NC, int M, int RL, int W>
 static hipError_t launch_r(const RArgs &a, int grid, hipStream_t st) {
     static std::atomic<uint64_t> attr{0};
-    hipError_t e = set_smem_attr_once(attr, (const void *)k_screen_r<NC, M, RL>, RSmem<RL>::total);
+    hipError_t e = set_smem_attr_once(attr, (const void *)k_screen_r<NC, M, RL, W>, RSmem<RL, W>::total);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_screen_r<NC, M, RL>), dim3(grid), dim3(256), RSmem<RL>::total, st, a);
+    hipLaunchKernelGGL((k_screen_r<NC, M, RL, W>), dim3(grid), dim3(64 * W), (RSmem<RL, W>::total), st, a);
     return hipGetLastError();
 }
 
-template <int M, int RL>
+template <int M, int RL, int W>
 static hipError_t launch_rm(const RArgs &a, int grid, hipStream_t st) {
     switch (a.dpad / 32) {
-        case 1: return launch_r<1, M, RL>(a, grid, st);
-        case 2: return launch_r<2, M, RL>(a, grid, st);
-        case 3: return launch_r<3, M, RL>(a, grid, st);
-        case 4: return launch_r<4, M, RL>(a, grid, st);
+        case 1: return launch_r<1, M, RL, W>(a, grid, st);
+        case 2: return launch_r<2, M, RL, W>(a, grid, st);
+        case 3: return launch_r<3, M, RL, W>(a, grid, st);
+        case 4: return launch_r<4, M, RL, W>(a, grid, st);
         default: return hipErrorInvalidValue;
     }
 }
 
-hipError_t launch_rscreen(const RArgs &a, int rl, int grid, hipStream_t st) {
-    if (a.metric == LIRA_METRIC_L2) {
-        if (rl == 1) return launch_rm<LIRA_METRIC_L2, 1>(a, grid, st);
-        if (rl == 2) return launch_rm<LIRA_METRIC_L2, 2>(a, grid, st);
-        if (rl == 4) return launch_rm<LIRA_METRIC_L2, 4>(a, grid, st);
-    } else {
-        if (rl == 1) return launch_rm<LIRA_METRIC_IP, 1>(a, grid, st);
-        if (rl == 2) return launch_rm<LIRA_METRIC_IP, 2>(a, grid, st);
-        if (rl == 4) return launch_rm<LIRA_METRIC_IP, 4>(a, grid, st);
-    }
+template <int M>
+static hipError_t launch_rmm(const RArgs &a, int rl, int waves, int grid, hipStream_t st) {
+    if (rl == 1) return launch_rm<M, 1, 4>(a, grid, st);
+    if (rl == 2) return launch_rm<M, 2, 4>(a, grid, st);
+    if (rl == 4) return waves == 8 ? launch_rm<M, 4, 8>(a, grid, st) : launch_rm<M, 4, 4>(a, grid, st);
     return hipErrorInvalidValue;
+}
+
+hipError_t launch_rscreen(const RArgs &a, int rl, int waves, int grid, hipStream_t st) {
+    return a.metric == LIRA_METRIC_L2 ? launch_rmm<LIRA_METRIC_L2>(a, rl, waves, grid, st)
+                                      : launch_rmm<LIRA_METRIC_IP>(a, rl, waves, grid, st);
 }
 
 }  // namespace lira

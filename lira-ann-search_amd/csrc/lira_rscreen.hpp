@@ -37,7 +37,9 @@ struct RArgs {
 // k <= 120 (row lists of 32 RL keys, RL = 1 / 2 / 4 for k <= 24 / 56 / 120; 64
 // query rows per item at RL 1, else 32), dpad <= 128 (the rows' hi parts in LDS)
 bool rscreen_shape_ok(int64_t dpad, int64_t k);
-int rscreen_smem(int rl);
-hipError_t launch_rscreen(const RArgs &a, int rl, int grid, hipStream_t st);
+// (RL 4 also as one 8-wave workgroup per CU with 64 rows per item: waves = 8)
+int rscreen_smem(int rl, int waves);
+int rscreen_qr(int rl, int waves);
+hipError_t launch_rscreen(const RArgs &a, int rl, int waves, int grid, hipStream_t st);
 
 }  // namespace lira

@@ -2123,6 +2123,7 @@ struct SPlan {
     int rl = 1, qr = 64, K2 = 32, bpc = 1, bpc_near = 1, nch_max = 1, grid = 1, smem = 0, mfma = 1, split = 0;
     int bpc_near_min = 1, workers = 1;  // the plan picks group 0's chunk size in [bpc_near_min, bpc_near]
     int rs = 0;  // the wave-streaming screen k_screen_r (lira_rscreen.hip) instead of k_screen_m
+    int waves = 4;  // (k_screen_r) waves per workgroup
     int near0 = 0;  // (k_screen_r, two groups) blocks in group 0's first chunk; 0: uniform chunks
     int pp = 0;  // per-pair query records (QN / QE / QH per pair, k_pairs or k_seed_t<.., PAIRS>)
                  // instead of k_qstage's per-block copy: the hi x hi k_screen_m
@@ -2142,7 +2143,10 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // k_screen_r (lira_rscreen.hip): the hi x hi screen on the centred split copy, L2
     // or centred IP (q.x = q.fl(x - c) + q.c), k <= 120 (RL 1: 64 queries per item;
     // RL 2, 4: 32), dpad <= 128, with the per-query seed, not PER_PARTITION
-    const int rs_qr = pl.rl == 1 ? 64 : 32;
+    // (RL 4: 32 rows with 4 waves, two workgroups per CU; LIRA_OPT_QR = 64: 64 rows with
+    // 8 waves, one workgroup per CU -- half the candidate bytes per screened pair)
+    const int rs_waves = pl.rl == 4 && op.qr == 64 ? 8 : 4;
+    const int rs_qr = rscreen_qr(pl.rl, rs_waves);
     const bool rs = op.rscreen && (op.split || !idx->X) && (op.mfma || !idx->X) && op.seed && !(flags & (LIRA_SCAN_NO_SPLIT | LIRA_SCAN_PER_PARTITION)) &&
                     idx->Xb && idx->xadjc && idx->pivot && idx->lstat && rscreen_shape_ok(idx->dpad, k) && xhi == 2 &&
                     (op.qr == 0 || op.qr == rs_qr) && (idx->metric == LIRA_METRIC_L2 || idx->ipc);
@@ -2194,13 +2198,14 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // (with or without the fp32 tiles: the seed then comes from the row-major copy
     // and the per-pair records from k_pairs -- BIGANN-100M's compact index)
     pl.rs = rs;
+    pl.waves = rs ? rs_waves : 4;
     if (rs) {
         pl.mfma = 1;
         pl.split = 3;
         pl.qr = rs_qr;
         pl.pp = 1;
     }
-    pl.smem = pl.rs          ? rscreen_smem(pl.rl)
+    pl.smem = pl.rs          ? rscreen_smem(pl.rl, pl.waves)
               : !pl.mfma     ? screen_smem(pl.qr, pl.rl)
               : pl.qr == 128 ? (pl.split == 2 ? SSmem<128, 1, true, true>::total
                                 : pl.rl == 1 ? SSmem<128, 1, true>::total : SSmem<128, 2, true>::total)
@@ -2253,6 +2258,12 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     // compiler-inserted waits drain it): cap the chunk at kBR blocks
     if (pl.mfma && idx->pivot && (idx->metric == LIRA_METRIC_L2 || pl.rs)) {
         pl.bpc = std::min(pl.bpc, SSmem<64, 1, true>::kBR);
+        pl.bpc_near = std::min(pl.bpc_near, pl.bpc);
+    }
+    // LIRA_OPT_CHUNK: at most this many blocks per chunk (smaller chunks stay in an XCD's
+    // L2 while the query blocks that share them stream them)
+    if (op.chunk > 0) {
+        pl.bpc = std::min(pl.bpc, op.chunk);
         pl.bpc_near = std::min(pl.bpc_near, pl.bpc);
     }
     // k_screen_m + k_smerge with the default near_rounds: the plan picks group 0's
@@ -2351,6 +2362,7 @@ std::string screen_describe(const lira_index *idx, int64_t nq, int64_t nprobe, i
                                         : "k_screen_m fp32 v_mfma_f32_16x16x4_f32")
                             : "k_screen VALU v_pk_fma_f32";
     s += " RL=" + std::to_string(pl.rl) + " QR=" + std::to_string(pl.qr) + " K2=" + std::to_string(pl.K2) +
+         (pl.rs ? " W=" + std::to_string(pl.waves) : std::string()) +
          " grid=" + std::to_string(pl.grid) + " smem=" + std::to_string(pl.smem);
     // the plan (chunking, groups, seed, spill / re-scan): a PMC record of another plan
     // does not describe this launch's traffic (bench.py matches the whole string)
@@ -2685,7 +2697,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
         r.scnt = pl.scap ? (unsigned *)(w + pl.off_scnt) : nullptr;
         r.scap = pl.scap;
         spilled = r.spill != nullptr;
-        e = launch_rscreen(r, pl.rl, pl.grid, st);
+        e = launch_rscreen(r, pl.rl, pl.waves, pl.grid, st);
     } else {
         e = idx->metric == LIRA_METRIC_L2 ? launch_screen_rl<LIRA_METRIC_L2>(a, pl, st)
                                           : launch_screen_rl<LIRA_METRIC_IP>(a, pl, st);
