@@ -199,6 +199,9 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *                        LIRA_OPT_KEEP_TILES = 1 (the other screens read the fp32 tiles on such an
  *                        index).  0: the uncentred split copy (round-4 layout).  Results never
  *                        depend on it.
+ *   LIRA_OPT_CHUNK       screen work items: at most this many blocks of 256 candidates per chunk
+ *                        of a bucket (0, default: the plan's choice, <= 128).  Results never
+ *                        depend on it.
  */
 #define LIRA_OPT_KEEP_TILES 1
 #define LIRA_OPT_SCREEN 2
@@ -224,6 +227,7 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
 #define LIRA_OPT_SPILL 22
 #define LIRA_OPT_SEED_TILES 23
 #define LIRA_OPT_IP_CENTRE 24
+#define LIRA_OPT_CHUNK 25
 int lira_index_set_option(lira_index *idx, int option, int64_t value);
 int lira_index_get_option(const lira_index *idx, int option, int64_t *value);
 /* 1 if the index holds the fp32 tile copy (LIRA_OPT_KEEP_TILES at build time) */

@@ -760,7 +760,7 @@ template <int METRIC>
 __device__ __forceinline__ float exact_score(const float *q, const float *Xr, int64_t d, int pos) {
     const float *xp = Xr + (int64_t)pos * d;
     float acc = 0.0f;
-    if ((d & 3) == 0) {  // 16-B loads of the row, 8 in flight; the same sequential sum
+    if ((d & 3) == 0 && ((uintptr_t)q & 15) == 0) {  // 16-B loads of the row, 8 in flight; the same sequential sum
         const float4 *x4 = (const float4 *)xp;
         const float4 *q4 = (const float4 *)q;
 #pragma unroll 8

@@ -28,7 +28,7 @@ OPTIONS = {"keep_tiles": 1, "screen": 2, "split": 3, "qr": 4, "two_phase": 5, "p
            "share": 8, "rounds": 9, "near_rounds": 10, "mfma": 11, "debug": 12, "pipeline": 13, "ring": 14, "probes_hint": 15, "xhi": 16,
            "order": 17, "wide": 18, "rscreen": 19, "near_first": 20,
            "rescan": 21, "spill": 22,
-           "seed_tiles": 23, "ip_centre": 24}
+           "seed_tiles": 23, "ip_centre": 24, "chunk": 25}
 LIRA_PROBE_NEAREST = 0
 LIRA_PROBE_THRESHOLD_GE = 1
 LIRA_PROBE_THRESHOLD_GT = 2

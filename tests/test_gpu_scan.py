@@ -592,7 +592,8 @@ def test_rscreen_ip_centred(k, data):
     if data == "clustered":  # far clusters: whole lists or tiles dropped by Cauchy-Schwarz
         assert st["blocks_skipped"] + st["pairs_pruned_plan"] > 0, st
     ref = run(idx, q, probe, k)
-    for name, v in (("spill", 0), ("spill", 1), ("near_first", 0), ("rescan", 1), ("prune", 0), ("rounds", 64)):
+    for name, v in (("spill", 0), ("spill", 1), ("near_first", 0), ("rescan", 1), ("prune", 0), ("rounds", 64),
+                    ("qr", 64)):  # (qr 64 at k > 24: 8 waves per item of 64 rows)
         old = idx.get_option(name)
         idx.set_option(name, v)
         D, I, _ = run(idx, q, probe, k)
