@@ -190,8 +190,10 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *                        tiles, L2, k <= 32): 0 (default) auto -- the seed fused with the
  *                        per-pair records (d <= 256): 4 below 4096 queries, else 2; the unfused
  *                        one: 1 for d > 512 (GIST1M), else 2; 1, 2 or 4 (fused only) fixed.
- *                        Results never depend on it.  4 returns LIRA_EUNSUPPORTED where the fused
- *                        seed cannot run (IP, d > 256, or no fp32 tiles).
+ *                        On the k_screen_r path the seed is k_seed_r (the first tiles screened on
+ *                        the matrix cores, bound by the screen's error model; 4 tiles for k > 32).
+ *                        Results never depend on it.  4 returns LIRA_EUNSUPPORTED where neither
+ *                        fused seed can run (d > 256; IP uncentred or d > 128).
  *   LIRA_OPT_IP_CENTRE   (build time, IP indexes) 1 (default): like L2, store each list's rows
  *                        radius-ordered around its pivot c with the split copy of fl(x - c), so the
  *                        wave-streaming screen k_screen_r takes IP as q.x = q.fl(x - c) + q.c with a

@@ -798,10 +798,13 @@ int lira_index_set_option(lira_index *idx, int option, int64_t value) {
         case LIRA_OPT_CHUNK: if (!in(0, 1 << 20)) break; o.chunk = v; return LIRA_OK;
         case LIRA_OPT_SEED_TILES:
             if (!in(0, 4) || v == 3) break;
-            // 4 tiles exist only in the seed fused with the per-pair records (L2, d <= 256,
-            // fp32 tiles kept); the unfused seed reads 1 or 2
-            if (v == 4 && (idx->metric != LIRA_METRIC_L2 || idx->d > 256 || !o.keep_tiles))
-                return fail(LIRA_EUNSUPPORTED, "LIRA_OPT_SEED_TILES 4 needs the fused seed (L2, d <= 256, fp32 tiles)");
+            // 4 tiles exist only in the seeds fused with the per-pair records: k_seed_r
+            // (k_screen_r's: L2 or centred IP, d <= 128) and k_seed_t (L2, d <= 256, fp32
+            // tiles kept); the unfused seed reads 1 or 2
+            if (v == 4 && !(idx->d <= 128 && (idx->metric == LIRA_METRIC_L2 || (o.ip_centre && o.keep_tiles))) &&
+                !(idx->metric == LIRA_METRIC_L2 && idx->d <= 256 && o.keep_tiles))
+                return fail(LIRA_EUNSUPPORTED, "LIRA_OPT_SEED_TILES 4 needs a fused seed (L2 or centred IP with "
+                                               "d <= 128, or L2 with d <= 256 and the fp32 tiles)");
             o.seed_tiles = v;
             return LIRA_OK;
         default: return fail(LIRA_EINVAL, "unknown option " + std::to_string(option));

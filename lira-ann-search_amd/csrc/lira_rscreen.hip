@@ -393,7 +393,9 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void k_screen_r(RArgs a) {
         // to land (two chunks ahead, round 4's ring at d = 128, left chunks 2-3 of
         // every tile waiting on HBM).  The wave's first tile is requested before the
         // prologue (under its loads and barriers), and again only if skipped.
-        constexpr int RS = NC;
+        // (NC = 0: dpad > 128, the dims streamed two chunks ahead -- a whole tile is
+        // dpad / 2 bytes per lane -- and the A operands too, see SA below)
+        constexpr int RS = NC == 0 ? 2 : NC;
         rbf16x8 B[RS][4];
         rf4 xa_n = (rf4)(0.0f);  // the next tile's xadj (candidates 4 cj .. + 3)
         // (xadj first, then B: the loop's first use is xa, so on every path into
@@ -456,6 +458,7 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void k_screen_r(RArgs a) {
 
         // A operands into LDS, in fragment order: [chunk c][row group rg][lane (g, j)]
         // = row 16 rg + j, dims 32 c + 8 g .. + 7 (each wave reads 1 KiB per (c, rg))
+        // (SA: none -- they are read from the per-pair records as the tiles stream)
         for (int e = tid; e < NC * NRG * 64; e += NT) {
             const int l = e & 63, rg = (e >> 6) % NRG, c = e / (64 * NRG);
             const int pr = pair_s[16 * rg + (l & 15)];
@@ -464,6 +467,24 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void k_screen_r(RArgs a) {
             ((uint4 *)(smem + S::aq))[e] = v;
         }
         __syncthreads();
+        // SA (NC = 0, dpad > 128: GIST1M's 960 dims would need 120 KB of LDS for the
+        // rows' hi parts): each wave reads the A fragments of chunk c from QH, the rows'
+        // records (L2-resident: one item's rows are 64 x dpad x 2 bytes), in a ring two
+        // chunks ahead like the B fragments.  A padding row reads row 0's record: its
+        // products are garbage in a row that never passes.
+        constexpr bool SA = NC == 0;
+        const int nca = SA ? (int)(a.dpad >> 5) : NC;
+        uint32_t arow[NRG];  // (element offsets into QH: 32-bit, on the uniform base)
+        rbf16x8 Ar[2][NRG];
+        if (SA) {
+#pragma unroll
+            for (int rg = 0; rg < NRG; ++rg) {
+                const int pr = pair_s[16 * rg + (lane & 15)];
+                arow[rg] = (uint32_t)((pr >= 0 ? pr : pair_s[0]) * (int)a.dpad + 8 * (lane >> 4));
+#pragma unroll
+                for (int h = 0; h < 2; ++h) Ar[h][rg] = *(const rbf16x8 *)(a.QH + arow[rg] + 32 * h);
+            }
+        }
 
         // ---- per-row bound state (lane = row; qbound is always set here)
         // my_qv: L2 qn = fl(||q'||^2), IP qc = fl(q.c); my_dq: L2 fl(||q - c||)
@@ -578,6 +599,36 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void k_screen_r(RArgs a) {
             // of rows 4 g + reg, so C is the same for every row group); each B
             // fragment's slot reloaded after its NRG MFMAs
             rf4 acc[NRG][4];
+            // SA: chunk pairs (slots 0, 1), the first pair peeled (C = -xadj there)
+            auto sa_chunk = [&](int c, int h, bool first) {
+                const int cn = c + 2;
+                rbf16x8 Acur[NRG];
+#pragma unroll
+                for (int rg = 0; rg < NRG; ++rg) Acur[rg] = Ar[h][rg];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const rf4 cx = (rf4)(-xa[i]);
+#pragma unroll
+                    for (int rg = 0; rg < NRG; ++rg)
+                        acc[rg][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Acur[rg], B[h][i], first ? cx : acc[rg][i],
+                                                                             0, 0, 0);
+                    B[h][i] = cn < nca ? *(const rbf16x8 *)(cbase + (int64_t)cn * 8192 + i * 256)
+                                       : *(const rbf16x8 *)(nbase + (int64_t)(cn - nca) * 8192 + i * 256);
+                }
+                const int ca = cn < nca ? cn : cn - nca;  // (the A ring runs on into the next tile: the same rows)
+#pragma unroll
+                for (int rg = 0; rg < NRG; ++rg) Ar[h][rg] = *(const rbf16x8 *)(a.QH + arow[rg] + 32 * ca);
+                __builtin_amdgcn_sched_barrier(0);
+            };
+            if (SA) {
+                sa_chunk(0, 0, true);
+                sa_chunk(1, 1, false);
+#pragma unroll 1
+                for (int c0 = 2; c0 < nca; c0 += 2) {
+                    sa_chunk(c0, 0, false);
+                    sa_chunk(c0 + 1, 1, false);
+                }
+            }
             // per chunk: the A fragments (LDS), this chunk's MFMAs, the slot's
             // reloads; a scheduling barrier per chunk keeps the reloads where they are
             // (left alone, hipcc sank them next to their consumers)
@@ -747,8 +798,207 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void k_screen_r(RArgs a) {
     }
 }
 
+// ---- k_seed_r: the screened seed bound + per-pair records --------------------
+// One wave per query.  The query's slot-0 record first (no filter: its own list),
+// then the bound: the first NT tiles of that list screened on the matrix cores
+// exactly as k_screen_r screens them (A = the query row's hi parts in row 0 of the
+// 16 x 32 operand, the other 15 rows zero: 2 NT NC MFMAs per query, ~16x the useful
+// MACs, still far below the 2 NT x 64 x d sequential fp32 sums of k_seed_t), every
+// screened score within errE_r of search.cpp's exact one, so the k-th smallest of the
+// 64 NT keys + E bounds the query's final k-th exact score (bound_P: k distinct
+// candidates of one list).  Then the records of slots 1.. under that bound (the
+// partition filter), as k_seed_t<..., PAIRS> / k_pairs.
+template <int NC, int M, int NT>
+__global__ __launch_bounds__(256) void k_seed_r(RSeedArgs a) {
+    __shared__ float sc_s[4][NT * 64];
+    __shared__ uint16_t qh_s[4][32 * NC];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int g = lane >> 4, cj = lane & 15;
+    const int64_t q = (int64_t)blockIdx.x * 4 + w;
+    if (q >= a.nq) return;  // (no workgroup barrier below)
+    const int centred = M == LIRA_METRIC_L2 ? 1 : 2;
+    const bool samp = a.work && (q & 7) == 0;
+    const int64_t pair0 = q * a.nprobe;
+    const int p0raw = a.probe[pair0];
+    const int p0 = p0raw >= 0 && p0raw < a.n_lists ? p0raw : -1;
+    const int tile0 = p0 >= 0 ? a.tile_off[p0] : 0, ntl = p0 >= 0 ? a.tile_off[p0 + 1] - tile0 : 0;
+    // the first seed tile's B fragments and every tile's xadj, requested first (their
+    // latency overlaps the record below); tiles past the list's end repeat its first
+    const int64_t tile_bytes = a.dpad * 64 * 4;
+    const uint32_t lane_off = (uint32_t)((g >> 1) * 4096 + (g & 1) * 1024 + cj * 16);
+    rbf16x8 Bc[NC][4], Bn[NC][4];
+    rf4 xa[NT];
+    auto load_tile = [&](int t, rbf16x8 (&Bt)[NC][4]) {
+        const int tt = tile0 + (t < ntl ? t : 0);
+        const char *base = a.Xb + (int64_t)tt * tile_bytes + lane_off;
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) Bt[c][i] = *(const rbf16x8 *)(base + c * 8192 + i * 256);
+    };
+    if (ntl > 0) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) xa[t] = *(const rf4 *)(a.xadj + (int64_t)(tile0 + (t < ntl ? t : 0)) * 64 + 4 * cj);
+        load_tile(0, Bc);
+    }
+    // slot 0's record, all 64 lanes (pair_record's values: q' = fl(q - c) (L2) or q,
+    // double sums; no filter -- the seed's own list), its hi parts kept in LDS for the A operand
+    float qv = 0.0f, qnorm = 0.0f, qres = 0.0f;
+    if (p0 >= 0) {
+        const float *qr = a.Q + q * a.d, *pv = a.pivot + (int64_t)p0 * a.d;
+        double s2 = 0.0, t2 = 0.0, e2 = 0.0;
+#pragma unroll
+        for (int r = 0; r < NC / 2 + 1; ++r) {
+            const int64_t j = lane + 64 * r;
+            if (j < 32 * NC) {
+                float x = 0.0f, cv = 0.0f;
+                if (j < a.d) {
+                    x = qr[j];
+                    cv = pv[j];
+                }
+                const float sv = M == LIRA_METRIC_L2 ? x - cv : x;
+                const uint32_t h = bf16_rne_sat(sv);
+                qh_s[w][j] = (uint16_t)h;
+                a.QH[pair0 * a.dpad + j] = (uint16_t)h;
+                if (j < a.d) {
+                    s2 = __builtin_fma((double)sv, (double)sv, s2);
+                    const double rr = (double)(sv - __uint_as_float(h << 16));
+                    e2 = __builtin_fma(rr, rr, e2);
+                    if (M == LIRA_METRIC_L2) {
+                        const double df = (double)x - (double)cv;
+                        t2 = __builtin_fma(df, df, t2);
+                    } else {
+                        t2 = __builtin_fma((double)x, (double)cv, t2);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            s2 += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, s2), m));
+            t2 += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, t2), m));
+            e2 += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, e2), m));
+        }
+        const float qnu = __double2float_ru(__builtin_sqrt(s2) * (1.0 + 0x1p-40));
+        const float dq = M == LIRA_METRIC_L2 ? (float)__builtin_sqrt(t2) : (float)t2;
+        qv = M == LIRA_METRIC_L2 ? (float)s2 : dq;
+        qnorm = qnu;
+        qres = __double2float_ru(__builtin_sqrt(e2) * (1.0 + 0x1p-40));
+        if (lane == 0) {
+            a.QN[pair0] = make_float4(qv, qnu, __int_as_float((int)pair0), dq);
+            a.QE[pair0] = qres;
+            if (a.pqn) a.pqn[pair0] = qnu;
+        }
+    }
+    if (lane == 0) a.probe_live[pair0] = p0raw;
+    int est = 0;
+    if (samp && lane < 16 && p0 >= 0) est = (a.list_size[p0] + 255) / 256;  // (slot 0: its whole list, lane 0 counts)
+    if (lane != 0) est = 0;
+    float T = __builtin_inff();
+    if (ntl > 0) {  // (an empty list: no bound)
+        // the screened tiles' largest radius and hi residual (errE_r is monotone in both)
+        float rb = 0.0f, hr = 0.0f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            if (t < ntl) {
+                rb = fmaxf(rb, a.tstat[tile0 + t].y);
+                hr = fmaxf(hr, a.tres ? a.tres[tile0 + t] : 0.0f);
+            }
+        }
+        const float Rb = fminf(a.rmax[p0], rup(rb));
+        const float Rx = M == LIRA_METRIC_IP ? a.rmaxx[p0] : 0.0f;
+        const float E = errE_r<M>(qnorm, Rb, a.tres ? hr : -1.0f, qres, (float)a.dpad, qv, Rx, (float)a.d);
+        // A: row 0 = hi(q'), dims 32 c + 8 g .. + 7 in lane (g, 0), the other rows zero
+        __builtin_amdgcn_wave_barrier();
+        rbf16x8 A[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (cj == 0) v = *(const uint4 *)&qh_s[w][32 * c + 8 * g];
+            A[c] = __builtin_bit_cast(rbf16x8, v);
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            if (t + 1 < NT) load_tile(t + 1, Bn);  // (the next tile's loads under this one's MFMAs)
+            rf4 acc[4];
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[c], Bc[c][i], c == 0 ? (rf4)(-xa[t][i]) : acc[i],
+                                                                     0, 0, 0);
+            if (t + 1 < NT) {
+#pragma unroll
+                for (int c = 0; c < NC; ++c)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) Bc[c][i] = Bn[c][i];
+            }
+            // row 0 (lanes 0..15, register 0): candidate 4 cj + i of the tile
+            if (g == 0)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float wv = acc[i][0];
+                    const float sc = M == LIRA_METRIC_L2 ? qv - 2.0f * wv : -(wv + qv);
+                    sc_s[w][t * 64 + 4 * cj + i] = t < ntl && sc == sc ? sc : __builtin_inff();
+                }
+        }
+        __builtin_amdgcn_wave_barrier();
+        u64 key[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) key[t] = ((u64)f2ord(sc_s[w][t * 64 + lane]) << 32) | (uint32_t)(t * 64 + lane);
+        wave_sort<NT>(key);
+        const u64 kk = wave_list_at<NT>(key, a.k - 1);
+        const float sk = key_score(kk);
+        if (sk < 3e38f)
+            T = M == LIRA_METRIC_L2 ? __double2float_ru(bound_P<LIRA_METRIC_L2>((double)sk, (double)E, (double)a.d))
+                                    : __double2float_ru(bound_P<LIRA_METRIC_IP>((double)sk, (double)E, (double)a.d));
+    }
+    const uint32_t qb = T < 3e38f ? f2ord(T) : ~0u;
+    if (lane == 0) a.qbound[q] = qb;
+    // slots 1.. under the bound (the partition filter)
+    for (int s0 = 1; s0 < a.nprobe; s0 += 4) {
+        const int slot = s0 + (lane >> 4);
+        const bool valid = slot < a.nprobe;
+        const int64_t pair = pair0 + (valid ? slot : 0);
+        const int praw = valid ? a.probe[pair] : -1;
+        est += pair_record(a.Q, a.d, pair, valid, praw, a.nprobe, a.n_lists, a.pivot, centred, a.lstat, qb,
+                           a.probe_live, a.QN, a.QE, a.pqn, a.QH, a.dpad, samp ? a.list_size : nullptr, a.lsamp,
+                           a.rmaxx);
+    }
+    if (samp) {  // lanes 0, 16, 32, 48 hold their pair groups' sums
+        const int tot = __builtin_amdgcn_readlane(est, 0) + __builtin_amdgcn_readlane(est, 16) +
+                        __builtin_amdgcn_readlane(est, 32) + __builtin_amdgcn_readlane(est, 48);
+        if (lane == 0 && tot) atomicAdd(a.work + ((q >> 3) & 63), (unsigned)tot);
+    }
+}
+
+template <int NC, int M>
+static hipError_t launch_seed_rn(const RSeedArgs &a, int nt, hipStream_t st) {
+    const dim3 g((unsigned)((a.nq + 3) / 4)), b(256);
+    if (nt == 1) hipLaunchKernelGGL((k_seed_r<NC, M, 1>), g, b, 0, st, a);
+    else if (nt == 2) hipLaunchKernelGGL((k_seed_r<NC, M, 2>), g, b, 0, st, a);
+    else hipLaunchKernelGGL((k_seed_r<NC, M, 4>), g, b, 0, st, a);
+    return hipGetLastError();
+}
+template <int M>
+static hipError_t launch_seed_rm(const RSeedArgs &a, int nt, hipStream_t st) {
+    switch (a.dpad / 32) {
+        case 1: return launch_seed_rn<1, M>(a, nt, st);
+        case 2: return launch_seed_rn<2, M>(a, nt, st);
+        case 3: return launch_seed_rn<3, M>(a, nt, st);
+        case 4: return launch_seed_rn<4, M>(a, nt, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+hipError_t launch_seed_r(const RSeedArgs &a, int nt, hipStream_t st) {
+    if (a.nq <= 0) return hipSuccess;
+    if (nt != 1 && nt != 2 && nt != 4) return hipErrorInvalidValue;
+    return a.metric == LIRA_METRIC_L2 ? launch_seed_rm<LIRA_METRIC_L2>(a, nt, st)
+                                      : launch_seed_rm<LIRA_METRIC_IP>(a, nt, st);
+}
+
 bool rscreen_shape_ok(int64_t dpad, int64_t k) {
-    return k >= 1 && k <= 120 && dpad >= 32 && dpad <= 128 && dpad % 32 == 0;
+    return k >= 1 && k <= 120 && dpad >= 32 && dpad % 32 == 0 && (dpad <= 128 || (dpad % 64 == 0 && dpad <= 4096));
 }
 int rscreen_smem(int rl, int waves) {
     return rl == 1 ? RSmem<1, 4>::total : rl == 2 ? RSmem<2, 4>::total : waves == 8 ? RSmem<4, 8>::total : RSmem<4, 4>::total;
@@ -773,7 +1023,9 @@ static hipError_t launch_rm(const RArgs &a, int grid, hipStream_t st) {
         case 2: return launch_r<2, M, RL, W>(a, grid, st);
         case 3: return launch_r<3, M, RL, W>(a, grid, st);
         case 4: return launch_r<4, M, RL, W>(a, grid, st);
-        default: return hipErrorInvalidValue;
+        default:
+            if (a.dpad % 64 == 0 && a.dpad <= 4096) return launch_r<0, M, RL, W>(a, grid, st);  // (streamed A)
+            return hipErrorInvalidValue;
     }
 }
 

@@ -33,6 +33,35 @@ struct RArgs {
     int scap;
 };
 
+// k_seed_r: the per-query starting bound from the split copy (hi x hi MFMA screen of
+// the first NT tiles of the query's nearest list, bound by errE_r) fused with the
+// per-pair records and the partition filter -- the k_screen_r path's seed
+struct RSeedArgs {
+    int metric;
+    const float *Q;
+    const int32_t *probe;
+    int nprobe, n_lists;
+    const int32_t *tile_off;
+    const char *Xb;
+    const float *xadj, *rmax, *rmaxx;  // centred xadj / rmax, max ||x|| (IP)
+    const float2 *tstat;
+    const float *tres;
+    const float *pivot;
+    const float2 *lstat;  // the partition filter (NULL: none)
+    int32_t *probe_live;
+    float4 *QN;
+    float *QE, *pqn;
+    uint16_t *QH;
+    const int32_t *list_size;  // (non-null) the work estimate, as k_seed_t
+    const float2 *lsamp;
+    unsigned int *work;
+    uint32_t *qbound;
+    int64_t d, dpad, nq;
+    int k;
+};
+// nt: tiles of 64 rows (1, 2 or 4; 64 nt >= k)
+hipError_t launch_seed_r(const RSeedArgs &a, int nt, hipStream_t st);
+
 // the shapes k_screen_r implements: L2 or IP on the centred split copy, hi x hi,
 // k <= 120 (row lists of 32 RL keys, RL = 1 / 2 / 4 for k <= 24 / 56 / 120; 64
 // query rows per item at RL 1, else 32), dpad <= 128 (the rows' hi parts in LDS)

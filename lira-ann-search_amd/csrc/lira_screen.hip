@@ -2397,15 +2397,17 @@ std::string screen_describe(const lira_index *idx, int64_t nq, int64_t nprobe, i
     const bool per_part = (flags & LIRA_SCAN_PER_PARTITION) != 0;
     const bool fill = nq >= (int64_t)pl.qr * idx->n_lists || nq * nprobe >= 4 * (int64_t)pl.qr * idx->n_lists;
     const int groups = !per_part && o.two_phase && nprobe >= 2 && (o.two_phase == 2 || fill) ? 2 : 1;
-    const bool fused = pl.pp && o.seed && idx->X && idx->metric == LIRA_METRIC_L2 && k <= 32 && idx->d <= 256;
-    const int seed_t = !o.seed ? 0 : fused ? (o.seed_tiles > 0 ? o.seed_tiles : nq < 4096 ? 4 : 2)
+    const bool fused_t = pl.pp && o.seed && idx->X && idx->metric == LIRA_METRIC_L2 && k <= 32 && idx->d <= 256;
+    const bool seed_r = !fused_t && pl.rs && o.seed && idx->dpad <= 128;
+    const bool fused = seed_r || fused_t;
+    const int seed_t = !o.seed ? 0 : seed_r && k > 32 ? 4 : fused ? (o.seed_tiles > 0 ? o.seed_tiles : nq < 4096 ? 4 : 2)
                        : idx->X && k <= 32 ? (idx->metric != LIRA_METRIC_L2 ? 2 : o.seed_tiles > 0 ? o.seed_tiles
                                                                                    : idx->d > 512 ? 1 : 2)
                        : 4;
     s += " plan: groups=" + std::to_string(groups) + " bpc=" + std::to_string(pl.bpc) +
          " near=" + std::to_string(groups == 2 ? pl.bpc_near_min : pl.bpc) + ".." +
          std::to_string(groups == 2 ? pl.bpc_near : pl.bpc) + " near0=" + std::to_string(groups == 2 ? pl.near0 : 0) +
-         " seed=" + std::to_string(seed_t) + (fused ? "f" : "") + " spill=" + std::to_string(pl.scap) +
+         " seed=" + std::to_string(seed_t) + (seed_r ? "r" : fused ? "f" : "") + " spill=" + std::to_string(pl.scap) +
          " rescan=" + std::to_string(pl.prescan);
     return s;
 }
@@ -2540,9 +2542,51 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     // (not for d > 256: one wave per query then walked d-long chains of dependent
     // loads for its nprobe pairs; k_pairs gives every pair its own 16 lanes --
     // measured GIST1M plan 0.160 -> 0.118 ms)
-    const bool fused = plive && qbound && o.seed && idx->X && idx->metric == LIRA_METRIC_L2 && k <= 32 && idx->d <= 256;
+    // k_screen_r's path where that fused VALU seed cannot run (IP, k > 32, the compact
+    // index): the screened seed on the matrix cores, fused with the records (k_seed_r,
+    // lira_rscreen.hip; 4 tiles for k > 32).  Measured against k_seed_t + k_pairs:
+    // DEEP10M plan 0.244 -> 0.218 ms latent, 0.224 -> 0.193 mixture, and its tighter
+    // exact k-th of 256 screened keys scan 6.29 -> 6.19 / 2.91 -> 2.83 ms; where the
+    // fused k_seed_t runs (SIFT1M) it stays: k_seed_r there was plan +4..6 us
+    const bool fused_t = plive && qbound && o.seed && idx->X && idx->metric == LIRA_METRIC_L2 && k <= 32 && idx->d <= 256;
+    const bool seed_r = !fused_t && pl.rs && plive && pl.pp && qbound && o.seed && centred && idx->tstat &&
+                        idx->lstat && idx->dpad <= 128;
+    const bool fused = seed_r || fused_t;
     if (qbound && !fused) LIRA_HIP_TRY(fill32_async(qbound, ~0u, (size_t)nq * 4, st));
-    if (fused) {
+    if (seed_r) {
+        RSeedArgs sr;
+        sr.metric = idx->metric;
+        sr.Q = q;
+        sr.probe = probe;
+        sr.nprobe = (int)nprobe;
+        sr.n_lists = (int)idx->n_lists;
+        sr.tile_off = idx->tile_off;
+        sr.Xb = (const char *)idx->Xb;
+        sr.xadj = idx->xadjc;
+        sr.rmax = idx->rmaxc;
+        sr.rmaxx = idx->rmax;
+        sr.tstat = idx->tstat;
+        sr.tres = idx->tres;
+        sr.pivot = idx->pivot;
+        sr.lstat = filter ? idx->lstat : nullptr;
+        sr.probe_live = plive;
+        sr.QN = QN;
+        sr.QE = QE;
+        sr.pqn = pqn;
+        sr.QH = QH;
+        const bool adapt = groups == 2 && pl.bpc_near_min < pl.bpc_near && idx->lsamp;
+        sr.list_size = adapt ? idx->list_size : nullptr;
+        sr.lsamp = adapt ? idx->lsamp : nullptr;
+        sr.work = adapt ? (unsigned int *)head + 64 : nullptr;
+        sr.qbound = qbound;
+        sr.d = idx->d;
+        sr.dpad = idx->dpad;
+        sr.nq = nq;
+        sr.k = (int)k;
+        const int nt_r = k > 32 ? 4 : o.seed_tiles > 0 ? o.seed_tiles : nq < 4096 ? 4 : 2;
+        const hipError_t e = launch_seed_r(sr, nt_r, st);
+        if (e != hipSuccess) return fail(LIRA_EHIP, std::string("k_seed_r launch: ") + hipGetErrorString(e));
+    } else if (fused) {
         SeedPairs sp;
         sp.pivot = idx->pivot;
         sp.centred = centred ? 1 : 0;

@@ -407,7 +407,7 @@ def test_options_do_not_change_results(metric):
                        ("prune", (0,)), ("split", (0,)), ("mfma", (0, 2)), ("rounds", (1, 64)),
                        ("near_rounds", (2, 8)), ("screen", (0,)), ("probes_hint", (1, 4)), ("xhi", (0, 1, 2)),
                        ("rscreen", (0,)), ("rescan", (0, 1)), ("spill", (0, 1, 4)), ("near_first", (0, 1, 4)),
-                       ("seed_tiles", (1, 2, 4) if metric == "L2" else (1, 2))):
+                       ("seed_tiles", (1, 2, 4))):
         old = idx.get_option(name)
         for v in vals:
             idx.set_option(name, v)
@@ -433,9 +433,10 @@ def test_options_do_not_change_results(metric):
             assert np.array_equal(I0, I1) and np.array_equal(bits(D0), bits(D1)), ("ip_centre", k)
     # the removed screen variants (k_screen_s / _w / _v, k_seed_b): 0 still reads back, others refused
     from lira_amd import LiraError
-    if metric == "inner_product":  # (4 seed tiles exist only in the fused L2 seed)
-        with pytest.raises(LiraError, match="EUNSUPPORTED"):
-            idx.set_option("seed_tiles", 4)
+    # (4 seed tiles exist only in the fused seeds: refused where neither can run)
+    wide = make_index(np.zeros((64, 300), np.float32), np.zeros((64, 1), np.int32), 1, metric)
+    with pytest.raises(LiraError, match="EUNSUPPORTED"):
+        wide.set_option("seed_tiles", 4)
     for name, bad in (("pipeline", 1), ("ring", 3), ("wide", 1), ("seed", 2)):
         with pytest.raises(LiraError, match="EUNSUPPORTED"):
             idx.set_option(name, bad)
