@@ -166,7 +166,9 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *                        ranges are narrow and the triangle-inequality skip drops more; 0: list order.
  *                        Results never depend on it.
  *   LIRA_OPT_RSCREEN     1 (default): the wave-streaming screen k_screen_r where it applies (L2 or
- *                        centred IP on the split copy with the hi x hi screen, k <= 120, dpad <= 128, the
+ *                        centred IP on the split copy with the hi x hi screen, k <= 120, dpad <= 128
+ *                        -- 2: also dpad > 128, a multiple of 64, the rows' hi parts streamed from
+ *                        their records (measured slower than k_screen_m on GIST1M latent), the
  *                        per-query seed on, not PER_PARTITION): query rows' hi parts in LDS, each
  *                        wave streaming its own candidate tiles into registers; 0: k_screen_m
  *   LIRA_OPT_NEAR_FIRST  (k_screen_r) blocks of 256 candidates in the first chunk of every query

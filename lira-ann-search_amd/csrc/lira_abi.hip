@@ -790,7 +790,7 @@ int lira_index_set_option(lira_index *idx, int option, int64_t value) {
         case LIRA_OPT_PROBES_HINT: if (!in(0, 1 << 20)) break; o.probes_hint = v; return LIRA_OK;
         case LIRA_OPT_XHI: if (!in(-1, 2)) break; o.xhi = v; return LIRA_OK;
         case LIRA_OPT_ORDER: if (!in(0, 1)) break; o.order = v; return LIRA_OK;
-        case LIRA_OPT_RSCREEN: if (!in(0, 1)) break; o.rscreen = v; return LIRA_OK;
+        case LIRA_OPT_RSCREEN: if (!in(0, 2)) break; o.rscreen = v; return LIRA_OK;
         case LIRA_OPT_NEAR_FIRST: if (!in(-1, 128)) break; o.near_first = v; return LIRA_OK;
         case LIRA_OPT_RESCAN: if (!in(-1, 1)) break; o.rescan = v; return LIRA_OK;
         case LIRA_OPT_SPILL: if (!in(-1, 1 << 16)) break; o.spill = v; return LIRA_OK;

@@ -2176,7 +2176,10 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     const int rs_qr = rscreen_qr(pl.rl, rs_waves);
     const bool rs = op.rscreen && (op.split || !idx->X) && (op.mfma || !idx->X) && op.seed && !(flags & (LIRA_SCAN_NO_SPLIT | LIRA_SCAN_PER_PARTITION)) &&
                     idx->Xb && idx->xadjc && idx->pivot && idx->lstat && rscreen_shape_ok(idx->dpad, k) && xhi == 2 &&
-                    (op.qr == 0 || op.qr == rs_qr) && (idx->metric == LIRA_METRIC_L2 || idx->ipc);
+                    (op.qr == 0 || op.qr == rs_qr) && (idx->metric == LIRA_METRIC_L2 || idx->ipc) &&
+                    // dpad > 128 (streamed A operands) only with LIRA_OPT_RSCREEN = 2: measured GIST1M
+                    // (d = 960) latent scan + merge 1.21 ms against k_screen_m's 1.10, mixture even
+                    (idx->dpad <= 128 || (op.rscreen == 2 && nq * nprobe * idx->dpad < (int64_t)UINT32_MAX));
     // the split-bf16 screen unless asked off (it is the only one without the fp32
     // tiles); a centred IP copy has no k_screen_m form: the fp32 tiles there
     const bool split_wanted = idx->ipc ? rs : (op.split && !(flags & LIRA_SCAN_NO_SPLIT)) || !idx->X;

@@ -119,7 +119,19 @@ def test_k_sweep(metric, k):
 @pytest.mark.parametrize("d", [1, 3, 31, 33, 96, 128, 200, 960])
 def test_dims(d):
     x, q, d2b, probe = random_case(200 + d, 3000, d, 6, 33, 3, "L2")
-    check_vs_oracle(x, q, d2b, probe, 6, 10, "L2")
+    idx = check_vs_oracle(x, q, d2b, probe, 6, 10, "L2")
+    if d > 128 and (d + 31) // 32 % 2 == 0:  # k_screen_r with the rows' hi parts streamed (LIRA_OPT_RSCREEN = 2)
+        off, ids = oracle.build_csr(d2b, 6)
+        vecs = oracle.gather_lists(x, off, ids)
+        for metric, k in (("L2", 10), ("L2", 100), ("inner_product", 100)):
+            idx2 = idx if metric == "L2" else make_index(x, d2b, 6, metric)
+            idx2.set_option("rscreen", 2)
+            assert idx2.describe(33, 3, k).startswith("k_screen_r"), (metric, k)
+            met = oracle.IP if metric == "inner_product" else oracle.L2
+            Do, Io, _ = oracle.scan_topk(q, off, ids, vecs, probe, k, met, idx2.max_replicas)
+            D, I, _ = run(idx2, q, probe, k)
+            assert np.array_equal(I, Io) and np.array_equal(bits(D), bits(Do)), (metric, k)
+            idx2.set_option("rscreen", 1)
 
 
 def test_uniform_random_float_inputs():
