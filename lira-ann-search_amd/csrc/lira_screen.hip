@@ -1769,6 +1769,30 @@ __global__ __launch_bounds__(256) void k_seed(const float *Q, const int32_t *pro
     if (lane == 0 && B < __builtin_inff()) qbound[q] = f2ord(B);
 }
 
+// The k-th smallest key of a sorted wave list, counting equal keys once when
+// dedup (a vector stored in two partitions gives the same key twice: its exact
+// score is the same sum); kEmptyKey if there are fewer.  Wave-uniform.
+template <int R>
+__device__ __forceinline__ u64 kth_distinct(const u64 (&lst)[R], int k, int dedup) {
+    if (!dedup) return k <= 64 * R ? wave_list_at<R>(lst, k - 1) : kEmptyKey;
+    const int lane = lane_id();
+    int cnt = 0;
+    u64 prev_last = kEmptyKey, res = kEmptyKey;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const u64 up = shfl64(lst[r], lane == 0 ? 0 : lane - 1);
+        const u64 prev = lane == 0 ? prev_last : up;
+        const bool nd = lst[r] != kEmptyKey && !((r > 0 || lane > 0) && prev == lst[r]);
+        const u64 bal = __ballot(nd);
+        const bool hit = nd && cnt + mbcnt64(bal) == k - 1;
+        const u64 hb = __ballot(hit);
+        if (hb) res = shfl64(lst[r], __builtin_ctzll(hb));
+        cnt += popc64(bal);
+        prev_last = shfl64(lst[r], 63);
+    }
+    return res;
+}
+
 template <int R>
 __device__ __forceinline__ void merge_batch_if(u64 (&lst)[R], u64 batch) {
     const u64 thr = wave_list_at<R>(lst, 64 * R - 1);
@@ -1812,6 +1836,13 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
 
     u64 lst[R];
     int pc = 0;  // pending survivors (storage rows) in pend[0..pc)
+    // Trun: the k-th smallest exact score re-checked so far (k distinct keys with
+    // dedup) -- it bounds the final k-th exact score like T, and is usually far
+    // tighter (T is a screened key + E), so the limits below tighten to it as the
+    // re-checks come in: a candidate of exact score <= the final k-th has
+    // s~ <= s_lim(final k-th, E) <= s_lim(Trun, E) (not with per-partition lists)
+    float Trun = __builtin_inff();
+    const bool tighten = !a.per_partition;
     auto reset = [&]() {
 #pragma unroll
         for (int r = 0; r < R; ++r) lst[r] = kEmptyKey;
@@ -1826,6 +1857,10 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
         n_rechecked += pc;
         merge_batch_if<R>(lst, key);
         pc = 0;
+        if (tighten) {
+            const u64 kk = kth_distinct<R>(lst, k, a.dedup);
+            if (kk != kEmptyKey) Trun = fminf(Trun, key_score(kk));
+        }
         __builtin_amdgcn_wave_barrier();
     };
     auto add = [&](bool take, uint32_t pos) {
@@ -1881,13 +1916,13 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
                 if (p < 0 || p >= a.n_lists || c >= a.nch[vnch(s, p)]) p = -1;
             }
             const u64 *src = a.partial + ((q * a.nprobe + (p >= 0 ? s : 0)) * (int64_t)NC + (p >= 0 ? c : 0)) * K2;
-            double lim = 0.0;
+            double lim = 0.0, E = 0.0;
             bool over = false, uns = a.unsorted != 0;
             if (p >= 0) {
                 const double qn_s = a.centred ? (double)a.pqn[q * a.nprobe + s] : qnorm;
-                const double E = a.pE ? (double)a.pE[(q * a.nprobe + s) * (int64_t)NC + c]
-                                      : err_E<METRIC>(qn_s, (double)a.rmax[p], dd, a.split, (double)a.dpad, a.centred);
-                lim = s_lim<METRIC>((double)T, E, dd);
+                E = a.pE ? (double)a.pE[(q * a.nprobe + s) * (int64_t)NC + c]
+                         : err_E<METRIC>(qn_s, (double)a.rmax[p], dd, a.split, (double)a.dpad, a.centred);
+                lim = s_lim<METRIC>((double)fminf(T, Trun), E, dd);
                 const u64 last = src[K2 - 1];
                 over = last != kEmptyKey && (double)key_score(last) <= lim;  // (kUnsortedMark: a NaN score)
                 uns = uns || last == kUnsortedMark;  // an unmerged row buffer (k_screen_m): walk to its first empty key
@@ -1897,7 +1932,12 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
             bool active = p >= 0 && (!over || sok) && a.rmode != 1;
             // four keys per round (two 16-B loads; K2 % 4 == 0, lists 32-B aligned):
             // the walk is one dependent load per round
+            float Tl = fminf(T, Trun);
             for (int e0 = 0; __any(active); e0 += 4) {
+                if (Trun < Tl) {  // (a flush tightened the bound: wave-uniform)
+                    Tl = Trun;
+                    if (p >= 0) lim = s_lim<METRIC>((double)Tl, E, dd);
+                }
                 u64 kv[4] = {kEmptyKey, kEmptyKey, kEmptyKey, kEmptyKey};
                 if (active && e0 < K2) {
                     const ulonglong2 a0 = *(const ulonglong2 *)(src + e0), a1 = *(const ulonglong2 *)(src + e0 + 2);
@@ -1940,7 +1980,7 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
                 const int ln = __builtin_ctzll(ov);
                 ov &= ov - 1;
                 const int li2 = l0 + ln;
-                rescan(s_lo + li2 / NCe, plv[s_lo + li2 / NCe], li2 % NCe, T);
+                rescan(s_lo + li2 / NCe, plv[s_lo + li2 / NCe], li2 % NCe, fminf(T, Trun));
             }
         }
     };
@@ -2003,7 +2043,7 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
                 if (i0 + lane < ns) {
                     const uint4 r = sp[i0 + lane];
                     const u64 key = ((u64)r.y << 32) | r.x;
-                    take = (double)key_score(key) <= s_lim<METRIC>((double)T, (double)__uint_as_float(r.z), dd);
+                    take = (double)key_score(key) <= s_lim<METRIC>((double)fminf(T, Trun), (double)__uint_as_float(r.z), dd);
                     pos = r.x;
                 }
                 add(take, pos);

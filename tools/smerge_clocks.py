@@ -33,8 +33,8 @@ for _ in range(reps):
     idx.search(q, probe, k)
 torch.cuda.synchronize()
 lib.lira_debug_smerge_clocks(v)
-names = ["prologue (bound, spill count)", "take_lists (list walk)", "spill records", "exact re-check + merge",
-         "emit"]
+names = ["prologue (bound, candidate count)", "take_lists (list walk)", "spill records",
+         "last exact re-check + merge", "emit"]
 tot = sum(v[i] for i in range(5))
 waves = max(1, v[5])
 print(f"{cfg}/{data}: {waves // reps} query waves per call, rechecked {v[6] / waves:.1f} per query")
