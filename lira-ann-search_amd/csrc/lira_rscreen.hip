@@ -61,7 +61,10 @@ struct RSmem {
     static constexpr int QR = RL == 1 || W == 8 ? 64 : 32;         // query rows per item
     static constexpr int K2 = 32 * RL;                             // row list keys
     static constexpr int NRG = QR / 16;                            // MFMA row groups
-    static constexpr int BC = W == 8 ? 8 : 16;                     // survivor buffer keys per (wave, row)
+    // survivor buffer keys per (wave, row): as many as the 80 KB allow -- every full
+    // buffer costs a locked 32 RL-key list merge (DEEP10M mixture, RL 4: 16 -> 24
+    // keys, scan 2.82 -> 2.17 ms)
+    static constexpr int BC = W == 8 ? 8 : RL == 4 ? 24 : RL == 2 ? 32 : 16;
     static constexpr int aq = 0;                                   // [4 chunks][NRG][64 lanes] 16 B: A operands
     static constexpr int lists = aq + 4 * NRG * 64 * 16;           // [QR][K2] u64
     static constexpr int bufs = lists + QR * K2 * 8;               // [W][QR][BC] u64
