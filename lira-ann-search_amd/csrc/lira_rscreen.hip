@@ -63,12 +63,14 @@ struct RSmem {
     static constexpr int NRG = QR / 16;                            // MFMA row groups
     // survivor buffer keys per (wave, row): as many as the 80 KB allow -- every full
     // buffer costs a locked 32 RL-key list merge (DEEP10M mixture, RL 4: 16 -> 24
-    // keys, scan 2.82 -> 2.17 ms)
-    static constexpr int BC = W == 8 ? 8 : RL == 4 ? 24 : RL == 2 ? 32 : 16;
+    // keys, scan 2.82 -> 2.17 ms); 6 bytes a key: its high word and its position in
+    // the item (the list key is rebuilt when merged)
+    static constexpr int BC = W == 8 ? 8 : RL == 1 ? 21 : 32;  // (<= 32: a flush merges one key per half-wave lane)
     static constexpr int aq = 0;                                   // [4 chunks][NRG][64 lanes] 16 B: A operands
     static constexpr int lists = aq + 4 * NRG * 64 * 16;           // [QR][K2] u64
-    static constexpr int bufs = lists + QR * K2 * 8;               // [W][QR][BC] u64
-    static constexpr int bufc = bufs + W * QR * BC * 8;            // [W][64] int (lane = row)
+    static constexpr int bufs = lists + QR * K2 * 8;               // [W][QR][BC] u32: wkey high words
+    static constexpr int bufl = bufs + W * QR * BC * 4;            // [W][QR][BC] u16: positions in the item
+    static constexpr int bufc = bufl + W * QR * BC * 2;            // [W][64] int (lane = row)
     static constexpr int hs = bufc + W * 64 * 4;                   // [W][64] float: the wave's thresholds
     static constexpr int tst = hs + W * 64 * 4;                    // [512] float2: tile radius ranges
     static constexpr int trs = tst + kRMaxTiles * 8;               // [512] float: tile hi residuals
@@ -85,6 +87,7 @@ struct RSmem {
 static_assert(RSmem<1, 4>::total <= 80 * 1024 && RSmem<2, 4>::total <= 80 * 1024 && RSmem<4, 4>::total <= 80 * 1024,
               "k_screen_r: two 4-wave workgroups per CU");
 static_assert(RSmem<4, 8>::total <= 160 * 1024, "k_screen_r: one 8-wave workgroup per CU");
+static_assert(RSmem<1, 4>::BC <= 32 && RSmem<2, 4>::BC <= 32 && RSmem<4, 4>::BC <= 32, "flush_row merges <= 32 keys");
 static_assert(kROCap >= 128, "a drained queue takes two full candidate masks");
 
 // a value the compiler must treat as produced here (keeps per-lane address
@@ -217,9 +220,10 @@ __device__ __forceinline__ void spill_evicted(const RArgs &a, u64 ev, bool hv, u
 // (readers take the list's k-th key, then the bound: program order in both),
 // half-wave merge, publish the query's bound if the list's k-th improved.
 template <int M, int RL, int BC>
-__device__ __forceinline__ void flush_row(u64 *lists, u64 *kth_s, const u64 *mybuf, int *lock_s, uint32_t *erun_s,
-                                          uint32_t *opub_s, const int *pair_s, int row, int n, int ew_bits, int k,
-                                          float qv_row, const RArgs &a, float Tc_row) {
+__device__ __forceinline__ void flush_row(u64 *lists, u64 *kth_s, const uint32_t *mbh, const uint16_t *mbl,
+                                          uint32_t pos_base, int *lock_s, uint32_t *erun_s, uint32_t *opub_s,
+                                          const int *pair_s, int row, int n, int ew_bits, int k, float qv_row,
+                                          const RArgs &a, float Tc_row) {
     constexpr int K2 = 32 * RL;
     const int lane = opaque(lane_id()), hl = lane & 31;  // (opaque: addresses computed here, not hoisted)
     if (lane == 0) {
@@ -230,7 +234,8 @@ __device__ __forceinline__ void flush_row(u64 *lists, u64 *kth_s, const u64 *myb
     u64 lst[RL];
 #pragma unroll
     for (int r = 0; r < RL; ++r) lst[r] = lists[row * K2 + r * 32 + hl];
-    const u64 b = hl < n ? wkey_to_key<M>(mybuf[row * BC + hl], qv_row) : kEmptyKey;
+    const u64 b = hl < n ? wkey_to_key<M>(((u64)mbh[row * BC + hl] << 32) | (pos_base + mbl[row * BC + hl]), qv_row)
+                         : kEmptyKey;
     u64 ev = kEmptyKey;
     if (a.spill)
         ev = merge_evict<RL>(lst, b);
@@ -265,7 +270,7 @@ __device__ __forceinline__ void flush_row(u64 *lists, u64 *kth_s, const u64 *myb
 // queue into the buffers (LDS atomic slots), merging every buffer that fills,
 // until the queue is empty.
 template <int M, int RL, int BC>
-__device__ __forceinline__ void drain_buffers(u64 *lists, u64 *kth_s, u64 *mybuf, int *mybufc, int *lock_s,
+__device__ __forceinline__ void drain_buffers(u64 *lists, u64 *kth_s, uint32_t *mbh, uint16_t *mbl, int *mybufc, int *lock_s,
                                               uint32_t *erun_s, uint32_t *opub_s, const int *pair_s,
                                               const float4 *rec_s, const u64 *oq_key, uint32_t pos_base, int nq,
                                               float Ew, int k, const RArgs &a, float Tc) {
@@ -275,7 +280,7 @@ __device__ __forceinline__ void drain_buffers(u64 *lists, u64 *kth_s, u64 *mybuf
         while (full) {
             const int row = __builtin_ctzll(full);
             full &= full - 1;
-            flush_row<M, RL, BC>(lists, kth_s, mybuf, lock_s, erun_s, opub_s, pair_s, row, BC,
+            flush_row<M, RL, BC>(lists, kth_s, mbh, mbl, pos_base, lock_s, erun_s, opub_s, pair_s, row, BC,
                              __builtin_amdgcn_readlane(__float_as_int(Ew), row), k, rec_s[row].x, a,
                              __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Tc), row)));
             if (lane == 0) mybufc[row] = 0;
@@ -290,12 +295,13 @@ __device__ __forceinline__ void drain_buffers(u64 *lists, u64 *kth_s, u64 *mybuf
         // the item; the selection does no conversion)
         const u64 q = pend ? oq_key[e] : 0ull;
         const int row = (int)((q >> 16) & 63u);
-        const u64 key = pend ? wkey(__uint_as_float((uint32_t)(q >> 32)), pos_base + (uint32_t)(q & 0xffffu)) : kEmptyKey;
+        const uint32_t kh = pend ? f2ord(-__uint_as_float((uint32_t)(q >> 32))) : 0u;  // (wkey's high word)
         while (__any(pend)) {
             if (pend) {
                 const int slot = atomicAdd(mybufc + row, 1);
                 if (slot < BC) {
-                    mybuf[row * BC + slot] = key;
+                    mbh[row * BC + slot] = kh;
+                    mbl[row * BC + slot] = (uint16_t)(q & 0xffffu);
                     pend = false;
                 }
             }
@@ -315,7 +321,8 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void k_screen_r(RArgs a) {
     constexpr int NSTEP = 8 * NRG;  // selection steps per tile: (row group, register, candidate pair)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     u64 *lists = (u64 *)(smem + S::lists);
-    u64 *bufs = (u64 *)(smem + S::bufs);
+    uint32_t *bufs = (uint32_t *)(smem + S::bufs);
+    uint16_t *bufl = (uint16_t *)(smem + S::bufl);
     int *bufc = (int *)(smem + S::bufc);
     float *hs = (float *)(smem + S::hs);
     float2 *tst = (float2 *)(smem + S::tst);
@@ -335,7 +342,8 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void k_screen_r(RArgs a) {
     const int g = lane >> 4, cj = lane & 15;
     const int k = a.k;
     const float dp = (float)a.dpad, dd = (float)a.d;
-    u64 *mybuf = bufs + wave * QR * BC;
+    uint32_t *mybuf = bufs + wave * QR * BC;
+    uint16_t *mybufl = bufl + wave * QR * BC;
     int *mybufc = bufc + wave * 64;
     float *myh = hs + wave * 64;
     u64 *oq_key = (u64 *)(smem + S::oqk) + wave * kROCap;
@@ -572,7 +580,7 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void k_screen_r(RArgs a) {
         int ovf = 0;  // survivor queue fill (wave-uniform)
         // survivor queue -> this wave's row buffers (full ones merged into the lists)
         auto drain = [&]() {
-            drain_buffers<M, RL, BC>(lists, kth_s, mybuf, mybufc, lock_s, erun_s, opub_s, pair_s, rec_s, oq_key,
+            drain_buffers<M, RL, BC>(lists, kth_s, mybuf, mybufl, mybufc, lock_s, erun_s, opub_s, pair_s, rec_s, oq_key,
                                  (uint32_t)tbase * 64u, ovf, Ew, k, a, Tc);
             ovf = 0;
         };
@@ -738,7 +746,8 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void k_screen_r(RArgs a) {
                 if (e < n) {
                     int w = 0, off = e;  // (the wave buffer holding key e of the row's concatenation)
                     while (off >= bufc[w * 64 + row]) off -= bufc[w++ * 64 + row];
-                    b = wkey_to_key<M>(bufs[(w * QR + row) * BC + off], qv_r);
+                    const int e2 = (w * QR + row) * BC + off;
+                    b = wkey_to_key<M>(((u64)bufs[e2] << 32) | ((uint32_t)tbase * 64u + bufl[e2]), qv_r);
                 }
                 u64 lst[RL];
 #pragma unroll
