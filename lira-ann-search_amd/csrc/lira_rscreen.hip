@@ -215,38 +215,48 @@ __device__ __forceinline__ void spill_evicted(const RArgs &a, u64 ev, bool hv, u
         a.spill[(int64_t)q * a.scap + at] = make_uint4((uint32_t)ev, (uint32_t)(ev >> 32), __float_as_uint(er), 0u);
 }
 
-// Merge this wave's buffer of `row` (n keys) into the shared list, under the
-// row's LDS lock: raise the row's running error bound to the wave's first
-// (readers take the list's k-th key, then the bound: program order in both),
-// half-wave merge, publish the query's bound if the list's k-th improved.
+// Merge this wave's buffers of two rows (half-wave h: row rows[h], BC keys; a
+// second row < 0: half 1 idles) into their shared lists, under the rows' LDS
+// locks (taken in row order, row0 < row1: no two waves wait on each other):
+// raise each row's running error bound to the wave's first (readers take the
+// list's k-th key, then the bound: program order in both), half-wave merges,
+// publish the query's bound where a list's k-th improved.  One row per half: a
+// single-row merge left half of the wave idle in every flush.
 template <int M, int RL, int BC>
-__device__ __forceinline__ void flush_row(u64 *lists, u64 *kth_s, const uint32_t *mbh, const uint16_t *mbl,
-                                          uint32_t pos_base, int *lock_s, uint32_t *erun_s, uint32_t *opub_s,
-                                          const int *pair_s, int row, int n, int ew_bits, int k, float qv_row,
-                                          const RArgs &a, float Tc_row) {
+__device__ __forceinline__ void flush_rows(u64 *lists, u64 *kth_s, const uint32_t *mbh, const uint16_t *mbl,
+                                           uint32_t pos_base, int *lock_s, uint32_t *erun_s, uint32_t *opub_s,
+                                           const int *pair_s, int row0, int row1, int ew0, int ew1, int k,
+                                           const float4 *rec_s, const RArgs &a, float Tc0, float Tc1) {
     constexpr int K2 = 32 * RL;
     const int lane = opaque(lane_id()), hl = lane & 31;  // (opaque: addresses computed here, not hoisted)
+    const bool h1 = lane >= 32, act = !h1 || row1 >= 0;
+    const int row = h1 && row1 >= 0 ? row1 : row0;
     if (lane == 0) {
-        while (atomicCAS(lock_s + row, 0, 1) != 0) __builtin_amdgcn_s_sleep(1);
-        atomicMax(erun_s + row, (uint32_t)ew_bits);
+        while (atomicCAS(lock_s + row0, 0, 1) != 0) __builtin_amdgcn_s_sleep(1);
+        atomicMax(erun_s + row0, (uint32_t)ew0);
+    }
+    if (lane == 32 && row1 >= 0) {
+        while (atomicCAS(lock_s + row1, 0, 1) != 0) __builtin_amdgcn_s_sleep(1);
+        atomicMax(erun_s + row1, (uint32_t)ew1);
     }
     asm volatile("" ::: "memory");
     u64 lst[RL];
 #pragma unroll
     for (int r = 0; r < RL; ++r) lst[r] = lists[row * K2 + r * 32 + hl];
-    const u64 b = hl < n ? wkey_to_key<M>(((u64)mbh[row * BC + hl] << 32) | (pos_base + mbl[row * BC + hl]), qv_row)
-                         : kEmptyKey;
+    const u64 b = act && hl < BC ? wkey_to_key<M>(((u64)mbh[row * BC + hl] << 32) | (pos_base + mbl[row * BC + hl]),
+                                       rec_s[row].x)
+                      : kEmptyKey;
     u64 ev = kEmptyKey;
     if (a.spill)
         ev = merge_evict<RL>(lst, b);
     else
         half_merge_batch1<RL>(lst, b);
-    if (lane < 32) {
+    if (act) {
 #pragma unroll
         for (int r = 0; r < RL; ++r) lists[row * K2 + r * 32 + hl] = lst[r];
     }
-    const u64 kk = list_at<RL>(lst, k - 1);
-    if (lane == 0) {
+    const u64 kk = list_at<RL>(lst, k - 1);  // (per half)
+    if (hl == 0 && act) {
         kth_s[row] = kk;
         if (kk != kEmptyKey && a.qbound) {
             const int pr = pair_s[row];
@@ -259,11 +269,11 @@ __device__ __forceinline__ void flush_row(u64 *lists, u64 *kth_s, const uint32_t
             }
         }
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (LDS in order: the list is written before the unlock)
-    if (lane == 0) *(volatile int *)(lock_s + row) = 0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (LDS in order: the lists are written before the unlocks)
+    if (hl == 0 && act) *(volatile int *)(lock_s + row) = 0;
     __builtin_amdgcn_wave_barrier();
-    if (a.spill)  // (after the unlock: the atomic's round trip holds no other wave)
-        spill_evicted<M>(a, ev, lane < 32, kk, __uint_as_float(erun_s[row]), Tc_row, pair_s[row]);
+    if (a.spill)  // (after the unlocks: the atomics' round trips hold no other wave)
+        spill_evicted<M>(a, ev, act, kk, __uint_as_float(erun_s[row]), h1 ? Tc1 : Tc0, pair_s[row]);
 }
 
 // Merge this wave's full row buffers into the lists, then move the survivor
@@ -278,12 +288,18 @@ __device__ __forceinline__ void drain_buffers(u64 *lists, u64 *kth_s, uint32_t *
     auto flush_full = [&]() {
         u64 full = __ballot(mybufc[lane] >= BC);  // lane = row
         while (full) {
-            const int row = __builtin_ctzll(full);
+            const int row0 = __builtin_ctzll(full);
             full &= full - 1;
-            flush_row<M, RL, BC>(lists, kth_s, mbh, mbl, pos_base, lock_s, erun_s, opub_s, pair_s, row, BC,
-                             __builtin_amdgcn_readlane(__float_as_int(Ew), row), k, rec_s[row].x, a,
-                             __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Tc), row)));
-            if (lane == 0) mybufc[row] = 0;
+            const int row1 = full ? __builtin_ctzll(full) : -1;
+            if (full) full &= full - 1;
+            const int r1 = row1 >= 0 ? row1 : row0;
+            flush_rows<M, RL, BC>(lists, kth_s, mbh, mbl, pos_base, lock_s, erun_s, opub_s, pair_s, row0, row1,
+                                  __builtin_amdgcn_readlane(__float_as_int(Ew), row0),
+                                  __builtin_amdgcn_readlane(__float_as_int(Ew), r1), k, rec_s, a,
+                                  __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Tc), row0)),
+                                  __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Tc), r1)));
+            if (lane == 0) mybufc[row0] = 0;
+            if (lane == 0 && row1 >= 0) mybufc[row1] = 0;
             __builtin_amdgcn_wave_barrier();
         }
     };
