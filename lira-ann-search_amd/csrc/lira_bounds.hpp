@@ -123,6 +123,9 @@ __device__ __forceinline__ float row_h(double lim, double qn, double qnorm, doub
 // slack, slack = 1.01 u |qc| + (d + 2) u ||q|| rmx[p] (search.cpp's own rounding
 // of the exact sum, rmx the list's max ||x||), so a list whose largest radius
 // lies below (-qc - slack - T) / ||q|| holds no candidate with exact score <= T.
+// G: lanes per pair (16; 64 for long rows, k_pairs at d > 256 -- the dims loop is
+// then a quarter as long: GIST1M's 960 dims were 60 dependent-load steps per lane)
+template <int G = 16>
 __device__ __forceinline__ int pair_record(const float *Q, int64_t d, int64_t pair, bool valid, int praw,
                                            int nprobe, int n_lists, const float *pivot, int centred,
                                            const float2 *lstat, uint32_t qb, int32_t *probe_live, float4 *QN,
@@ -130,12 +133,12 @@ __device__ __forceinline__ int pair_record(const float *Q, int64_t d, int64_t pa
                                            const int32_t *est_size = nullptr, const float2 *est_samp = nullptr,
                                            const float *rmx = nullptr) {
     const bool ipm = centred == 2;
-    const int sub = threadIdx.x & 15;
+    const int sub = threadIdx.x & (G - 1);
     const int p = praw < n_lists ? praw : -1;  // (an id >= n_lists passes through: k_count reports it)
     const int64_t q = valid ? pair / nprobe : 0;
     // (estimate) this lane's sample tile of the list and the list's size, loaded ahead
     const bool est_on = est_size && p >= 0;
-    const float2 ts = est_on ? est_samp[p * 16 + sub] : make_float2(0.0f, 0.0f);
+    const float2 ts = est_on && sub < 16 ? est_samp[p * 16 + sub] : make_float2(0.0f, 0.0f);
     const int lsz = est_on ? est_size[p] : 0;
     double s = 0.0, t = 0.0, e = 0.0;
     if (p >= 0 && (QN || lstat)) {
@@ -144,7 +147,7 @@ __device__ __forceinline__ int pair_record(const float *Q, int64_t d, int64_t pa
         // (unrolled: 8 iterations' loads in flight together -- a dependent load per
         // iteration made the fused seed + pairs kernel latency-bound)
 #pragma unroll 8
-        for (int64_t j = sub; j < d; j += 16) {
+        for (int64_t j = sub; j < d; j += G) {
             const float x = qr[j], cv = pv ? pv[j] : 0.0f;
             const float sv = centred == 1 && pv ? x - cv : x;
             if (qh) qh[j] = (uint16_t)bf16_rne_sat(sv);
@@ -164,10 +167,10 @@ __device__ __forceinline__ int pair_record(const float *Q, int64_t d, int64_t pa
             }
         }
         if (qh)
-            for (int64_t j = d + sub; j < dpad; j += 16) qh[j] = 0;
+            for (int64_t j = d + sub; j < dpad; j += G) qh[j] = 0;
     }
 #pragma unroll
-    for (int m = 8; m >= 1; m >>= 1) {  // within the 16-lane DPP row
+    for (int m = G / 2; m >= 1; m >>= 1) {  // within the pair's lanes
         s += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, s), m));
         t += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, t), m));
         e += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, e), m));
@@ -207,9 +210,9 @@ __device__ __forceinline__ int pair_record(const float *Q, int64_t d, int64_t pa
     }
     int est = 0;
     if (est_size) {
-        const bool hit = est_on && valid && live >= 0 && !(ts.y < fa || ts.x > fb);
+        const bool hit = est_on && valid && live >= 0 && sub < 16 && !(ts.y < fa || ts.x > fb);
         const unsigned long long bal = __ballot(hit);
-        const int hits = __builtin_popcount((unsigned)((bal >> (threadIdx.x & 48)) & 0xffffu));  // (this pair's 16 lanes)
+        const int hits = __builtin_popcount((unsigned)((bal >> (threadIdx.x & (64 - G))) & 0xffffu));  // (the pair's first 16 lanes)
         est = (int)(((int64_t)((lsz + 255) / 256) * hits) / 16);  // blocks of 4 tiles
     }
     if (sub != 0 || !valid) return est;

@@ -2121,19 +2121,21 @@ __global__ __launch_bounds__(256) void k_rescan(RescanArgs a) {
 }
 
 // ---- per-pair records + the partition filter (lira_bounds.hpp pair_record) ----
-// One pair per 16 lanes, the filter bound from qbound (k_seed_t's seed); the
-// default L2 screen runs the same records inside k_seed_t<..., PAIRS> instead.
+// One pair per G lanes (16; a whole wave for d > 256), the filter bound from
+// qbound (k_seed_t's seed); the default L2 screen runs the same records inside
+// k_seed_t<..., PAIRS> instead.
+template <int G>
 __global__ __launch_bounds__(256) void k_pairs(const float *Q, int64_t d, const int32_t *probe, int64_t npairs,
                                                int nprobe, int n_lists, const float *pivot, int centred,
                                                const float2 *lstat, const uint32_t *qbound, int32_t *probe_live,
                                                float4 *QN, float *QE, float *pqn, uint16_t *QH, int64_t dpad,
                                                const float *rmx) {
-    const int64_t pair = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+    const int64_t pair = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
     const bool valid = pair < npairs;
     const int praw = valid ? probe[pair] : -1;
     const uint32_t qb = valid && lstat && qbound ? qbound[pair / nprobe] : ~0u;
-    pair_record(Q, d, pair, valid, praw, nprobe, n_lists, pivot, centred, lstat && qbound ? lstat : nullptr, qb,
-                probe_live, QN, QE, pqn, QH, dpad, nullptr, nullptr, rmx);
+    pair_record<G>(Q, d, pair, valid, praw, nprobe, n_lists, pivot, centred, lstat && qbound ? lstat : nullptr, qb,
+                   probe_live, QN, QE, pqn, QH, dpad, nullptr, nullptr, rmx);
 }
 
 // (stats on) what the plan's partition filter removed: pairs whose probe slot
@@ -2159,10 +2161,15 @@ static hipError_t launch_pairs(const float *Q, int64_t d, const int32_t *probe, 
                                int n_lists, const float *pivot, int centred, const float2 *lstat,
                                const uint32_t *qbound, int32_t *probe_live, float4 *QN, float *QE, float *pqn,
                                uint16_t *QH, int64_t dpad, const float *rmx, hipStream_t st) {
-    const unsigned g = (unsigned)((npairs * 16 + 255) / 256);
+    const bool wide = d > 256;
+    const unsigned g = (unsigned)((npairs * (wide ? 64 : 16) + 255) / 256);
     if (g == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_pairs, dim3(g), dim3(256), 0, st, Q, d, probe, npairs, nprobe, n_lists, pivot, centred, lstat,
-                       qbound, probe_live, QN, QE, pqn, QH, dpad, rmx);
+    if (wide)
+        hipLaunchKernelGGL((k_pairs<64>), dim3(g), dim3(256), 0, st, Q, d, probe, npairs, nprobe, n_lists, pivot,
+                           centred, lstat, qbound, probe_live, QN, QE, pqn, QH, dpad, rmx);
+    else
+        hipLaunchKernelGGL((k_pairs<16>), dim3(g), dim3(256), 0, st, Q, d, probe, npairs, nprobe, n_lists, pivot,
+                           centred, lstat, qbound, probe_live, QN, QE, pqn, QH, dpad, rmx);
     return hipGetLastError();
 }
 
