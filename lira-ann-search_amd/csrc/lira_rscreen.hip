@@ -984,7 +984,7 @@ __global__ __launch_bounds__(256) void k_seed_r(RSeedArgs a) {
     const uint32_t qb = T < 3e38f ? f2ord(T) : ~0u;
     if (lane == 0) a.qbound[q] = qb;
     // slots 1.. under the bound (the partition filter)
-    for (int s0 = 1; s0 < a.nprobe; s0 += 4) {
+    for (int s0 = 1; a.records && s0 < a.nprobe; s0 += 4) {
         const int slot = s0 + (lane >> 4);
         const bool valid = slot < a.nprobe;
         const int64_t pair = pair0 + (valid ? slot : 0);

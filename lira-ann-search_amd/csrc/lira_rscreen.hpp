@@ -58,6 +58,7 @@ struct RSeedArgs {
     uint32_t *qbound;
     int64_t d, dpad, nq;
     int k;
+    int records;  // 1: the records of slots 1.. too; 0: slot 0 only (k_pairs takes the rest)
 };
 // nt: tiles of 64 rows (1, 2 or 4; 64 nt >= k)
 hipError_t launch_seed_r(const RSeedArgs &a, int nt, hipStream_t st);

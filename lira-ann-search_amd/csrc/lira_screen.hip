@@ -2602,6 +2602,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     const bool seed_r = !fused_t && pl.rs && plive && pl.pp && qbound && o.seed && centred && idx->tstat &&
                         idx->lstat && idx->dpad <= 128;
     const bool fused = seed_r || fused_t;
+    bool seed_split = false;  // (k_seed_r without the slots 1.. records: k_pairs below)
     if (qbound && !fused) LIRA_HIP_TRY(fill32_async(qbound, ~0u, (size_t)nq * 4, st));
     if (seed_r) {
         RSeedArgs sr;
@@ -2633,6 +2634,11 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
         sr.dpad = idx->dpad;
         sr.nq = nq;
         sr.k = (int)k;
+        // (nprobe > 16, no work estimate: the other slots' records in k_pairs, 16 lanes per
+        // pair over the whole GPU -- one wave walking 31 slots four at a time was a chain
+        // of ~8 dependent pivot-row rounds per query)
+        seed_split = nprobe > 16 && !adapt;
+        sr.records = seed_split ? 0 : 1;
         const int nt_r = k > 32 ? 4 : o.seed_tiles > 0 ? o.seed_tiles : nq < 4096 ? 4 : 2;
         const hipError_t e = launch_seed_r(sr, nt_r, st);
         if (e != hipSuccess) return fail(LIRA_EHIP, std::string("k_seed_r launch: ") + hipGetErrorString(e));
@@ -2698,7 +2704,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
                                (int)k, qbound);
         LIRA_HIP_TRY(hipGetLastError());
     }
-    if (plive && !fused)
+    if (plive && (!fused || seed_split))
         LIRA_HIP_TRY(launch_pairs(q, idx->d, probe, npairs, (int)nprobe, (int)idx->n_lists, idx->pivot,
                                   idx->ipc ? 2 : centred ? 1 : 0, filter ? idx->lstat : nullptr, filter ? qbound : nullptr,
                                   plive, pl.pp ? QN : nullptr, pl.pp ? QE : nullptr, pl.pp ? pqn : nullptr, QH, idx->dpad,
