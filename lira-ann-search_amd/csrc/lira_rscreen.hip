@@ -141,11 +141,11 @@ __device__ __forceinline__ u64 rkey(float wv, float qv, uint32_t pos) {
     return ((u64)f2ord(s) << 32) | pos;
 }
 
-// Buffered survivors carry fl(dot - xadj) instead of the score: wkey = (f2ord(-wv),
-// storage position), ascending in the score for a fixed row (both metrics); converted
-// to the list key (rkey, the same arithmetic) when merged, where the row's qn / qc is
-// one broadcast read (the selection then needs no LDS read)
-__device__ __forceinline__ u64 wkey(float wv, uint32_t pos) { return ((u64)f2ord(-wv) << 32) | pos; }
+// Buffered survivors carry fl(dot - xadj) instead of the score: a wkey is
+// (f2ord(-wv), storage position), ascending in the score for a fixed row (both
+// metrics); the buffers hold its high word and the position in the item (u16),
+// and it is converted to the list key (rkey, the same arithmetic) when merged,
+// where the row's qn / qc is one broadcast read (the selection needs no LDS read)
 template <int M>
 __device__ __forceinline__ u64 wkey_to_key(u64 wk, float qv) {
     return rkey<M>(-ord2f((uint32_t)(wk >> 32)), qv, (uint32_t)wk);
