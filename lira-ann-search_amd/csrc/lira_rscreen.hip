@@ -687,6 +687,10 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void k_screen_r(RArgs a) {
             // The pass runs over (entry, half) steps h = 2 e + (i >> 1); a step that
             // would overflow the queue stops it there, the queue is drained (one
             // inlined call site) and the pass resumes at that step (rare)
+            // (MXPRE, 32-row variants: each entry first compares the max of its four
+            // slots -- one ballot instead of four on the sparse latent tiles; measured
+            // slower on the 64-row SIFT1M mixture, so not there)
+            constexpr bool MXPRE = RL >= 2;
             const uint32_t lpos0 = (uint32_t)(u * 64 + 4 * cj);
             for (int s0 = 0;;) {
                 // (the accumulators as if redefined: keeps the compares from being
@@ -706,6 +710,11 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void k_screen_r(RArgs a) {
                         const int e = 4 * rg + reg;
                         if (2 * e + 1 < s0 || 2 * e >= stop) continue;
                         const float hp = hv[rg][reg];
+                        if (MXPRE) {  // (NaN-ignoring max: a NaN slot fails its own compare either way)
+                            const float mx = fmaxf(fmaxf(acc[rg][0][reg], acc[rg][1][reg]),
+                                                   fmaxf(acc[rg][2][reg], acc[rg][3][reg]));
+                            if (!__ballot(mx >= hp)) continue;
+                        }
                         u64 m[4];
 #pragma unroll
                         for (int i = 0; i < 4; ++i) m[i] = __ballot(acc[rg][i][reg] >= hp);
