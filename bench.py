@@ -445,9 +445,11 @@ def run_workload(args, data, rank, world, gpu, dev, dist, primary):
                     "roofline -- the partition-major scan reads a candidate once per query block and "
                     "skips or screens most of them; reported for continuity only"},
         "work": {"blocks_computed": work["blocks"], "blocks_skipped": work["blocks_skipped"],
-                 "pairs_pruned_plan": work["pairs_pruned_plan"],
-                 "candidates_pruned_plan": work["candidates_pruned_plan"],
-                 "blocks_pruned_plan": work["candidates_pruned_plan"] / (qr * 256.0),
+                 # (the plan filter's counters exist only when the screened path ran alone)
+                 "pairs_pruned_plan": work.get("pairs_pruned_plan"),
+                 "candidates_pruned_plan": work.get("candidates_pruned_plan"),
+                 "blocks_pruned_plan": (work["candidates_pruned_plan"] / (qr * 256.0)
+                                        if "candidates_pruned_plan" in work else None),
                  "blocks_unit": f"tiles of 64 candidates x {qr} rows" if kname == "k_screen_r"
                  else "blocks of 256 candidates x qr rows",
                  "blocks_pruned_plan_note": "(query, candidate) pairs the plan's partition filter removed, in "

@@ -341,6 +341,22 @@ int lira_order_probes(int32_t *probe, int64_t n, int64_t max_probe, const float 
  * being captured (LIRA_EINVAL: make one eager call of the same shape before the
  * capture); a cached buffer that a captured graph uses is kept allocated when a
  * later eager call outgrows it (until lira_index_destroy), so replays stay valid.
+ *
+ * Threading and streams.  Calls are asynchronous and stream-
+ * ordered.  Several streams (and host threads) may search ONE handle at the same
+ * time: the cached workspace is kept per stream (the plan counters, item tables,
+ * row lists and bounds of one call are never shared with another stream's call),
+ * and the host-side state (workspace table, profiling events, stats flags) is
+ * guarded by a lock in the handle.  Up to 8 streams hold cached workspaces at
+ * once; a 9th takes over the buffer of a stream whose last call has completed,
+ * else the call returns LIRA_ESTATE (pass a workspace instead).  A capture on a
+ * stream that has no buffer of its own (torch.cuda.graph's side stream) uses the
+ * largest buffer an eager call sized: replay that graph on the stream whose eager
+ * calls sized it (or pass a workspace), because the two share it.  Caller-supplied
+ * workspaces are the caller's: one per concurrent call.  Not allowed concurrently
+ * with a search: add_partitions / build / set_option / destroy on the same handle.
+ * The work counters (lira_index_set_stats) and profiling sums aggregate every
+ * stream's calls; lira_index_check reads one error word per handle.
  */
 int lira_scan_workspace_size(const lira_index *idx, int64_t nq, int64_t nprobe_max, int64_t k,
                              unsigned flags, size_t *bytes);

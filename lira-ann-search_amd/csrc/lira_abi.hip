@@ -354,6 +354,7 @@ static void free_storage(lira_index *idx) {
     idx->tile_off = nullptr;
     idx->list_size = nullptr;
     idx->n_lists = idx->ntotal = idx->n_tiles = idx->max_list = idx->max_list_tiles = 0;
+    idx->ipc = false;  // (the centred IP layout went with xadjc / pivot / Xb)
     idx->h_list_size.clear();
     idx->h_tile_off.clear();
 }
@@ -362,25 +363,77 @@ int cached_workspace(lira_index_impl *idx, size_t need, hipStream_t st, void **o
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     LIRA_HIP_TRY(hipStreamIsCapturing(st, &cs));
     const bool capturing = cs == hipStreamCaptureStatusActive;
-    if (idx->ws_bytes < need) {
+    std::lock_guard<std::mutex> lock(idx->mu);
+    lira_index_impl::WsEntry *e = nullptr;
+    for (auto &x : idx->ws_list)
+        if (x.st == st) e = &x;
+    if (capturing && (!e || e->bytes < need)) {
+        // a capture on a stream of its own (torch.cuda.graph's side stream) after eager
+        // calls on another: the graph takes the largest buffer an eager call sized (it
+        // cannot allocate mid-capture); its replays then share that buffer with the eager
+        // stream's calls -- replay it on that stream, or pass a workspace
+        lira_index_impl::WsEntry *b = nullptr;
+        for (auto &x : idx->ws_list)
+            if (x.bytes >= need && (!b || x.bytes > b->bytes)) b = &x;
+        if (b) {
+            b->in_graph = true;
+            *out = b->p;
+            return LIRA_OK;
+        }
+    }
+    if (!e) {
+        if ((int)idx->ws_list.size() < lira_index_impl::kMaxWsStreams) {
+            idx->ws_list.emplace_back();
+            e = &idx->ws_list.back();
+        } else {  // hand over an idle entry: its last call completed, no graph uses it
+            for (auto &x : idx->ws_list) {
+                if (x.in_graph) continue;
+                const hipError_t q = x.done ? hipEventQuery(x.done) : hipSuccess;
+                if (q == hipSuccess) {
+                    e = &x;
+                    break;
+                }
+                if (q != hipErrorNotReady) return fail(LIRA_EHIP, std::string("hipEventQuery: ") + hipGetErrorString(q));
+            }
+            if (!e)
+                return fail(LIRA_ESTATE, "the cached scan workspace is in use on " +
+                                             std::to_string(lira_index_impl::kMaxWsStreams) +
+                                             " other streams: pass a workspace (lira_scan_workspace_size)");
+        }
+        e->st = st;
+    }
+    if (e->bytes < need) {
         if (capturing)
             return fail(LIRA_EINVAL, "the cached scan workspace must grow to " + std::to_string(need) +
                                          " bytes while the stream is being captured: make the same call once "
                                          "before the capture, or pass a workspace");
-        if (idx->ws) {
-            if (idx->ws_in_graph)
-                idx->ws_retired.push_back(idx->ws);
+        if (e->p) {
+            if (e->in_graph)
+                idx->ws_retired.push_back(e->p);
             else
-                hipFree(idx->ws);
+                hipFree(e->p);
         }
-        idx->ws = nullptr;
-        idx->ws_bytes = 0;
-        idx->ws_in_graph = false;
-        LIRA_HIP_TRY(hipMalloc(&idx->ws, need));
-        idx->ws_bytes = need;
+        e->p = nullptr;
+        e->bytes = 0;
+        e->in_graph = false;
+        LIRA_HIP_TRY(hipMalloc(&e->p, need));
+        e->bytes = need;
     }
-    if (capturing) idx->ws_in_graph = true;
-    *out = idx->ws;
+    if (capturing) e->in_graph = true;
+    *out = e->p;
+    return LIRA_OK;
+}
+
+int cached_workspace_enqueued(lira_index_impl *idx, hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    LIRA_HIP_TRY(hipStreamIsCapturing(st, &cs));
+    if (cs == hipStreamCaptureStatusActive) return LIRA_OK;  // (a graph's entry is never handed over)
+    std::lock_guard<std::mutex> lock(idx->mu);
+    for (auto &x : idx->ws_list) {
+        if (x.st != st) continue;
+        if (!x.done) LIRA_HIP_TRY(hipEventCreateWithFlags(&x.done, hipEventDisableTiming));
+        LIRA_HIP_TRY(hipEventRecord(x.done, st));
+    }
     return LIRA_OK;
 }
 
@@ -444,7 +497,10 @@ int lira_index_destroy(lira_index *idx) {
     hipDeviceSynchronize();
     free_storage(idx);
     if (idx->err) hipFree(idx->err);
-    if (idx->ws) hipFree(idx->ws);
+    for (auto &x : idx->ws_list) {
+        if (x.p) hipFree(x.p);
+        if (x.done) hipEventDestroy(x.done);
+    }
     for (void *w : idx->ws_retired) hipFree(w);
     for (hipEvent_t e : idx->ev_pool) hipEventDestroy(e);
     if (idx->stats) hipFree(idx->stats);
@@ -800,11 +856,17 @@ int lira_index_set_option(lira_index *idx, int option, int64_t value) {
             if (!in(0, 4) || v == 3) break;
             // 4 tiles exist only in the seeds fused with the per-pair records: k_seed_r
             // (k_screen_r's: L2 or centred IP, d <= 128) and k_seed_t (L2, d <= 256, fp32
-            // tiles kept); the unfused seed reads 1 or 2
-            if (v == 4 && !(idx->d <= 128 && (idx->metric == LIRA_METRIC_L2 || (o.ip_centre && o.keep_tiles))) &&
-                !(idx->metric == LIRA_METRIC_L2 && idx->d <= 256 && o.keep_tiles))
-                return fail(LIRA_EUNSUPPORTED, "LIRA_OPT_SEED_TILES 4 needs a fused seed (L2 or centred IP with "
-                                               "d <= 128, or L2 with d <= 256 and the fp32 tiles)");
+            // tiles kept); the unfused seed reads 1 or 2.  Once the index has lists the layout
+            // as built decides (idx->ipc, idx->X), before that the options that will build it
+            if (v == 4) {
+                const bool built = idx->Xr != nullptr;
+                const bool cip = built ? idx->ipc : (o.ip_centre && o.keep_tiles);
+                const bool tiles = built ? idx->X != nullptr : o.keep_tiles != 0;
+                if (!(idx->d <= 128 && (idx->metric == LIRA_METRIC_L2 || cip)) &&
+                    !(idx->metric == LIRA_METRIC_L2 && idx->d <= 256 && tiles))
+                    return fail(LIRA_EUNSUPPORTED, "LIRA_OPT_SEED_TILES 4 needs a fused seed (L2 or centred IP with "
+                                                   "d <= 128, or L2 with d <= 256 and the fp32 tiles)");
+            }
             o.seed_tiles = v;
             return LIRA_OK;
         default: return fail(LIRA_EINVAL, "unknown option " + std::to_string(option));
@@ -888,6 +950,7 @@ int lira_scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *p
 
 int lira_index_set_profiling(lira_index *idx, int enable) {
     if (!idx) return fail(LIRA_EINVAL, "index is NULL");
+    std::lock_guard<std::mutex> lock(idx->mu);
     idx->profiling = enable != 0;
     idx->ev_used = 0;
     return LIRA_OK;
@@ -908,6 +971,7 @@ int lira_index_set_stats(lira_index *idx, int enable) {
 
 int lira_index_stats_paths(const lira_index *idx, int *out) {
     if (!idx || !out) return fail(LIRA_EINVAL, "index or out is NULL");
+    std::lock_guard<std::mutex> lock(const_cast<lira_index *>(idx)->mu);
     *out = idx->stats_paths;
     return LIRA_OK;
 }
@@ -928,11 +992,13 @@ int lira_index_profile_read(lira_index *idx, double *plan_ms, double *scan_ms, d
                             int64_t *calls) {
     if (!idx) return fail(LIRA_EINVAL, "index is NULL");
     DeviceGuard g(idx->device);
+    std::lock_guard<std::mutex> lock(idx->mu);
     double sp = 0, ss = 0, sm = 0;
     const size_t n = idx->ev_used / 4;
-    if (n) LIRA_HIP_TRY(hipEventSynchronize(idx->ev_pool[idx->ev_used - 1]));
     for (size_t c = 0; c < n; ++c) {
         hipEvent_t *e = &idx->ev_pool[4 * c];
+        // (each call's own last event: calls on several streams complete in any order)
+        LIRA_HIP_TRY(hipEventSynchronize(e[3]));
         float a = 0, b = 0, m = 0;
         LIRA_HIP_TRY(hipEventElapsedTime(&a, e[0], e[1]));
         LIRA_HIP_TRY(hipEventElapsedTime(&b, e[1], e[2]));

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include <atomic>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -110,10 +111,24 @@ struct lira_index_impl {
     // x - pivot), rounded up -- the hi-only screen's error bound per block
     float *tres = nullptr;
     int32_t *err = nullptr;        // device error word
-    void *ws = nullptr;            // cached scan workspace
-    size_t ws_bytes = 0;
-    bool ws_in_graph = false;      // a stream capture recorded kernels that use ws
+    // Cached scan workspaces (workspace == NULL calls), one per stream: two streams
+    // searching one handle concurrently never share a buffer (plan counters, item
+    // tables, row lists, bounds).  At most kMaxWsStreams streams hold one at a time;
+    // an entry whose last call has completed (its `done` event) and that no captured
+    // graph uses is handed to a new stream, else the call returns LIRA_ESTATE.
+    struct WsEntry {
+        hipStream_t st = nullptr;
+        void *p = nullptr;
+        size_t bytes = 0;
+        bool in_graph = false;       // a stream capture recorded kernels that use p
+        hipEvent_t done = nullptr;   // recorded after the last eager call that used p
+    };
+    static constexpr int kMaxWsStreams = 8;
+    std::vector<WsEntry> ws_list;
     std::vector<void *> ws_retired;  // outgrown workspaces a captured graph may still use (freed at destroy)
+    // guards the host-side state that concurrent calls on one handle touch:
+    // ws_list / ws_retired, the profiling event pool and stats_paths
+    std::mutex mu;
     // profiling: 4 events per recorded call (start, after plan, after scan, after merge)
     bool profiling = false;
     std::vector<hipEvent_t> ev_pool;
@@ -126,12 +141,16 @@ struct lira_index_impl {
 
 int64_t round_up(int64_t x, int64_t m);
 
-// The handle's cached scan workspace, at least `need` bytes, for a call on `st`.
+// The handle's cached scan workspace of stream `st`, at least `need` bytes.
 // Growing it while `st` is being captured is refused (LIRA_EINVAL: the graph would
 // bake in an allocation made mid-capture); a workspace that a captured graph uses
 // is never freed when a later eager call outgrows it (retired until destroy), so a
-// replay after such a call reads valid memory.
+// replay after such a call reads valid memory.  LIRA_ESTATE when kMaxWsStreams
+// other streams hold workspaces that are still in use.
 int cached_workspace(lira_index_impl *idx, size_t need, hipStream_t st, void **out);
+// after a call's kernels that use st's cached workspace are enqueued: record its
+// `done` event (eager calls only), so the entry can pass to another stream later
+int cached_workspace_enqueued(lira_index_impl *idx, hipStream_t st);
 
 }  // namespace lira
 

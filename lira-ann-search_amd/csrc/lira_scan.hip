@@ -1270,21 +1270,34 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
                                            : "k = " + std::to_string(k) +
                                                  " needs the fp32 tiles (LIRA_OPT_KEEP_TILES) or k <= 120");
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    if (idx->profiling) {
-        while (idx->ev_pool.size() < idx->ev_used + 4) {
-            hipEvent_t e;
-            LIRA_HIP_TRY(hipEventCreate(&e));
-            idx->ev_pool.push_back(e);
+    size_t ev_slot = 0;
+    {
+        std::lock_guard<std::mutex> lock(idx->mu);
+        if (idx->profiling) {
+            while (idx->ev_pool.size() < idx->ev_used + 4) {
+                hipEvent_t e;
+                LIRA_HIP_TRY(hipEventCreate(&e));
+                idx->ev_pool.push_back(e);
+            }
+            ev_slot = idx->ev_used;
+            for (int i = 0; i < 4; ++i) ev[i] = idx->ev_pool[ev_slot + i];
+            idx->ev_used += 4;
         }
-        for (int i = 0; i < 4; ++i) ev[i] = idx->ev_pool[idx->ev_used + i];
-        idx->ev_used += 4;
+        if (idx->stats_on) idx->stats_paths |= scr ? 2 : 1;
     }
-    if (idx->stats_on) idx->stats_paths |= scr ? 2 : 1;
-    const int rc = scr ? screen_topk(idx, q, nq, probe, nprobe, k, flags, Rm, out_D, out_I, out_ncand, ws, ws_bytes,
-                                     st, ev)
-                       : exact_topk(idx, q, nq, probe, nprobe, k, flags, Rm, out_D, out_I, out_ncand, ws, ws_bytes,
-                                    st, ev);
-    if (rc != LIRA_OK && ev[0]) idx->ev_used -= 4;  // this call's events were not all recorded
+    int rc = scr ? screen_topk(idx, q, nq, probe, nprobe, k, flags, Rm, out_D, out_I, out_ncand, ws, ws_bytes, st, ev)
+                 : exact_topk(idx, q, nq, probe, nprobe, k, flags, Rm, out_D, out_I, out_ncand, ws, ws_bytes, st, ev);
+    if (rc == LIRA_OK && !ws) rc = cached_workspace_enqueued(idx, st);
+    if (rc != LIRA_OK && ev[0]) {
+        // this call's events were not all recorded: drop its slots if they are the
+        // pool's last (another stream's call may have taken later ones meanwhile),
+        // else record all four now, so the read sees a valid zero-length call
+        std::lock_guard<std::mutex> lock(idx->mu);
+        if (idx->ev_used == ev_slot + 4)
+            idx->ev_used = ev_slot;
+        else
+            for (int i = 0; i < 4; ++i) hipEventRecord(ev[i], st);
+    }
     return rc;
 }
 

@@ -60,6 +60,36 @@ def build_csr(data_2_bkt: torch.Tensor, n_bkt: int):
     return offsets.cpu().numpy(), ids, max(1, max_rep)
 
 
+def _scan_flags(dedup, per_partition, fma, prune, exact, split) -> int:
+    return (_lib.LIRA_SCAN_DEDUP if dedup else 0) | \
+        (_lib.LIRA_SCAN_PER_PARTITION if per_partition else 0) | \
+        (_lib.LIRA_SCAN_FMA if fma else 0) | \
+        (0 if prune else _lib.LIRA_SCAN_NO_PRUNE) | \
+        (_lib.LIRA_SCAN_EXACT if exact else 0) | \
+        (0 if split else _lib.LIRA_SCAN_NO_SPLIT)
+
+
+def parse_stats(v, paths: int) -> dict:
+    """The 8 work counters of lira_index_stats_read as a dict (include/lira_hip.h).
+
+    Slots [1] / [3] mean chunks_nominal / blocks_dropped on the all-exact scan
+    (paths == 1) and the plan filter's removed pairs / their (query, candidate)
+    pairs on the screened one (paths == 2); with both paths or none they are
+    summed, reported as slot1 / slot3.  Callers read the path-specific keys
+    with .get(): which ones exist depends on `paths`.
+    """
+    out = {"chunks_computed": v[0], "blocks": v[2], "blocks_skipped": v[4], "rechecked": v[5],
+           "rescans": v[6], "survivors": v[7],
+           "paths": {1: "exact", 2: "screen", 3: "exact+screen"}.get(paths, "none")}
+    if paths == 1:
+        out.update(chunks_nominal=v[1], blocks_dropped=v[3])
+    elif paths == 2:
+        out.update(pairs_pruned_plan=v[1], candidates_pruned_plan=v[3])
+    else:
+        out.update(slot1=v[1], slot3=v[3])
+    return out
+
+
 class PartitionedIndex:
     """Inverted lists of fp32 vectors on one GPU, searched by the HIP scan.
 
@@ -187,7 +217,7 @@ class PartitionedIndex:
     # --------------------------------------------------------------- search
     def search(self, q: torch.Tensor, probe: torch.Tensor, k: int, dedup: bool = True,
                per_partition: bool = False, out=None, stream=None, fma: bool = False,
-               prune: bool = True, exact: bool = False, split: bool = True):
+               prune: bool = True, exact: bool = False, split: bool = True, workspace=None):
         """Scan the probed lists of every query; exact top-k.
 
         q (nq, d) fp32, probe (nq, nprobe_max) int32 (-1 = unused slot).
@@ -205,6 +235,9 @@ class PartitionedIndex:
         dot products run as split-bf16 MFMAs (hi/lo bf16 parts, fp32
         accumulation); split=False uses the fp32 MFMA screen instead
         (LIRA_SCAN_NO_SPLIT; same results).
+        workspace: a device uint8 tensor of at least workspace_size() bytes, or
+        None for the handle's cached buffer of the current stream (lira_hip.h,
+        "Threading and streams").
         """
         q = _dev(q, torch.float32, self.device)
         probe = _dev(probe, torch.int32, self.device)
@@ -223,17 +256,23 @@ class PartitionedIndex:
             ncand = torch.empty(nq, dtype=torch.int64, device=self.device)
         else:
             D, I, ncand = out
-        flags = (_lib.LIRA_SCAN_DEDUP if dedup else 0) | \
-            (_lib.LIRA_SCAN_PER_PARTITION if per_partition else 0) | \
-            (_lib.LIRA_SCAN_FMA if fma else 0) | \
-            (0 if prune else _lib.LIRA_SCAN_NO_PRUNE) | \
-            (_lib.LIRA_SCAN_EXACT if exact else 0) | \
-            (0 if split else _lib.LIRA_SCAN_NO_SPLIT)
+        flags = _scan_flags(dedup, per_partition, fma, prune, exact, split)
+        if workspace is not None and (workspace.device != self.device or workspace.dtype != torch.uint8):
+            raise ValueError(f"workspace must be a uint8 tensor on {self.device}")
         with torch.cuda.device(self.device):
             _lib.call("lira_scan_topk", self._h, _lib.ptr(q), nq, _lib.ptr(probe), npm, int(k),
-                      flags, _lib.ptr(D), _lib.ptr(I), _lib.ptr(ncand), None, 0,
-                      _lib.stream_ptr(stream))
+                      flags, _lib.ptr(D), _lib.ptr(I), _lib.ptr(ncand),
+                      None if workspace is None else _lib.ptr(workspace),
+                      0 if workspace is None else workspace.numel(), _lib.stream_ptr(stream))
         return D, I, ncand
+
+    def workspace_size(self, nq: int, nprobe: int, k: int, dedup: bool = True, per_partition: bool = False,
+                       fma: bool = False, prune: bool = True, exact: bool = False, split: bool = True) -> int:
+        """Bytes of the caller-supplied workspace search(..., workspace=) needs for this shape."""
+        sz = ctypes.c_size_t()
+        _lib.call("lira_scan_workspace_size", self._h, int(nq), int(nprobe), int(k),
+                  _scan_flags(dedup, per_partition, fma, prune, exact, split), ctypes.byref(sz))
+        return sz.value
 
     def describe(self, nq: int, nprobe: int, k: int, dedup: bool = True, exact: bool = False) -> str:
         """The scan kernel a search of this shape runs (lira_scan_describe)."""
@@ -273,18 +312,7 @@ class PartitionedIndex:
         with torch.cuda.device(self.device):
             _lib.call("lira_index_stats_paths", self._h, ctypes.byref(paths))
             _lib.call("lira_index_stats_read", self._h, v)
-        out = {"chunks_computed": v[0], "blocks": v[2], "blocks_skipped": v[4], "rechecked": v[5],
-               "rescans": v[6], "survivors": v[7],
-               "paths": {1: "exact", 2: "screen", 3: "exact+screen"}.get(paths.value, "none")}
-        # slots [1] / [3]: chunks_nominal / blocks_dropped on the all-exact scan, the plan
-        # filter's removed pairs / their (query, candidate) pairs on the screened one
-        if paths.value == 1:
-            out.update(chunks_nominal=v[1], blocks_dropped=v[3])
-        elif paths.value == 2:
-            out.update(pairs_pruned_plan=v[1], candidates_pruned_plan=v[3])
-        else:  # (both paths, or none: the two meanings are summed)
-            out.update(slot1=v[1], slot3=v[3])
-        return out
+        return parse_stats(list(v), paths.value)
 
     def set_option(self, name: str, value) -> None:
         """Set one LIRA_OPT_* knob by name (see include/lira_hip.h)."""

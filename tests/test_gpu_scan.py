@@ -443,6 +443,11 @@ def test_options_do_not_change_results(metric):
             D0, I0, _ = run(idu, q, probe, k)
             D1, I1, _ = run(idx, q, probe, k)
             assert np.array_equal(I0, I1) and np.array_equal(bits(D0), bits(D1)), ("ip_centre", k)
+        # an index built uncentred has no fused seed, whatever ip_centre says afterwards
+        from lira_amd import LiraError
+        idu.set_option("ip_centre", 1)
+        with pytest.raises(LiraError, match="EUNSUPPORTED"):
+            idu.set_option("seed_tiles", 4)
     # the removed screen variants (k_screen_s / _w / _v, k_seed_b): 0 still reads back, others refused
     from lira_amd import LiraError
     # (4 seed tiles exist only in the fused seeds: refused where neither can run)
@@ -674,3 +679,61 @@ def test_graph_capture_workspace_growth():
                 idx2.search(qt[:200], pt[:200], 10, out=(D, I, nc))
     torch.cuda.synchronize()
     del g2
+
+
+def test_two_streams_one_handle():
+    # lira_hip.h "Threading and streams": two torch streams search ONE handle at the
+    # same time with the cached workspace (workspace = NULL); each stream gets its own
+    # buffer, so both results equal the oracle's.  Then the 8-stream cap: 8 streams
+    # whose buffers captured graphs pin, a 9th eager stream is refused (ESTATE).
+    import torch
+    from lira_amd import LiraError
+    dev = torch.device("cuda", 0)
+    x, q, d2b, probe = clustered_case(97, 30000, 64, 16, 1500, 4)
+    idx = make_index(x, d2b, 16, "L2")
+    off, ids = oracle.build_csr(d2b, 16)
+    vecs = oracle.gather_lists(x, off, ids)
+    halves = [(0, 900), (900, 1500)]  # different sizes: different plans and workspaces
+    want = [oracle.scan_topk(q[a:b], off, ids, vecs, probe[a:b], 10, oracle.L2, 1) for a, b in halves]
+    qt, pt = torch.from_numpy(q).to(dev), torch.from_numpy(probe).to(dev)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = [(torch.empty((b - a, 10), dtype=torch.float32, device=dev),
+             torch.empty((b - a, 10), dtype=torch.int64, device=dev),
+             torch.empty(b - a, dtype=torch.int64, device=dev)) for a, b in halves]
+    torch.cuda.synchronize()
+    for rep in range(4):
+        for s, (a, b), o in zip(streams, halves, outs):  # enqueued back to back, no sync between
+            with torch.cuda.stream(s):
+                o[1].fill_(-7)
+                idx.search(qt[a:b], pt[a:b], 10, out=o)
+        torch.cuda.synchronize()
+        idx.check()
+        for (Do, Io, nco), (D, I, nc) in zip(want, outs):
+            assert np.array_equal(I.cpu().numpy(), Io), rep
+            assert np.array_equal(bits(D.cpu().numpy()), bits(Do)), rep
+            assert np.array_equal(nc.cpu().numpy(), nco), rep
+    # 8 streams whose buffers are held by captured graphs: a 9th stream cannot take one
+    graphs, gs = [], [torch.cuda.Stream() for _ in range(8)]
+    D, I, nc = outs[0]
+    for s in gs:
+        with torch.cuda.stream(s):
+            idx.search(qt[:900], pt[:900], 10, out=(D, I, nc))  # sizes this stream's buffer
+            s.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                idx.search(qt[:900], pt[:900], 10, out=(D, I, nc))
+            graphs.append(g)
+    torch.cuda.synchronize()
+    s9 = torch.cuda.Stream()
+    with torch.cuda.stream(s9):
+        with pytest.raises(LiraError, match="ESTATE"):
+            idx.search(qt[:900], pt[:900], 10, out=(D, I, nc))
+        # ... while a caller-supplied workspace always works
+        ws = torch.empty(idx.workspace_size(900, 4, 10), dtype=torch.uint8, device=dev)
+        idx.search(qt[:900], pt[:900], 10, out=(D, I, nc), workspace=ws)
+    torch.cuda.synchronize()
+    assert np.array_equal(I.cpu().numpy(), want[0][1])
+    graphs[3].replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(I.cpu().numpy(), want[0][1])
+    del graphs

@@ -79,3 +79,22 @@ def test_build_csr_torch_matches_oracle():
     o_off, o_ids = oracle.build_csr(d2b, 9)
     assert np.array_equal(off, o_off) and np.array_equal(ids.numpy(), o_ids)
     assert rep == max(np.bincount(o_ids))
+
+
+@pytest.mark.parametrize("paths", [0, 1, 2, 3])
+def test_parse_stats_every_path(paths):
+    """lira_index_stats_read's slots [1] / [3] change meaning with the path that
+    ran; the path-specific keys exist only for that path (callers use .get)."""
+    from lira_amd.index import parse_stats
+    v = [10, 11, 12, 13, 14, 15, 16, 17]
+    st = parse_stats(v, paths)
+    assert (st["chunks_computed"], st["blocks"], st["blocks_skipped"]) == (10, 12, 14)
+    assert (st["rechecked"], st["rescans"], st["survivors"]) == (15, 16, 17)
+    assert st["paths"] == {0: "none", 1: "exact", 2: "screen", 3: "exact+screen"}[paths]
+    if paths == 1:
+        assert (st["chunks_nominal"], st["blocks_dropped"]) == (11, 13)
+    elif paths == 2:
+        assert (st["pairs_pruned_plan"], st["candidates_pruned_plan"]) == (11, 13)
+    else:
+        assert (st["slot1"], st["slot3"]) == (11, 13)
+        assert st.get("pairs_pruned_plan") is None  # what bench.py's work block reads
