@@ -433,11 +433,13 @@ __device__ __forceinline__ void emit_list(const u64 (&lst)[R], int k, int dedup,
 
 // ---- stream-ordered fill of 32-bit words (instead of hipMemsetAsync) ----
 // The search path's per-call resets (plan counters, flags, the seed bound) are a
-// kernel of our own: a hipMemsetAsync captured into a HIP graph replayed into an
-// illegal-address fault once the same memset had also run eagerly after the
-// capture (graph replay after an eager call of the library faulted on MI355X,
-// ROCm 7.2; replays back to back did not).  A kernel node is ordered and
-// self-contained like every other node of the step.
+// kernel of our own.  Round 4 saw a captured search step fault (illegal address)
+// when replayed after eager calls of the same search, while its resets were
+// hipMemsetAsync; since they are kernel nodes the fault has not recurred
+// (test_graph_replay_after_eager_calls).  The memset is a suspect, not a shown
+// cause: a one-memset capture / eager / replay repro does not fault, but it also
+// lacks the library's pattern (two captured fills of different value and size
+// interleaved with the plan and scan kernels on one stream) -- DESIGN.md §7.8.
 // (VEC: 16-B stores, p 16-B aligned; else one 4-B store per word, any 4-B aligned p)
 template <bool VEC>
 static __global__ __launch_bounds__(256) void k_fill32(uint32_t *p, uint32_t v, int64_t n) {
