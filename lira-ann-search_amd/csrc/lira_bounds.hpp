@@ -125,24 +125,32 @@ __device__ __forceinline__ float row_h(double lim, double qn, double qnorm, doub
 // lies below (-qc - slack - T) / ||q|| holds no candidate with exact score <= T.
 // G: lanes per pair (16; 64 for long rows, k_pairs at d > 256 -- the dims loop is
 // then a quarter as long: GIST1M's 960 dims were 60 dependent-load steps per lane)
+// pair_record in two halves, so a kernel can run the record's sums (which do not
+// depend on the seed bound) while other waves compute that bound (k_seed_w):
+// pair_sums -- the double sums of the pair's 16 (G) lanes and the QH row, every lane
+// holds the pair's totals; pair_finish -- the filter under qb and the record writes.
+struct PairSums {
+    double s, t, e;
+    float2 ts;  // (estimate) this lane's sample tile of the list
+    int lsz;    // (estimate) the list's size
+};
 template <int G = 16>
-__device__ __forceinline__ int pair_record(const float *Q, int64_t d, int64_t pair, bool valid, int praw,
-                                           int nprobe, int n_lists, const float *pivot, int centred,
-                                           const float2 *lstat, uint32_t qb, int32_t *probe_live, float4 *QN,
-                                           float *QE, float *pqn, uint16_t *QH, int64_t dpad,
-                                           const int32_t *est_size = nullptr, const float2 *est_samp = nullptr,
-                                           const float *rmx = nullptr) {
+__device__ __forceinline__ PairSums pair_sums(const float *Q, int64_t d, int64_t pair, bool valid, int praw,
+                                              int n_lists, const float *pivot, int centred, const float2 *lstat,
+                                              const float4 *QN, float *QE, uint16_t *QH, int64_t dpad,
+                                              const int32_t *est_size = nullptr, const float2 *est_samp = nullptr) {
     const bool ipm = centred == 2;
     const int sub = threadIdx.x & (G - 1);
     const int p = praw < n_lists ? praw : -1;  // (an id >= n_lists passes through: k_count reports it)
-    const int64_t q = valid ? pair / nprobe : 0;
+    (void)valid;  // (Q is the pair's query row)
+    PairSums r;
     // (estimate) this lane's sample tile of the list and the list's size, loaded ahead
     const bool est_on = est_size && p >= 0;
-    const float2 ts = est_on && sub < 16 ? est_samp[p * 16 + sub] : make_float2(0.0f, 0.0f);
-    const int lsz = est_on ? est_size[p] : 0;
+    r.ts = est_on && sub < 16 ? est_samp[p * 16 + sub] : make_float2(0.0f, 0.0f);
+    r.lsz = est_on ? est_size[p] : 0;
     double s = 0.0, t = 0.0, e = 0.0;
     if (p >= 0 && (QN || lstat)) {
-        const float *qr = Q + q * d, *pv = pivot ? pivot + (int64_t)p * d : nullptr;
+        const float *qr = Q, *pv = pivot ? pivot + (int64_t)p * d : nullptr;
         uint16_t *qh = QH ? QH + pair * dpad : nullptr;
         // (unrolled: 8 iterations' loads in flight together -- a dependent load per
         // iteration made the fused seed + pairs kernel latency-bound)
@@ -175,6 +183,22 @@ __device__ __forceinline__ int pair_record(const float *Q, int64_t d, int64_t pa
         t += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, t), m));
         e += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, e), m));
     }
+    r.s = s;
+    r.t = t;
+    r.e = e;
+    return r;
+}
+
+template <int G = 16>
+__device__ __forceinline__ int pair_finish(const PairSums &r, int64_t d, int64_t pair, bool valid, int praw,
+                                           int nprobe, int n_lists, int centred, const float2 *lstat, uint32_t qb,
+                                           int32_t *probe_live, float4 *QN, float *QE, float *pqn,
+                                           const int32_t *est_size = nullptr, const float *rmx = nullptr) {
+    const bool ipm = centred == 2;
+    const int sub = threadIdx.x & (G - 1);
+    const int p = praw < n_lists ? praw : -1;
+    const bool est_on = est_size && p >= 0;
+    const double s = r.s, t = r.t, e = r.e;
     // (the interval math runs in lane 0 of the pair only, unless the estimate needs it in all 16)
     if (!est_size && (sub != 0 || !valid)) return 0;
     int live = p;
@@ -210,10 +234,10 @@ __device__ __forceinline__ int pair_record(const float *Q, int64_t d, int64_t pa
     }
     int est = 0;
     if (est_size) {
-        const bool hit = est_on && valid && live >= 0 && sub < 16 && !(ts.y < fa || ts.x > fb);
+        const bool hit = est_on && valid && live >= 0 && sub < 16 && !(r.ts.y < fa || r.ts.x > fb);
         const unsigned long long bal = __ballot(hit);
         const int hits = __builtin_popcount((unsigned)((bal >> (threadIdx.x & (64 - G))) & 0xffffu));  // (the pair's first 16 lanes)
-        est = (int)(((int64_t)((lsz + 255) / 256) * hits) / 16);  // blocks of 4 tiles
+        est = (int)(((int64_t)((r.lsz + 255) / 256) * hits) / 16);  // blocks of 4 tiles
     }
     if (sub != 0 || !valid) return est;
     probe_live[pair] = praw >= n_lists ? praw : live;
@@ -223,6 +247,20 @@ __device__ __forceinline__ int pair_record(const float *Q, int64_t d, int64_t pa
     if (QE) QE[pair] = __double2float_ru(__builtin_sqrt(e) * (1.0 + 0x1p-40));
     if (pqn) pqn[pair] = qnu;
     return est;
+}
+
+template <int G = 16>
+__device__ __forceinline__ int pair_record(const float *Q, int64_t d, int64_t pair, bool valid, int praw,
+                                           int nprobe, int n_lists, const float *pivot, int centred,
+                                           const float2 *lstat, uint32_t qb, int32_t *probe_live, float4 *QN,
+                                           float *QE, float *pqn, uint16_t *QH, int64_t dpad,
+                                           const int32_t *est_size = nullptr, const float2 *est_samp = nullptr,
+                                           const float *rmx = nullptr) {
+    const int64_t q = valid ? pair / nprobe : 0;
+    const PairSums r = pair_sums<G>(Q + q * d, d, pair, valid, praw, n_lists, pivot, centred, lstat, QN, QE, QH,
+                                    dpad, est_size, est_samp);
+    return pair_finish<G>(r, d, pair, valid, praw, nprobe, n_lists, centred, lstat, qb, probe_live, QN, QE, pqn,
+                          est_size, rmx);
 }
 
 }  // namespace lira

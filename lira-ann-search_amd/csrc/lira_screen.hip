@@ -1682,6 +1682,129 @@ __global__ __launch_bounds__(256) void k_seed_t(const float *Q, const int32_t *p
     }
 }
 
+// k_seed_t<L2, NT, true> with all of the query's pair records in ONE round
+// (k_seed_p): G = 64 / nprobe_pow2 lanes per (query, slot) pair, each lane a
+// contiguous run of D dims (16-B loads of q and the pivot, 8-B stores of 4 bf16
+// of QH), so the nprobe pairs' loads are in flight together and the filter runs
+// in every pair's lanes at once.  k_seed_t walked the pairs 4 at a time (16 lanes
+// each, dims strided by 16): at nprobe 8 two rounds of probe -> pivot -> reduce
+// -> filter chains after the seed's own, about 35 of its 55 us per 10 k SIFT1M
+// queries (seed tiles 1 / 2 / 4: 46 / 56 / 101 us).  The records are the same
+// values as pair_record's (double sums in another order: fl() of the same exact
+// sum up to the double rounding, which the screen's error model absorbs -- the
+// results never depend on it); the seed bound is seed_bound's, bit for bit.
+template <int NT, int G>
+__global__ __launch_bounds__(256) void k_seed_p(const float *Q, const int32_t *probe, int nprobe, int n_lists,
+                                                const int32_t *tile_off, const int32_t *ids, const float *X,
+                                                int64_t d, int64_t dpad, int64_t nq, int k, uint32_t *qbound,
+                                                SeedPairs sp) {
+    static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "lanes per pair");
+    const int lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    const int slot = lane / G, sub = lane % G;
+    const bool valid = slot < nprobe;
+    const int64_t pair = q * nprobe + (valid ? slot : 0);
+    const int praw = valid ? probe[pair] : -1;
+    const int p = praw < n_lists ? praw : -1;
+    const float *qrow = Q + q * d;
+    // this lane's dims [j0, j1): D = ceil(d / G) rounded up to 4
+    const int64_t D = ((d + G - 1) / G + 3) & ~(int64_t)3;
+    const int64_t j0 = sub * D, j1 = min<int64_t>(d, j0 + D);
+    const bool est_on = sp.work && (q & 7) == 0 && p >= 0;
+    // (estimate) the 16 sample tiles of the list, 16 / G per lane
+    float2 ts[16 / G];
+#pragma unroll
+    for (int i = 0; i < 16 / G; ++i) ts[i] = est_on ? sp.lsamp[p * 16 + sub + G * i] : make_float2(0.0f, 0.0f);
+    const int lsz = est_on ? sp.list_size[p] : 0;
+    double s = 0.0, t = 0.0, e = 0.0;
+    if (p >= 0) {
+        const float *pv = sp.pivot + (int64_t)p * d;
+        uint16_t *qh = sp.QH ? sp.QH + pair * dpad : nullptr;
+        const bool cen = sp.centred == 1;
+        auto one = [&](float x, float cv, uint32_t &hb) {
+            const float sv = cen ? x - cv : x;
+            hb = bf16_rne_sat(sv);
+            const double xc = (double)sv;
+            s = __builtin_fma(xc, xc, s);
+            const double rr = (double)(sv - __uint_as_float(hb << 16));
+            e = __builtin_fma(rr, rr, e);
+            const double df = (double)x - (double)cv;
+            t = __builtin_fma(df, df, t);
+        };
+        if ((d & 3) == 0) {  // 16-B loads (rows 16-B aligned), 4 bf16 per 8-B store
+#pragma unroll 4
+            for (int64_t j = j0; j < j1; j += 4) {
+                const float4 x4 = *(const float4 *)(qrow + j), c4 = *(const float4 *)(pv + j);
+                uint32_t h0, h1, h2, h3;
+                one(x4.x, c4.x, h0);
+                one(x4.y, c4.y, h1);
+                one(x4.z, c4.z, h2);
+                one(x4.w, c4.w, h3);
+                if (qh) *(uint2 *)(qh + j) = make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
+            }
+        } else {
+            for (int64_t j = j0; j < j1; ++j) {
+                uint32_t h;
+                one(qrow[j], pv[j], h);
+                if (qh) qh[j] = (uint16_t)h;
+            }
+        }
+        if (qh) {  // zeros from d to dpad: in this lane's run, then past all G runs
+            for (int64_t j = max(d, j0); j < min(j0 + D, dpad); ++j) qh[j] = 0;
+            for (int64_t j = G * D + sub; j < dpad; j += G) qh[j] = 0;
+        }
+    }
+#pragma unroll
+    for (int m = G / 2; m >= 1; m >>= 1) {  // within the pair's lanes
+        s += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, s), m));
+        t += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, t), m));
+        e += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, e), m));
+    }
+    // the seed bound (seed_bound: the first NT tiles of slot 0's list)
+    const float B = seed_bound<LIRA_METRIC_L2, NT>(Q, probe, nprobe, n_lists, tile_off, ids, X, d, dpad, q, k);
+    const uint32_t qb = B < __builtin_inff() ? f2ord(B) : ~0u;
+    if (lane == 0) qbound[q] = qb;
+    // the filter (pair_record's triangle test), in every lane of every pair
+    int live = p;
+    const float dq = (float)__builtin_sqrt(t);
+    const double qnd = __builtin_sqrt(s);
+    float fa = -__builtin_inff(), fb = __builtin_inff();
+    if (p >= 0 && sp.lstat && slot >= 1) {
+        const double dd = (double)d, F = 1.0 - (dd + 4.0) * kU;
+        if (qb != ~0u && F > 0.5) {
+            const double T = (double)ord2f(qb);
+            if (T < 1e300) {
+                const double rad = __builtin_sqrt((fmax(T, 0.0) + dd * 0x1p-140) / F) * (1.0 + 0x1p-40);
+                double A = (double)dq * (1.0 - 0x1p-22) - rad, Bb = (double)dq * (1.0 + 0x1p-22) + rad;
+                A -= __builtin_fabs(A) * 0x1p-50;
+                Bb += __builtin_fabs(Bb) * 0x1p-50;
+                fa = __double2float_rd(A);
+                fb = __double2float_ru(Bb);
+                const float2 ls = sp.lstat[p];
+                if (ls.y < fa || ls.x > fb) live = -1;
+            }
+        }
+    }
+    if (sp.work && (q & 7) == 0) {  // the plan's work estimate (pair_record's, summed per query)
+        int hits = 0;
+#pragma unroll
+        for (int i = 0; i < 16 / G; ++i) hits += est_on && valid && live >= 0 && !(ts[i].y < fa || ts[i].x > fb);
+#pragma unroll
+        for (int m = G / 2; m >= 1; m >>= 1) hits += __shfl_xor(hits, m, 64);
+        const int est = sub == 0 ? (int)(((int64_t)((lsz + 255) / 256) * hits) / 16) : 0;
+        const int tot = (int)wave_sum_u64((u64)(uint32_t)est);
+        if (lane == 0 && tot) atomicAdd(sp.work + ((q >> 3) & 63), (unsigned)tot);
+    }
+    if (sub != 0 || !valid) return;
+    sp.probe_live[pair] = praw >= n_lists ? praw : live;
+    if (live < 0) return;
+    const float qnu = __double2float_ru(qnd * (1.0 + 0x1p-40));
+    if (sp.QN) sp.QN[pair] = make_float4((float)s, qnu, __int_as_float((int)pair), dq);
+    if (sp.QE) sp.QE[pair] = __double2float_ru(__builtin_sqrt(e) * (1.0 + 0x1p-40));
+    if (sp.pqn) sp.pqn[pair] = qnu;
+}
+
 // One workgroup per query, wave w = tile w of its first probed partition.  The
 // tile's 64 rows (contiguous in the row-major copy) are read 32 dims at a time,
 // coalesced (lane l loads 16-B pieces of rows l/8 + 8 i), transposed through a
@@ -2660,18 +2783,45 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
         // (256 seed rows below 4096 queries: 1 250-query step scan 0.136 -> 0.123 ms for
         // +0.008 ms of seed; at 10 k queries the seed's +0.043 ms outweighs the scan's gain)
         const int nt_f = o.seed_tiles > 0 ? o.seed_tiles : nq < 4096 ? 4 : 2;
-        if (nt_f == 4)
-            hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2, 4, true>), dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, q,
-                               probe, (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad,
-                               nq, (int)k, qbound, sp);
-        else if (nt_f == 1)
-            hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2, 1, true>), dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, q,
-                               probe, (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad,
-                               nq, (int)k, qbound, sp);
-        else
-            hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2, 2, true>), dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, q,
-                               probe, (int)nprobe, (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad,
-                               nq, (int)k, qbound, sp);
+        // every pair record in one round (k_seed_p, nprobe <= 64): G lanes per pair
+        // (k_count's atomics moved into it -- each live pair ranked by an atomic on its
+        // partition's counter -- measured 49 -> 70 us: same-address atomics serialise)
+        const int gp = nprobe <= 4 ? 16 : nprobe <= 8 ? 8 : nprobe <= 16 ? 4 : nprobe <= 32 ? 2 : 1;
+        const dim3 g4((unsigned)((nq + 3) / 4));
+        if (nprobe <= 64 && sp.pivot) {
+#define LIRA_SEED_P(NTV, GV)                                                                                    \
+    hipLaunchKernelGGL((k_seed_p<NTV, GV>), g4, dim3(256), 0, st, q, probe, (int)nprobe, (int)idx->n_lists,     \
+                       idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound, sp)
+#define LIRA_SEED_PG(NTV)                                                                                       \
+    switch (gp) {                                                                                               \
+        case 16: LIRA_SEED_P(NTV, 16); break;                                                                   \
+        case 8: LIRA_SEED_P(NTV, 8); break;                                                                     \
+        case 4: LIRA_SEED_P(NTV, 4); break;                                                                     \
+        case 2: LIRA_SEED_P(NTV, 2); break;                                                                     \
+        default: LIRA_SEED_P(NTV, 1); break;                                                                    \
+    }
+            if (nt_f == 4) {
+                LIRA_SEED_PG(4)
+            } else if (nt_f == 1) {
+                LIRA_SEED_PG(1)
+            } else {
+                LIRA_SEED_PG(2)
+            }
+#undef LIRA_SEED_PG
+#undef LIRA_SEED_P
+        } else if (nt_f == 4) {
+            hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2, 4, true>), g4, dim3(256), 0, st, q, probe, (int)nprobe,
+                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k,
+                               qbound, sp);
+        } else if (nt_f == 1) {
+            hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2, 1, true>), g4, dim3(256), 0, st, q, probe, (int)nprobe,
+                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k,
+                               qbound, sp);
+        } else {
+            hipLaunchKernelGGL((k_seed_t<LIRA_METRIC_L2, 2, true>), g4, dim3(256), 0, st, q, probe, (int)nprobe,
+                               (int)idx->n_lists, idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k,
+                               qbound, sp);
+        }
         LIRA_HIP_TRY(hipGetLastError());
     } else if (qbound && o.seed && idx->X) {  // from the fp32 tiles (coalesced)
         const dim3 g((unsigned)((nq + 3) / 4));
