@@ -66,11 +66,17 @@ struct RSmem {
     // keys, scan 2.82 -> 2.17 ms); 6 bytes a key: its high word and its position in
     // the item (the list key is rebuilt when merged)
     static constexpr int BC = W == 8 ? 8 : RL == 1 ? 21 : 32;  // (<= 32: a flush merges one key per half-wave lane)
+    // buffer strides in entries: odd per row (BCS) and per wave (WS = 1 mod 32), so the
+    // lanes of a drain round that write the same slot of different rows, and the
+    // epilogue's reads of the same slot of different waves' buffers, fall on
+    // different banks (a 32-entry row stride put every row's slot s on one bank)
+    static constexpr int BCS = BC | 1;
+    static constexpr int WS = QR * BCS + ((1 - QR * BCS) & 31);
     static constexpr int aq = 0;                                   // [4 chunks][NRG][64 lanes] 16 B: A operands
     static constexpr int lists = aq + 4 * NRG * 64 * 16;           // [QR][K2] u64
-    static constexpr int bufs = lists + QR * K2 * 8;               // [W][QR][BC] u32: wkey high words
-    static constexpr int bufl = bufs + W * QR * BC * 4;            // [W][QR][BC] u16: positions in the item
-    static constexpr int bufc = bufl + W * QR * BC * 2;            // [W][64] int (lane = row)
+    static constexpr int bufs = lists + QR * K2 * 8;               // [W][WS] u32: [row][BCS] wkey high words
+    static constexpr int bufl = bufs + W * WS * 4;                 // [W][WS] u16: positions in the item
+    static constexpr int bufc = (bufl + W * WS * 2 + 15) & ~15;    // [W][64] int (lane = row)
     static constexpr int hs = bufc + W * 64 * 4;                   // [W][64] float: the wave's thresholds
     static constexpr int tst = hs + W * 64 * 4;                    // [512] float2: tile radius ranges
     static constexpr int trs = tst + kRMaxTiles * 8;               // [512] float: tile hi residuals
@@ -222,7 +228,7 @@ __device__ __forceinline__ void spill_evicted(const RArgs &a, u64 ev, bool hv, u
 // list's k-th key, then the bound: program order in both), half-wave merges,
 // publish the query's bound where a list's k-th improved.  One row per half: a
 // single-row merge left half of the wave idle in every flush.
-template <int M, int RL, int BC>
+template <int M, int RL, int BC, int BCS = BC | 1>
 __device__ __forceinline__ void flush_rows(u64 *lists, u64 *kth_s, const uint32_t *mbh, const uint16_t *mbl,
                                            uint32_t pos_base, int *lock_s, uint32_t *erun_s, uint32_t *opub_s,
                                            const int *pair_s, int row0, int row1, int ew0, int ew1, int k,
@@ -243,7 +249,7 @@ __device__ __forceinline__ void flush_rows(u64 *lists, u64 *kth_s, const uint32_
     u64 lst[RL];
 #pragma unroll
     for (int r = 0; r < RL; ++r) lst[r] = lists[row * K2 + r * 32 + hl];
-    const u64 b = act && hl < BC ? wkey_to_key<M>(((u64)mbh[row * BC + hl] << 32) | (pos_base + mbl[row * BC + hl]),
+    const u64 b = act && hl < BC ? wkey_to_key<M>(((u64)mbh[row * BCS + hl] << 32) | (pos_base + mbl[row * BCS + hl]),
                                        rec_s[row].x)
                       : kEmptyKey;
     u64 ev = kEmptyKey;
@@ -279,7 +285,7 @@ __device__ __forceinline__ void flush_rows(u64 *lists, u64 *kth_s, const uint32_
 // Merge this wave's full row buffers into the lists, then move the survivor
 // queue into the buffers (LDS atomic slots), merging every buffer that fills,
 // until the queue is empty.
-template <int M, int RL, int BC>
+template <int M, int RL, int BC, int BCS = BC | 1>
 __device__ __forceinline__ void drain_buffers(u64 *lists, u64 *kth_s, uint32_t *mbh, uint16_t *mbl, int *mybufc, int *lock_s,
                                               uint32_t *erun_s, uint32_t *opub_s, const int *pair_s,
                                               const float4 *rec_s, const u64 *oq_key, uint32_t pos_base, int nq,
@@ -316,8 +322,8 @@ __device__ __forceinline__ void drain_buffers(u64 *lists, u64 *kth_s, uint32_t *
             if (pend) {
                 const int slot = atomicAdd(mybufc + row, 1);
                 if (slot < BC) {
-                    mbh[row * BC + slot] = kh;
-                    mbl[row * BC + slot] = (uint16_t)(q & 0xffffu);
+                    mbh[row * BCS + slot] = kh;
+                    mbl[row * BCS + slot] = (uint16_t)(q & 0xffffu);
                     pend = false;
                 }
             }
@@ -358,8 +364,8 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void k_screen_r(RArgs a) {
     const int g = lane >> 4, cj = lane & 15;
     const int k = a.k;
     const float dp = (float)a.dpad, dd = (float)a.d;
-    uint32_t *mybuf = bufs + wave * QR * BC;
-    uint16_t *mybufl = bufl + wave * QR * BC;
+    uint32_t *mybuf = bufs + wave * S::WS;
+    uint16_t *mybufl = bufl + wave * S::WS;
     int *mybufc = bufc + wave * 64;
     float *myh = hs + wave * 64;
     u64 *oq_key = (u64 *)(smem + S::oqk) + wave * kROCap;
@@ -771,7 +777,7 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void k_screen_r(RArgs a) {
                 if (e < n) {
                     int w = 0, off = e;  // (the wave buffer holding key e of the row's concatenation)
                     while (off >= bufc[w * 64 + row]) off -= bufc[w++ * 64 + row];
-                    const int e2 = (w * QR + row) * BC + off;
+                    const int e2 = w * S::WS + row * S::BCS + off;
                     b = wkey_to_key<M>(((u64)bufs[e2] << 32) | ((uint32_t)tbase * 64u + bufl[e2]), qv_r);
                 }
                 u64 lst[RL];
