@@ -340,10 +340,22 @@ __global__ __launch_bounds__(1024) void k_plan_fill(const int32_t *probe, int64_
                                                     int bpc_near, int qr, int32_t *qoff, int32_t *item_off,
                                                     int32_t *nch, int32_t *head, int32_t *qblk_off, int4 *itab,
                                                     int32_t *cursor, int32_t *qlist, int bpc_near_min,
-                                                    int workers, int near_div, int near0) {
+                                                    int workers, int near_div, int near0, const int32_t *cnt8) {
     __shared__ int32_t sq[kFuseMax], hist[kFuseMax], base[kFuseMax], scan[1024];
     __shared__ int32_t carry;
     const int n_virt = groups * n_lists, tid = threadIdx.x;
+    if (cnt8) {  // (the seed's per-XCD counts: every block sums them into base[]; block 0
+                 // also writes cnt, which its plan and the screen read)
+        for (int v = tid; v < n_virt; v += 1024) {
+            int c = 0;
+#pragma unroll
+            for (int x = 0; x < 8; ++x) c += cnt8[x * n_virt + v];
+            base[v] = c;
+            if (blockIdx.x == 0) ((int32_t *)cnt)[v] = c;
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
     if (blockIdx.x == 0)
         plan_body(cnt, tile_off, n_lists, n_virt, bpc, bpc_near, qr, qoff, item_off, nch, head, qblk_off, itab,
                   bpc_near_min, workers, near_div, near0);
@@ -352,7 +364,7 @@ __global__ __launch_bounds__(1024) void k_plan_fill(const int32_t *probe, int64_
     for (int b = tid; b < n_virt; b += 1024) hist[b] = 0;
     __syncthreads();
     for (int b0 = 0; b0 < n_virt; b0 += 1024) {
-        const int v = b0 + tid < n_virt ? cnt[b0 + tid] : 0;
+        const int v = b0 + tid < n_virt ? (cnt8 ? base[b0 + tid] : cnt[b0 + tid]) : 0;
         scan[tid] = v;
         __syncthreads();
         for (int off = 1; off < 1024; off <<= 1) {
@@ -1309,16 +1321,20 @@ int scan_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *probe,
 hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npairs, int nprobe, int bpc,
                        int bpc_near, int qr, int groups, int32_t *cnt, int32_t *cursor, int32_t *qoff, int32_t *item_off,
                        int32_t *nch, int32_t *head, int32_t *qlist, int32_t *qblk_off, int4 *itab,
-                       hipStream_t st, int bpc_near_min, int workers, int near_div, int near0) {
+                       hipStream_t st, int bpc_near_min, int workers, int near_div, int near0,
+                       const int32_t *cnt8) {
     const int nl = (int)idx->n_lists, nv = groups * nl;
     const unsigned pg = (unsigned)((npairs + kPairsPerBlock - 1) / kPairsPerBlock);
     const size_t hc = nv <= kHistMax ? (size_t)nv * 4 : 0;
     const size_t hf = nv <= kHistMax / 2 ? (size_t)nv * 8 : 0;
-    hipLaunchKernelGGL(k_count, dim3(pg), dim3(256), hc, st, probe, npairs, nl, nprobe, 1, groups, cnt, idx->err);
+    // (cnt8: the seed already counted every live pair, per XCD -- k_seed_p; the fused
+    // plan sums the 8 replicas into cnt)
+    const bool counted = cnt8 && nv <= kFuseMax && qblk_off;
+    if (!counted) hipLaunchKernelGGL(k_count, dim3(pg), dim3(256), hc, st, probe, npairs, nl, nprobe, 1, groups, cnt, idx->err);
     if (nv <= kFuseMax && qblk_off) {
         hipLaunchKernelGGL(k_plan_fill, dim3(std::max(pg, 1u)), dim3(1024), 0, st, probe, npairs, nl, nprobe, groups, cnt,
                            idx->tile_off, bpc, bpc_near, qr, qoff, item_off, nch, head, qblk_off, itab, cursor, qlist,
-                           bpc_near_min, workers, near_div, near0);
+                           bpc_near_min, workers, near_div, near0, counted ? cnt8 : nullptr);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, cnt, idx->tile_off, nl, nv, bpc, bpc_near, qr, qoff,

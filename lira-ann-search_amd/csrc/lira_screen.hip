@@ -60,7 +60,8 @@ hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npai
                        int bpc_near,
                        int qr, int groups, int32_t *cnt, int32_t *cursor, int32_t *qoff, int32_t *item_off,
                        int32_t *nch, int32_t *head, int32_t *qlist, int32_t *qblk_off, int4 *itab,
-                       hipStream_t st, int bpc_near_min, int workers, int near_div, int near0);
+                       hipStream_t st, int bpc_near_min, int workers, int near_div, int near0,
+                       const int32_t *cnt8 = nullptr);
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -1647,6 +1648,15 @@ struct SeedPairs {
     const int32_t *list_size;  // (non-null) estimate the blocks each pair will screen (pair_record,
     const float2 *lsamp;       //   from lira_index::lsamp) on every 8th query, summed into
     unsigned int *work;        //   work[(q / 8) % 64] (the plan adds the 64 up and scales by 8)
+    // (k_seed_p, non-null cnt) k_count's counts: every live pair adds 1 to its virtual
+    // partition's counter (groups == 2: slot 0 -> p, else n_lists + p) in its XCD's
+    // replica cnt[xcd * nv + v] (device-scope atomics on one address serialise: one
+    // counter per partition cost the 10 k-query seed 19 us), no rank taken; k_plan_fill
+    // sums the replicas; a probe id >= n_lists sets err
+    int32_t *cnt = nullptr;
+    int nv = 0;
+    int32_t *err = nullptr;
+    int groups = 1;
 };
 template <int METRIC, int NT = kSeedTiles, bool PAIRS = false>
 __global__ __launch_bounds__(256) void k_seed_t(const float *Q, const int32_t *probe, int nprobe, int n_lists,
@@ -1798,6 +1808,10 @@ __global__ __launch_bounds__(256) void k_seed_p(const float *Q, const int32_t *p
     }
     if (sub != 0 || !valid) return;
     sp.probe_live[pair] = praw >= n_lists ? praw : live;
+    if (sp.cnt) {
+        if (praw >= n_lists) atomicOr(sp.err, 1);
+        if (live >= 0) atomicAdd(sp.cnt + xcd_id() * sp.nv + (sp.groups == 2 && slot >= 1 ? n_lists + live : live), 1);
+    }
     if (live < 0) return;
     const float qnu = __double2float_ru(qnd * (1.0 + 0x1p-40));
     if (sp.QN) sp.QN[pair] = make_float4((float)s, qnu, __int_as_float((int)pair), dq);
@@ -2329,7 +2343,7 @@ struct SPlan {
     int64_t max_qblk = 0;
     size_t off_rst, off_rq, off_rbuf, off_scnt, off_spill;
     size_t off_cnt, off_cursor, off_head, off_done, off_qoff, off_item, off_nch, off_qblk, off_itab, off_qlist, off_qt, off_qn,
-        off_partial, off_qbound, off_pqn, off_pe, off_qe, off_live, total;
+        off_partial, off_qbound, off_pqn, off_pe, off_qe, off_live, off_cnt8, total;
 };
 
 static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64_t k, unsigned flags) {
@@ -2512,6 +2526,7 @@ static SPlan make_splan(const lira_index *idx, int64_t nq, int64_t nprobe, int64
     };
     const size_t nl = 2 * (size_t)idx->n_lists;  // up to two groups of virtual partitions
     pl.off_cnt = take(nl * 4);
+    pl.off_cnt8 = take(8 * nl * 4);  // (k_seed_p) per-XCD replicas of cnt, summed by k_plan_fill
     pl.off_cursor = take(nl * 4);
     pl.off_head = take(128 * 4);  // [0..1] totals, [2..9] XCD queue counters, [10..18] queue bounds,
                                   // [19] group 0's chunk size, [20] the most chunks of a bucket,
@@ -2726,6 +2741,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
                         idx->lstat && idx->dpad <= 128;
     const bool fused = seed_r || fused_t;
     bool seed_split = false;  // (k_seed_r without the slots 1.. records: k_pairs below)
+    bool seed_counted = false;  // (k_seed_p counted the live pairs: no k_count)
     if (qbound && !fused) LIRA_HIP_TRY(fill32_async(qbound, ~0u, (size_t)nq * 4, st));
     if (seed_r) {
         RSeedArgs sr;
@@ -2789,6 +2805,11 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
         const int gp = nprobe <= 4 ? 16 : nprobe <= 8 ? 8 : nprobe <= 16 ? 4 : nprobe <= 32 ? 2 : 1;
         const dim3 g4((unsigned)((nq + 3) / 4));
         if (nprobe <= 64 && sp.pivot) {
+            sp.cnt = (int32_t *)(w + pl.off_cnt8);
+            sp.nv = groups * (int)idx->n_lists;
+            sp.err = idx->err;
+            sp.groups = groups;
+            seed_counted = true;
 #define LIRA_SEED_P(NTV, GV)                                                                                    \
     hipLaunchKernelGGL((k_seed_p<NTV, GV>), g4, dim3(256), 0, st, q, probe, (int)nprobe, (int)idx->n_lists,     \
                        idx->tile_off, idx->ids, idx->X, idx->d, idx->dpad, nq, (int)k, qbound, sp)
@@ -2864,7 +2885,7 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
     LIRA_HIP_TRY(launch_plan(idx, pprobe, npairs, (int)nprobe, pl.bpc, groups == 2 ? pl.bpc_near : pl.bpc, pl.qr, groups, cnt, cursor, qoff, item_off,
                              nch, head, qlist, qblk, itab, st,
                              groups == 2 && fused && idx->lsamp ? pl.bpc_near_min : (groups == 2 ? pl.bpc_near : pl.bpc),
-                             pl.workers, pl.rs ? 2 : 4, groups == 2 ? pl.near0 : 0));
+                             pl.workers, pl.rs ? 2 : 4, groups == 2 ? pl.near0 : 0, seed_counted ? (int32_t *)(w + pl.off_cnt8) : nullptr));
     if (!pl.pp) {
     const dim3 qgrid((unsigned)pl.max_qblk, (unsigned)((idx->dpad + 64 * kQSlabs - 1) / (64 * kQSlabs)));
     if (pl.qr == 128 && pl.split)
