@@ -366,6 +366,41 @@ __device__ __forceinline__ int row16_total(int inc) {
     const int g = (int)(threadIdx.x & 63) >> 4;
     return g == 0 ? t0 : g == 1 ? t1 : g == 2 ? t2 : t3;
 }
+// Inclusive prefix sum over the wave: the rows' DPP scans plus the earlier rows' totals
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    v = row16_incl_scan(v);
+    const int t0 = __builtin_amdgcn_readlane(v, 15), t1 = __builtin_amdgcn_readlane(v, 31);
+    const int t2 = __builtin_amdgcn_readlane(v, 47);
+    const int g = (int)(threadIdx.x & 63) >> 4;
+    return v + (g > 0 ? t0 : 0) + (g > 1 ? t1 : 0) + (g > 2 ? t2 : 0);
+}
+// Inclusive prefix sums of N values per thread over a workgroup of NW waves (one
+// call site per workgroup, every thread): wave scans, the waves' totals through
+// LDS (ws: N x NW ints), two barriers -- a Hillis-Steele scan over 1024 threads
+// took 10 steps of two barriers each.  tot[i]: the workgroup's total of value i.
+template <int N, int NW>
+__device__ __forceinline__ void block_incl_scan(int (&v)[N], int (&tot)[N], int *ws) {
+    const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = wave_incl_scan(v[i]);
+    __syncthreads();  // (ws may still be read by a previous call)
+    if (lane == 63)
+#pragma unroll
+        for (int i = 0; i < N; ++i) ws[i * NW + w] = v[i];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        int off = 0, t = 0;
+#pragma unroll
+        for (int j = 0; j < NW; ++j) {
+            const int x = ws[i * NW + j];
+            off += j < w ? x : 0;
+            t += x;
+        }
+        v[i] += off;
+        tot[i] = t;
+    }
+}
 // ---- per-query merge helpers (k_merge, k_smerge) ----
 __device__ __forceinline__ void emit_key(u64 key, int metric, float *D, int64_t *I) {
     if (key == kEmptyKey) {

@@ -125,24 +125,23 @@ __device__ __forceinline__ void plan_body(const int32_t *cnt, const int32_t *til
                                           int bpc, int bpc_near, int qr, int32_t *qoff, int32_t *item_off,
                                           int32_t *nch, int32_t *head, int32_t *qblk_off, int4 *itab,
                                           int bpc_near_min, int workers, int near_div, int near0) {
+    // (scans: wave DPP scans + one LDS exchange, block_incl_scan; the carries between
+    // 1024-wide passes are workgroup-uniform registers)
     __shared__ int32_t s_a[1024], s_b[1024], s_c[1024];
-    __shared__ int32_t carry_a, carry_b, carry_c, s_nchmax;
-    if (threadIdx.x == 0) carry_a = carry_b = carry_c = s_nchmax = 0;
+    __shared__ int32_t s_ws[3 * 16], s_nchmax, s_bpc;
+    if (threadIdx.x == 0) s_nchmax = 0;
     if (bpc_near_min < bpc_near && n_virt > n_lists) {
         unsigned long long w = threadIdx.x < 64 ? (unsigned)head[64 + threadIdx.x] : 0u;
         if (threadIdx.x < 64) {
 #pragma unroll
             for (int m = 32; m >= 1; m >>= 1) w += shfl_xor64(w, m);
         }
-        s_a[0] = 0;  // (scratch: overwritten by the scans below)
-        __syncthreads();
         if (threadIdx.x == 0) {
             const long long per = (long long)(8ull * w / (unsigned long long)max(1, qr)) / max(1, workers);  // (1/8 sampled)
-            s_a[0] = (int)min<long long>(bpc_near, max<long long>(bpc_near_min, (per + near_div - 1) / near_div));
+            s_bpc = (int)min<long long>(bpc_near, max<long long>(bpc_near_min, (per + near_div - 1) / near_div));
         }
         __syncthreads();
-        bpc_near = s_a[0];
-        __syncthreads();
+        bpc_near = s_bpc;
     }
     // near0 > 0 (two groups): group 0's first chunk is near0 blocks, the rest
     // bpc_near; head[21] = the first chunk's size (= bpc_near when uniform)
@@ -150,10 +149,10 @@ __device__ __forceinline__ void plan_body(const int32_t *cnt, const int32_t *til
         head[19] = bpc_near;
         head[21] = near0 > 0 && n_virt > n_lists ? near0 : bpc_near;
     }
-    __syncthreads();
+    int carry_a = 0, carry_b = 0, carry_c = 0;
     for (int base = 0; base < n_virt; base += 1024) {
         int p = base + threadIdx.x;
-        int c = 0, items = 0, nqb = 0;
+        int c = 0, items = 0, nqb = 0, nc = 0;
         if (p < n_virt) {
             c = cnt[p];
             const int pp = p >= n_lists ? p - n_lists : p;
@@ -161,41 +160,26 @@ __device__ __forceinline__ void plan_body(const int32_t *cnt, const int32_t *til
             int nblk = (ntl + kBlockTiles - 1) / kBlockTiles;
             const bool g0 = n_virt > n_lists && p < n_lists;
             const int b = g0 ? bpc_near : bpc;  // group 0: bpc_near
-            int nc = (nblk + b - 1) / b;
+            nc = (nblk + b - 1) / b;
             if (g0 && near0 > 0) nc = nblk <= 0 ? 0 : nblk <= near0 ? 1 : 1 + (nblk - near0 + bpc_near - 1) / bpc_near;
             nch[p] = nc;
             nqb = (c + qr - 1) / qr;
             items = nqb * nc;
         }
-        s_a[threadIdx.x] = c;
-        s_b[threadIdx.x] = items;
-        s_c[threadIdx.x] = nqb;
-        __syncthreads();
-        for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
-            int va = threadIdx.x >= off ? s_a[threadIdx.x - off] : 0;
-            int vb = threadIdx.x >= off ? s_b[threadIdx.x - off] : 0;
-            int vc = threadIdx.x >= off ? s_c[threadIdx.x - off] : 0;
-            __syncthreads();
-            s_a[threadIdx.x] += va;
-            s_b[threadIdx.x] += vb;
-            s_c[threadIdx.x] += vc;
-            __syncthreads();
-        }
-        if (p < n_virt && nch[p] > 0) atomicMax(&s_nchmax, nch[p]);  // (the merge's chunk slots per bucket)
+        int v3[3] = {c, items, nqb}, t3[3];
+        block_incl_scan<3, 16>(v3, t3, s_ws);
+        if (p < n_virt && nc > 0) atomicMax(&s_nchmax, nc);  // (the merge's chunk slots per bucket)
         if (p < n_virt) {
-            qoff[p] = carry_a + s_a[threadIdx.x] - c;
-            item_off[p] = carry_b + s_b[threadIdx.x] - items;
-            if (qblk_off) qblk_off[p] = carry_c + s_c[threadIdx.x] - nqb;
+            qoff[p] = carry_a + v3[0] - c;
+            item_off[p] = carry_b + v3[1] - items;
+            if (qblk_off) qblk_off[p] = carry_c + v3[2] - nqb;
             // (the item table is written below, in queue order)
         }
-        __syncthreads();
-        if (threadIdx.x == 1023) {
-            carry_a += s_a[1023];
-            carry_b += s_b[1023];
-            carry_c += s_c[1023];
-        }
-        __syncthreads();
+        carry_a += t3[0];
+        carry_b += t3[1];
+        carry_c += t3[2];
     }
+    __syncthreads();
     if (threadIdx.x == 0) {
         head[20] = s_nchmax;
         qoff[n_virt] = carry_a;
@@ -226,12 +210,10 @@ __device__ __forceinline__ void plan_body(const int32_t *cnt, const int32_t *til
     // Slots per queue: m0 chunk-0 slots, then m partition slots; s_d = the
     // slot's first chunk.
     __shared__ int32_t s_g[1024], s_d[1024];
-    __syncthreads();
     const int m = (n_virt + 7) / 8;
     const bool two = n_virt > n_lists;
     const int m0 = two && near0 > 0 ? (n_lists + 7) / 8 : 0, M = m0 + m;  // (k_screen_r's plans only)
-    if (threadIdx.x == 0) carry_b = 0;
-    __syncthreads();
+    carry_b = 0;
     for (int base = 0; base < 8 * M; base += 1024) {
         const int vv = base + threadIdx.x;
         const int r = vv / M, j = vv % M;
@@ -246,21 +228,17 @@ __device__ __forceinline__ void plan_body(const int32_t *cnt, const int32_t *til
             items = first ? (nc > 0 ? nqb : 0) : g0 ? nqb * max(0, nc - 1) : nqb * nc;
             c0 = !first && g0 ? 1 : 0;
         }
-        s_b[threadIdx.x] = items;
+        int v1[1] = {items}, t1[1];
+        block_incl_scan<1, 16>(v1, t1, s_ws);
+        s_b[threadIdx.x] = v1[0];
         s_a[threadIdx.x] = v;
         s_c[threadIdx.x] = nqb;
         s_d[threadIdx.x] = c0;
         s_g[threadIdx.x] = v < n_virt ? qblk_off[v] : 0;
         __syncthreads();
-        for (int off = 1; off < 1024; off <<= 1) {
-            int vb = threadIdx.x >= off ? s_b[threadIdx.x - off] : 0;
-            __syncthreads();
-            s_b[threadIdx.x] += vb;
-            __syncthreads();
-        }
-        const int i0 = carry_b + s_b[threadIdx.x] - items;
+        const int i0 = carry_b + v1[0] - items;
         if (vv < 8 * M && j == 0) head[10 + r] = i0;
-        const int total = s_b[1023];
+        const int total = t1[0];
         for (int i = threadIdx.x; i < total; i += 1024) {
             int lo = 0, hi = 1023;  // first slot whose inclusive prefix exceeds i
             while (lo < hi) {
@@ -271,9 +249,8 @@ __device__ __forceinline__ void plan_body(const int32_t *cnt, const int32_t *til
             const int cl = local / nq_b, qb = local - cl * nq_b;
             itab[carry_b + i] = make_int4(s_a[lo], qb, s_d[lo] + cl, s_g[lo] + qb);
         }
-        __syncthreads();
-        if (threadIdx.x == 1023) carry_b += s_b[1023];
-        __syncthreads();
+        carry_b += total;
+        __syncthreads();  // (s_* reused by the next pass)
     }
     if (threadIdx.x == 0) head[18] = carry_b;
 }
@@ -341,9 +318,10 @@ __global__ __launch_bounds__(1024) void k_plan_fill(const int32_t *probe, int64_
                                                     int32_t *nch, int32_t *head, int32_t *qblk_off, int4 *itab,
                                                     int32_t *cursor, int32_t *qlist, int bpc_near_min,
                                                     int workers, int near_div, int near0, const int32_t *cnt8) {
-    __shared__ int32_t sq[kFuseMax], hist[kFuseMax], base[kFuseMax], scan[1024];
-    __shared__ int32_t carry;
+    __shared__ int32_t sq[kFuseMax], hist[kFuseMax], base[kFuseMax], ws[16];
     const int n_virt = groups * n_lists, tid = threadIdx.x;
+    // block 0 plans (the item table is the screen's critical path: it does nothing
+    // else), blocks 1.. fill their slices of the pairs
     if (cnt8) {  // (the seed's per-XCD counts: every block sums them into base[]; block 0
                  // also writes cnt, which its plan and the screen read)
         for (int v = tid; v < n_virt; v += 1024) {
@@ -356,30 +334,24 @@ __global__ __launch_bounds__(1024) void k_plan_fill(const int32_t *probe, int64_
         __threadfence_block();
         __syncthreads();
     }
-    if (blockIdx.x == 0)
+    if (blockIdx.x == 0) {
         plan_body(cnt, tile_off, n_lists, n_virt, bpc, bpc_near, qr, qoff, item_off, nch, head, qblk_off, itab,
                   bpc_near_min, workers, near_div, near0);
+        return;
+    }
     // exclusive prefix of cnt over the virtual partitions -> sq
-    if (tid == 0) carry = 0;
-    for (int b = tid; b < n_virt; b += 1024) hist[b] = 0;
-    __syncthreads();
+    int carry = 0;
     for (int b0 = 0; b0 < n_virt; b0 += 1024) {
         const int v = b0 + tid < n_virt ? (cnt8 ? base[b0 + tid] : cnt[b0 + tid]) : 0;
-        scan[tid] = v;
-        __syncthreads();
-        for (int off = 1; off < 1024; off <<= 1) {
-            const int o = tid >= off ? scan[tid - off] : 0;
-            __syncthreads();
-            scan[tid] += o;
-            __syncthreads();
-        }
-        if (b0 + tid < n_virt) sq[b0 + tid] = carry + scan[tid] - v;
-        __syncthreads();
-        if (tid == 1023) carry += scan[1023];
-        __syncthreads();
+        int x[1] = {v}, t[1];
+        block_incl_scan<1, 16>(x, t, ws);
+        if (b0 + tid < n_virt) sq[b0 + tid] = carry + x[0] - v;
+        carry += t[0];
     }
+    for (int b = tid; b < n_virt; b += 1024) hist[b] = 0;
+    __syncthreads();
     // k_fill with the local offsets
-    const int64_t s = (int64_t)blockIdx.x * kPairsPerBlock;
+    const int64_t s = (int64_t)(blockIdx.x - 1) * kPairsPerBlock;
     const int64_t e = min<int64_t>(npairs, s + kPairsPerBlock);
     for (int64_t i = s + tid; i < e; i += 1024) {
         const int p = probe[i];
@@ -1332,7 +1304,7 @@ hipError_t launch_plan(const lira_index *idx, const int32_t *probe, int64_t npai
     const bool counted = cnt8 && nv <= kFuseMax && qblk_off;
     if (!counted) hipLaunchKernelGGL(k_count, dim3(pg), dim3(256), hc, st, probe, npairs, nl, nprobe, 1, groups, cnt, idx->err);
     if (nv <= kFuseMax && qblk_off) {
-        hipLaunchKernelGGL(k_plan_fill, dim3(std::max(pg, 1u)), dim3(1024), 0, st, probe, npairs, nl, nprobe, groups, cnt,
+        hipLaunchKernelGGL(k_plan_fill, dim3(pg + 1), dim3(1024), 0, st, probe, npairs, nl, nprobe, groups, cnt,
                            idx->tile_off, bpc, bpc_near, qr, qoff, item_off, nch, head, qblk_off, itab, cursor, qlist,
                            bpc_near_min, workers, near_div, near0, counted ? cnt8 : nullptr);
         return hipGetLastError();
