@@ -214,6 +214,40 @@ __global__ __launch_bounds__(256) void k_centroid_gemm(const float *__restrict__
     }
 }
 
+// search.cpp:220-235's sequential sum of fl(q_j - c_j)^2 over one centroid row, 16
+// dims of loads per step where both rows are 16-B aligned
+__device__ __forceinline__ float exact_l2_row(const float *qr, const float *cr, int64_t d) {
+    float acc = 0.0f;
+    int64_t j = 0;
+    if ((((uintptr_t)cr | (uintptr_t)qr) & 15) == 0) {
+#pragma unroll 2
+        for (; j + 16 <= d; j += 16) {
+            float4 cv[4], qv[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                cv[e] = *(const float4 *)(cr + j + 4 * e);
+                qv[e] = *(const float4 *)(qr + j + 4 * e);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float df = qv[e].x - cv[e].x;
+                acc = acc + df * df;
+                df = qv[e].y - cv[e].y;
+                acc = acc + df * df;
+                df = qv[e].z - cv[e].z;
+                acc = acc + df * df;
+                df = qv[e].w - cv[e].w;
+                acc = acc + df * df;
+            }
+        }
+    }
+    for (; j < d; ++j) {
+        const float df = qr[j] - cr[j];
+        acc = acc + df * df;
+    }
+    return acc;
+}
+
 // -------------------------------------------------------- nearest, re-checked
 // One wave per query.  1) T = nprobe-th smallest approximate value; 2) every b
 // with A_b <= T + 2M (M = the query's error bound) gets its exact search.cpp
@@ -225,66 +259,111 @@ __global__ __launch_bounds__(256) void k_rank_select(const float *__restrict__ A
                                                      const float *__restrict__ q, int64_t nq,
                                                      const float *__restrict__ cent, int nb,
                                                      int64_t d, int nprobe, int32_t *out) {
+    __shared__ uint32_t s_cand[4][64];
     const int lane = threadIdx.x & 63;
     const int64_t qi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (qi >= nq) return;
     const float *arow = A + qi * nb;
-    u64 lst[R];
+    // T: any value with at least min(nprobe, nb) approximate values <= T works (the
+    // candidates are every b with A_b <= T + 2M, re-checked exactly; T >= the nprobe-th
+    // smallest keeps every member of the exact top-nprobe among them).  nb <= 1024: the
+    // row in registers (16 per lane, one round of loads) and T by bisection on the
+    // value range, stopped once few extra values pass -- the nprobe-th key by u64 bitonic
+    // merges of the 16 batches was ~3.7 k VALU instructions per query (BIGANN-100M,
+    // B = 1024: VALU-bound at ~60 us per 10 k queries).  Larger nb: those merges.
+    constexpr int NV = 16;
+    float lim;
+    if (nb <= 64 * NV) {
+        float av[NV];
 #pragma unroll
-    for (int r = 0; r < R; ++r) lst[r] = kEmptyKey;
-    for (int b0 = 0; b0 < nb; b0 += 64) {
-        int b = b0 + lane;
-        u64 key = b < nb ? make_key(arow[b], b) : kEmptyKey;
-        u64 thr = wave_list_at<R>(lst, nprobe - 1);
-        if (__ballot(key < thr)) wave_merge_batch<R>(lst, key);
+        for (int i = 0; i < NV; ++i) {
+            const int b = 64 * i + lane;
+            av[i] = b < nb ? arow[b] : __builtin_nanf("");
+        }
+        float lo = __builtin_inff(), hi = -__builtin_inff();
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            if (av[i] == av[i]) {
+                lo = fminf(lo, av[i]);
+                hi = fmaxf(hi, av[i]);
+            }
+        }
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            lo = fminf(lo, __shfl_xor(lo, m, 64));
+            hi = fmaxf(hi, __shfl_xor(hi, m, 64));
+        }
+        auto count_le = [&](float t) __attribute__((always_inline)) {
+            int c = 0;
+#pragma unroll
+            for (int i = 0; i < NV; ++i) c += av[i] <= t;  // (NaN: never)
+            return (int)wave_sum_u64((u64)c);
+        };
+        const int target = min(nprobe, nb);
+        // invariant: count(<= hi) >= target; a pass keeps the lower half while it holds
+        for (int it = 0; it < 24 && hi > lo; ++it) {
+            const float mid = lo + (hi - lo) * 0.5f;
+            if (!(mid > lo && mid < hi)) break;
+            const int c = count_le(mid);
+            if (c >= target) hi = mid; else lo = mid;
+            if (c >= target && c <= target + 16) break;  // (few extra candidates: good enough)
+        }
+        lim = hi < __builtin_inff() ? hi + 2.0f * err[qi] * 1.0001f : __builtin_inff();
+    } else {
+        u64 lst[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) lst[r] = kEmptyKey;
+        for (int b0 = 0; b0 < nb; b0 += 64) {
+            const int b = b0 + lane;
+            const u64 key = b < nb ? make_key(arow[b], b) : kEmptyKey;
+            const u64 thr = wave_list_at<R>(lst, nprobe - 1);
+            if (__ballot(key < thr)) wave_merge_batch<R>(lst, key);
+        }
+        const u64 tk = wave_list_at<R>(lst, nprobe - 1);
+        lim = tk == kEmptyKey ? __builtin_inff() : key_score(tk) + 2.0f * err[qi] * 1.0001f;
     }
-    const u64 tk = wave_list_at<R>(lst, nprobe - 1);
-    const float lim = tk == kEmptyKey ? __builtin_inff() : key_score(tk) + 2.0f * err[qi] * 1.0001f;
     const float *qr = q + qi * d;
     u64 fin[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) fin[r] = kEmptyKey;
-    for (int b0 = 0; b0 < nb; b0 += 64) {
-        int b = b0 + lane;
-        bool cand = b < nb && arow[b] <= lim;
-        if (!__ballot(cand)) continue;
+    // the candidates (A_b <= lim: ~nprobe of them) compacted into the wave's LDS list
+    // first, then re-checked 64 at a time, one per lane: walking the B / 64 batches
+    // with a re-check each (a couple of live lanes per batch at B = 1024) made every
+    // query a chain of 16 dependent d-long sums (BIGANN-100M: 0.32 ms per 10 k queries)
+    uint32_t *cl = s_cand[threadIdx.x >> 6];
+    int nc = 0;
+    auto flush = [&]() __attribute__((always_inline)) {
         u64 key = kEmptyKey;
-        if (cand) {
-            // search.cpp:220-235's sequential sum; 16 dims of loads in flight
-            // per step (a load per dim left each lane waiting on L2 latency:
-            // GIST1M d = 960, 170 us per call)
-            const float *cr = cent + (int64_t)b * d;
-            float acc = 0.0f;
-            int64_t j = 0;
-            if ((((uintptr_t)cr | (uintptr_t)qr) & 15) == 0) {
-                for (; j + 16 <= d; j += 16) {
-                    float4 cv[4], qv[4];
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        cv[e] = *(const float4 *)(cr + j + 4 * e);
-                        qv[e] = *(const float4 *)(qr + j + 4 * e);
-                    }
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        float df = qv[e].x - cv[e].x;
-                        acc = acc + df * df;
-                        df = qv[e].y - cv[e].y;
-                        acc = acc + df * df;
-                        df = qv[e].z - cv[e].z;
-                        acc = acc + df * df;
-                        df = qv[e].w - cv[e].w;
-                        acc = acc + df * df;
-                    }
-                }
-            }
-            for (; j < d; ++j) {
-                float df = qr[j] - cr[j];
-                acc = acc + df * df;
-            }
-            key = make_key(sqrt_rn_f32(acc), b);
+        if (lane < nc) {
+            const int b = (int)cl[lane];
+            key = make_key(sqrt_rn_f32(exact_l2_row(qr, cent + (int64_t)b * d, d)), b);
         }
         wave_merge_batch<R>(fin, key);
+        nc = 0;
+        __builtin_amdgcn_wave_barrier();
+    };
+    for (int c0 = 0; c0 < nb; c0 += 64 * NV) {
+        float av[NV];
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            const int b = c0 + 64 * i + lane;
+            av[i] = b < nb ? arow[b] : 0.0f;
+        }
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            const int b = c0 + 64 * i + lane;
+            if (c0 + 64 * i >= nb) break;
+            const bool cand = b < nb && av[i] <= lim;
+            const u64 m = __ballot(cand);
+            const int n = popc64(m);
+            if (!n) continue;
+            if (nc + n > 64) flush();
+            if (cand) cl[nc + mbcnt64(m)] = (uint32_t)b;
+            nc += n;
+            __builtin_amdgcn_wave_barrier();
+        }
     }
+    if (nc) flush();
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         int e = r * 64 + lane;

@@ -1703,6 +1703,9 @@ __global__ __launch_bounds__(256) void k_seed_t(const float *Q, const int32_t *p
 // values as pair_record's (double sums in another order: fl() of the same exact
 // sum up to the double rounding, which the screen's error model absorbs -- the
 // results never depend on it); the seed bound is seed_bound's, bit for bit.
+// (110 VGPRs, 4 waves per SIMD; capped at 78 for 6 -- 2 of the 16-B record loads in flight
+// instead of 4 -- it ran 51 -> 100 us per 10 k queries: the waves' load chains, not
+// their number, set its time)
 template <int NT, int G>
 __global__ __launch_bounds__(256) void k_seed_p(const float *Q, const int32_t *probe, int nprobe, int n_lists,
                                                 const int32_t *tile_off, const int32_t *ids, const float *X,
@@ -1936,7 +1939,10 @@ __device__ __forceinline__ void merge_batch_if(u64 (&lst)[R], u64 batch) {
     if (__ballot(batch < thr)) wave_merge_batch<R>(lst, batch);
 }
 
-template <int METRIC, int R>
+// MODE 0: the common call -- no per-partition lists, no k_rescan queue (rmode 0) -- compiled
+// without those paths: 128 VGPRs and no spills (22 spilled with them; SIFT1M mixture merge
+// 73 -> 64 us); MODE 1: every call
+template <int METRIC, int R, int MODE>
 __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 VGPRs: 4 waves per SIMD)
     __shared__ uint32_t s_pend[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1964,9 +1970,11 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
     uint32_t *pend = s_pend[w];
     int64_t ncand = 0;
     unsigned long long n_rechecked = 0, n_rescans = 0;
-    const bool fall = a.rmode == 2 && a.rfall[q] != 0u;
+    const int rmode = MODE ? a.rmode : 0;
+    const bool per_partition = MODE ? a.per_partition != 0 : false;
+    const bool fall = rmode == 2 && a.rfall[q] != 0u;
     // lists + spills hold every key within reach: no list is re-scanned
-    const bool sok = a.spill && !a.per_partition && a.scnt[q] <= (unsigned)a.scap;
+    const bool sok = a.spill && !per_partition && a.scnt[q] <= (unsigned)a.scap;
     // a list of the query whose last slot is within its limit: only then can an
     // evicted key be needed (evicted keys lie above their list's final last key)
     bool any_over = false;
@@ -1979,7 +1987,7 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
     // re-checks come in: a candidate of exact score <= the final k-th has
     // s~ <= s_lim(final k-th, E) <= s_lim(Trun, E) (not with per-partition lists)
     float Trun = __builtin_inff();
-    const bool tighten = !a.per_partition;
+    const bool tighten = !per_partition;
     auto reset = [&]() {
 #pragma unroll
         for (int r = 0; r < R; ++r) lst[r] = kEmptyKey;
@@ -2066,7 +2074,7 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
             }
             // (with spill lists a full list is walked like any other; its evicted keys
             // are in the spill list, read below only if some list of the query is full)
-            bool active = p >= 0 && (!over || sok) && a.rmode != 1;
+            bool active = p >= 0 && (!over || sok) && rmode != 1;
             // four keys per round (two 16-B loads; K2 % 4 == 0, lists 32-B aligned):
             // the walk is one dependent load per round
             float Tl = fminf(T, Trun);
@@ -2096,7 +2104,7 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
             u64 ov = __ballot(over);
             any_over = any_over || ov != 0;
             if (sok) continue;  // (no re-scans)
-            if (a.rmode == 1) {  // queue them for k_rescan
+            if (rmode == 1) {  // queue them for k_rescan
                 if (ov) {
                     unsigned base = 0;
                     if (lane == 0) base = atomicAdd(a.rq_n, (unsigned)popc64(ov));
@@ -2112,7 +2120,7 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
                 continue;
             }
             n_rescans += popc64(ov);
-            if (a.rmode == 2 && !fall) continue;  // k_rescan has them
+            if (rmode == 2 && !fall) continue;  // k_rescan has them
             while (ov) {
                 const int ln = __builtin_ctzll(ov);
                 ov &= ov - 1;
@@ -2122,7 +2130,7 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
         }
     };
 
-    if (a.per_partition) {
+    if (per_partition) {
         for (int s = 0; s < a.nprobe; ++s) {
             const int p = prow[s];
             reset();
@@ -2170,7 +2178,7 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
             ncand = (int64_t)wave_sum_u64((u64)nc);
         }
         take_lists(0, a.nprobe, T);
-        if (a.rmode == 1) return;
+        if (rmode == 1) return;
         if (sok && any_over) {  // the spilled keys within their lists' limits
             const int ns = (int)a.scnt[q];
             const uint4 *sp = a.spill + q * (int64_t)a.scap;
@@ -2187,7 +2195,7 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
             }
         }
         flush_pending();
-        if (a.rmode == 2 && !fall) {  // k_rescan's exact survivors (all within T)
+        if (rmode == 2 && !fall) {  // k_rescan's exact survivors (all within T)
             const int nr = (int)min(a.rcnt[q], (unsigned)a.rcap);
             const u64 *rb = a.rbuf + q * (int64_t)a.rcap;
             for (int i0 = 0; i0 < nr; i0 += 64) merge_batch_if<R>(lst, i0 + lane < nr ? rb[i0 + lane] : kEmptyKey);
@@ -2659,11 +2667,20 @@ static hipError_t launch_screen_rl(const ScreenArgs &a, const SPlan &pl, hipStre
 template <int M>
 static void launch_smerge(int R, const SMergeArgs &m, hipStream_t st) {
     const dim3 g((unsigned)((m.nq + 3) / 4)), b(256);
+    if (!m.per_partition && m.rmode == 0) {
+        switch (R) {
+            case 1: hipLaunchKernelGGL((k_smerge<M, 1, 0>), g, b, 0, st, m); break;
+            case 2: hipLaunchKernelGGL((k_smerge<M, 2, 0>), g, b, 0, st, m); break;
+            case 4: hipLaunchKernelGGL((k_smerge<M, 4, 0>), g, b, 0, st, m); break;
+            default: hipLaunchKernelGGL((k_smerge<M, 8, 0>), g, b, 0, st, m); break;
+        }
+        return;
+    }
     switch (R) {
-        case 1: hipLaunchKernelGGL((k_smerge<M, 1>), g, b, 0, st, m); break;
-        case 2: hipLaunchKernelGGL((k_smerge<M, 2>), g, b, 0, st, m); break;
-        case 4: hipLaunchKernelGGL((k_smerge<M, 4>), g, b, 0, st, m); break;
-        default: hipLaunchKernelGGL((k_smerge<M, 8>), g, b, 0, st, m); break;
+        case 1: hipLaunchKernelGGL((k_smerge<M, 1, 1>), g, b, 0, st, m); break;
+        case 2: hipLaunchKernelGGL((k_smerge<M, 2, 1>), g, b, 0, st, m); break;
+        case 4: hipLaunchKernelGGL((k_smerge<M, 4, 1>), g, b, 0, st, m); break;
+        default: hipLaunchKernelGGL((k_smerge<M, 8, 1>), g, b, 0, st, m); break;
     }
 }
 
@@ -2821,6 +2838,10 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
         case 2: LIRA_SEED_P(NTV, 2); break;                                                                     \
         default: LIRA_SEED_P(NTV, 1); break;                                                                    \
     }
+            // (a grouped form -- each slot-0 list's first tiles staged in LDS once per
+            // workgroup for the queries that probe it first, then the records alone -- measured
+            // 50 + 21 us against 51: the workgroups' probe-column scans and the records' own
+            // latency chain cost more than the tile reads it saved)
             if (nt_f == 4) {
                 LIRA_SEED_PG(4)
             } else if (nt_f == 1) {
