@@ -172,7 +172,7 @@ int lira_index_memory(const lira_index *idx, int64_t *bytes);
  *                        per-query seed on, not PER_PARTITION): query rows' hi parts in LDS, each
  *                        wave streaming its own candidate tiles into registers; 0: k_screen_m
  *   LIRA_OPT_NEAR_FIRST  (k_screen_r) blocks of 256 candidates in the first chunk of every query
- *                        block's nearest partition: -1 (default) 2; 0: chunks of one size.  Those
+ *                        block's nearest partition: -1 (default) 4; 0: chunks of one size.  Those
  *                        small first chunks are queued first; the query block's later chunks wait
  *                        for its first one, so they start from the bounds it published instead of
  *                        the 128-row seed's.  Results never depend on it.

@@ -53,7 +53,7 @@ struct lira_opts {
     int xhi = -1;
     int order = 1;
     int rscreen = 1;
-    int near_first = -1;  // LIRA_OPT_NEAR_FIRST (-1: the default, 2 blocks)
+    int near_first = -1;  // LIRA_OPT_NEAR_FIRST (-1: the default, 4 blocks)
     int rescan = -1;      // LIRA_OPT_RESCAN (-1: auto)
     int spill = -1;       // LIRA_OPT_SPILL (-1: 256 records per query)
     int seed_tiles = 0;   // LIRA_OPT_SEED_TILES (0: auto)

@@ -452,21 +452,30 @@ __global__ __launch_bounds__(256) void k_rank_select64(const float *__restrict__
 __global__ __launch_bounds__(512) void k_rank_exact64(const float *__restrict__ q, int64_t nq,
                                                       const float *__restrict__ cent, int nb, int64_t d,
                                                       int nprobe, int qpw, int32_t *out) {
-    extern __shared__ float4 Cs[];  // [d/4][64]
+    extern __shared__ float4 Cs[];  // [d/4][64], then the workgroup's 8 qpw query rows [8 qpw][d/4]
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nd4 = (int)(d >> 2);
-    // coalesced row reads (consecutive threads: consecutive float4 of one row)
+    float4 *Qs = Cs + 64 * nd4;
+    const int64_t qb0 = (int64_t)blockIdx.x * (8 * qpw);
+    // coalesced row reads (consecutive threads: consecutive float4 of one row); the
+    // workgroup's query rows come in the same round, so a wave's chain per query is
+    // LDS reads only (its rows by wave-uniform global loads, four rounds of eight 16-B
+    // loads per query, were most of the kernel's time: SIFT1M 22 us per 10 k queries)
     for (int i = tid; i < 64 * nd4; i += 512) {
         const int b = i / nd4, j4 = i - b * nd4;
         Cs[j4 * 64 + b] = b < nb ? *(const float4 *)(cent + (int64_t)b * d + 4 * j4) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    for (int i = tid; i < 8 * qpw * nd4; i += 512) {
+        const int64_t qi = qb0 + i / nd4;
+        Qs[i] = qi < nq ? *(const float4 *)(q + qi * d + 4 * (i % nd4)) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     __syncthreads();
-    const int64_t q0 = (int64_t)blockIdx.x * (8 * qpw) + w * qpw;
+    const int64_t q0 = qb0 + w * qpw;
     for (int r = 0; r < qpw; ++r) {
         const int64_t qi = q0 + r;
         if (qi >= nq) break;
-        const float4 *qr = (const float4 *)(q + qi * d);
+        const float4 *qr = Qs + (int64_t)(w * qpw + r) * nd4;
         float acc = 0.0f;
 #pragma unroll 8
         for (int j4 = 0; j4 < nd4; ++j4) {
@@ -776,7 +785,10 @@ int lira_rank_nearest(const float *q, int64_t nq, const float *centroids, int64_
     if (rank_exact64_ok(q, centroids, n_centroids, d)) {  // (no workspace needed)
         const int qpw = nq >= 8192 ? 2 : 1;
         const unsigned g = (unsigned)((nq + 8 * qpw - 1) / (8 * qpw));
-        hipLaunchKernelGGL(k_rank_exact64, dim3(g), dim3(512), (size_t)d * 64 * 4, (hipStream_t)stream, q, nq,
+        static std::atomic<uint64_t> attr{0};  // (d = 256, qpw 4: 64 + 32 KB)
+        LIRA_HIP_TRY(set_smem_attr_once(attr, (const void *)k_rank_exact64, 128 * 1024));
+        hipLaunchKernelGGL(k_rank_exact64, dim3(g), dim3(512), (size_t)d * 64 * 4 + (size_t)8 * qpw * d * 4,
+                           (hipStream_t)stream, q, nq,
                            centroids, (int)n_centroids, d, (int)nprobe, qpw, out_probe);
         LIRA_HIP_TRY(hipGetLastError());
         return LIRA_OK;
