@@ -1583,8 +1583,9 @@ __device__ __forceinline__ float seed_bound(const float *Q, const int32_t *probe
                 acc[2 * t] = acc2[t].x;
                 acc[2 * t + 1] = acc2[t].y;
             }
-            if (NT & 1) {  // (an odd tile: scalar)
-#pragma unroll 16
+            if (NT & 1) {  // (an odd tile: scalar; 64 loads in flight -- GIST1M's one seed tile
+                           // of 960 dims ran as 60 dependent rounds of 16 at unroll 16: 39 -> 31 us)
+#pragma unroll 64
                 for (int jj = 0; jj < 64; ++jj) {
                     const float qj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qv), jj));
                     const float xv = xt[NT - 1][(j0 + jj) * kTile];
