@@ -1693,49 +1693,22 @@ __global__ __launch_bounds__(256) void k_seed_t(const float *Q, const int32_t *p
     }
 }
 
-// k_seed_t<L2, NT, true> with all of the query's pair records in ONE round
-// (k_seed_p): G = 64 / nprobe_pow2 lanes per (query, slot) pair, each lane a
-// contiguous run of D dims (16-B loads of q and the pivot, 8-B stores of 4 bf16
-// of QH), so the nprobe pairs' loads are in flight together and the filter runs
-// in every pair's lanes at once.  k_seed_t walked the pairs 4 at a time (16 lanes
-// each, dims strided by 16): at nprobe 8 two rounds of probe -> pivot -> reduce
-// -> filter chains after the seed's own, about 35 of its 55 us per 10 k SIFT1M
-// queries (seed tiles 1 / 2 / 4: 46 / 56 / 101 us).  The records are the same
-// values as pair_record's (double sums in another order: fl() of the same exact
-// sum up to the double rounding, which the screen's error model absorbs -- the
-// results never depend on it); the seed bound is seed_bound's, bit for bit.
-// (110 VGPRs, 4 waves per SIMD; capped at 78 for 6 -- 2 of the 16-B record loads in flight
-// instead of 4 -- it ran 51 -> 100 us per 10 k queries: the waves' load chains, not
-// their number, set its time)
-template <int NT, int G>
-__global__ __launch_bounds__(256) void k_seed_p(const float *Q, const int32_t *probe, int nprobe, int n_lists,
-                                                const int32_t *tile_off, const int32_t *ids, const float *X,
-                                                int64_t d, int64_t dpad, int64_t nq, int k, uint32_t *qbound,
-                                                SeedPairs sp) {
-    static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "lanes per pair");
-    const int lane = threadIdx.x & 63;
-    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (q >= nq) return;
-    const int slot = lane / G, sub = lane % G;
-    const bool valid = slot < nprobe;
-    const int64_t pair = q * nprobe + (valid ? slot : 0);
-    const int praw = valid ? probe[pair] : -1;
-    const int p = praw < n_lists ? praw : -1;
-    const float *qrow = Q + q * d;
-    // this lane's dims [j0, j1): D = ceil(d / G) rounded up to 4
+// One (query, slot) pair's record sums over G lanes, lane sub owning the contiguous
+// dims [sub D, sub D + D) (D = ceil(d / G) rounded up to 4): s = sum fl(q - c)^2 (L2
+// centred) or q^2, e = the hi residuals', t = sum (q - c)^2 (L2) or q.c (IP, centred
+// == 2), all in double; the QH row (hi(q') in bf16, zero past d) written 4 at a time.
+// Every lane returns the pair's totals (pair_record's values up to the double sums'
+// order).  p < 0: zeros, nothing written.
+template <int G>
+__device__ __forceinline__ void pair_sums_run(const float *qrow, const float *pv, int64_t d, int64_t dpad, int64_t pair,
+                                              int sub, int p, uint16_t *QH, int centred, double &s, double &t,
+                                              double &e) {
     const int64_t D = ((d + G - 1) / G + 3) & ~(int64_t)3;
     const int64_t j0 = sub * D, j1 = min<int64_t>(d, j0 + D);
-    const bool est_on = sp.work && (q & 7) == 0 && p >= 0;
-    // (estimate) the 16 sample tiles of the list, 16 / G per lane
-    float2 ts[16 / G];
-#pragma unroll
-    for (int i = 0; i < 16 / G; ++i) ts[i] = est_on ? sp.lsamp[p * 16 + sub + G * i] : make_float2(0.0f, 0.0f);
-    const int lsz = est_on ? sp.list_size[p] : 0;
-    double s = 0.0, t = 0.0, e = 0.0;
+    s = t = e = 0.0;
     if (p >= 0) {
-        const float *pv = sp.pivot + (int64_t)p * d;
-        uint16_t *qh = sp.QH ? sp.QH + pair * dpad : nullptr;
-        const bool cen = sp.centred == 1;
+        uint16_t *qh = QH ? QH + pair * dpad : nullptr;
+        const bool cen = centred == 1, ipm = centred == 2;
         auto one = [&](float x, float cv, uint32_t &hb) {
             const float sv = cen ? x - cv : x;
             hb = bf16_rne_sat(sv);
@@ -1743,8 +1716,12 @@ __global__ __launch_bounds__(256) void k_seed_p(const float *Q, const int32_t *p
             s = __builtin_fma(xc, xc, s);
             const double rr = (double)(sv - __uint_as_float(hb << 16));
             e = __builtin_fma(rr, rr, e);
-            const double df = (double)x - (double)cv;
-            t = __builtin_fma(df, df, t);
+            if (ipm) {
+                t = __builtin_fma((double)x, (double)cv, t);
+            } else {
+                const double df = (double)x - (double)cv;
+                t = __builtin_fma(df, df, t);
+            }
         };
         if ((d & 3) == 0) {  // 16-B loads (rows 16-B aligned), 4 bf16 per 8-B store
 #pragma unroll 4
@@ -1775,6 +1752,46 @@ __global__ __launch_bounds__(256) void k_seed_p(const float *Q, const int32_t *p
         t += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, t), m));
         e += __builtin_bit_cast(double, shfl_xor64(__builtin_bit_cast(u64, e), m));
     }
+}
+
+// k_seed_t<L2, NT, true> with all of the query's pair records in ONE round
+// (k_seed_p): G = 64 / nprobe_pow2 lanes per (query, slot) pair, each lane a
+// contiguous run of D dims (16-B loads of q and the pivot, 8-B stores of 4 bf16
+// of QH), so the nprobe pairs' loads are in flight together and the filter runs
+// in every pair's lanes at once.  k_seed_t walked the pairs 4 at a time (16 lanes
+// each, dims strided by 16): at nprobe 8 two rounds of probe -> pivot -> reduce
+// -> filter chains after the seed's own, about 35 of its 55 us per 10 k SIFT1M
+// queries (seed tiles 1 / 2 / 4: 46 / 56 / 101 us).  The records are the same
+// values as pair_record's (double sums in another order: fl() of the same exact
+// sum up to the double rounding, which the screen's error model absorbs -- the
+// results never depend on it); the seed bound is seed_bound's, bit for bit.
+// (110 VGPRs, 4 waves per SIMD; capped at 78 for 6 -- 2 of the 16-B record loads in flight
+// instead of 4 -- it ran 51 -> 100 us per 10 k queries: the waves' load chains, not
+// their number, set its time)
+template <int NT, int G>
+__global__ __launch_bounds__(256) void k_seed_p(const float *Q, const int32_t *probe, int nprobe, int n_lists,
+                                                const int32_t *tile_off, const int32_t *ids, const float *X,
+                                                int64_t d, int64_t dpad, int64_t nq, int k, uint32_t *qbound,
+                                                SeedPairs sp) {
+    static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "lanes per pair");
+    const int lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    const int slot = lane / G, sub = lane % G;
+    const bool valid = slot < nprobe;
+    const int64_t pair = q * nprobe + (valid ? slot : 0);
+    const int praw = valid ? probe[pair] : -1;
+    const int p = praw < n_lists ? praw : -1;
+    const float *qrow = Q + q * d;
+    const bool est_on = sp.work && (q & 7) == 0 && p >= 0;
+    // (estimate) the 16 sample tiles of the list, 16 / G per lane
+    float2 ts[16 / G];
+#pragma unroll
+    for (int i = 0; i < 16 / G; ++i) ts[i] = est_on ? sp.lsamp[p * 16 + sub + G * i] : make_float2(0.0f, 0.0f);
+    const int lsz = est_on ? sp.list_size[p] : 0;
+    double s, t, e;
+    pair_sums_run<G>(qrow, p >= 0 ? sp.pivot + (int64_t)p * d : nullptr, d, dpad, pair, sub, p, sp.QH, sp.centred, s, t,
+                     e);
     // the seed bound (seed_bound: the first NT tiles of slot 0's list)
     const float B = seed_bound<LIRA_METRIC_L2, NT>(Q, probe, nprobe, n_lists, tile_off, ids, X, d, dpad, q, k);
     const uint32_t qb = B < __builtin_inff() ? f2ord(B) : ~0u;
@@ -2275,13 +2292,23 @@ __global__ __launch_bounds__(256) void k_pairs(const float *Q, int64_t d, const 
                                                int nprobe, int n_lists, const float *pivot, int centred,
                                                const float2 *lstat, const uint32_t *qbound, int32_t *probe_live,
                                                float4 *QN, float *QE, float *pqn, uint16_t *QH, int64_t dpad,
-                                               const float *rmx) {
+                                               const float *rmx, int32_t *cnt8, int nv, int groups, int32_t *err) {
     const int64_t pair = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
     const bool valid = pair < npairs;
     const int praw = valid ? probe[pair] : -1;
     const uint32_t qb = valid && lstat && qbound ? qbound[pair / nprobe] : ~0u;
     pair_record<G>(Q, d, pair, valid, praw, nprobe, n_lists, pivot, centred, lstat && qbound ? lstat : nullptr, qb,
                    probe_live, QN, QE, pqn, QH, dpad, nullptr, nullptr, rmx);
+    // (cnt8) k_count's work: the live pair counted in its XCD's replica (as k_seed_p)
+    if (cnt8 && valid && (threadIdx.x & (G - 1)) == 0) {
+        if (praw >= n_lists) {
+            atomicOr(err, 1);
+        } else {
+            const int live = probe_live[pair];  // (this lane's own store above)
+            if (live >= 0)
+                atomicAdd(cnt8 + xcd_id() * nv + (groups == 2 && (int)(pair % nprobe) >= 1 ? n_lists + live : live), 1);
+        }
+    }
 }
 
 // (stats on) what the plan's partition filter removed: pairs whose probe slot
@@ -2306,16 +2333,19 @@ __global__ __launch_bounds__(256) void k_prune_stats(const int32_t *probe, const
 static hipError_t launch_pairs(const float *Q, int64_t d, const int32_t *probe, int64_t npairs, int nprobe,
                                int n_lists, const float *pivot, int centred, const float2 *lstat,
                                const uint32_t *qbound, int32_t *probe_live, float4 *QN, float *QE, float *pqn,
-                               uint16_t *QH, int64_t dpad, const float *rmx, hipStream_t st) {
+                               uint16_t *QH, int64_t dpad, const float *rmx, hipStream_t st,
+                               int32_t *cnt8 = nullptr, int nv = 0, int groups = 1, int32_t *err = nullptr) {
     const bool wide = d > 256;
     const unsigned g = (unsigned)((npairs * (wide ? 64 : 16) + 255) / 256);
     if (g == 0) return hipSuccess;
+    // (one wave per query, G = 64 / nprobe lanes per pair as in k_seed_p, measured the same:
+    // DEEP10M 80 vs 77 us per 10 k queries)
     if (wide)
         hipLaunchKernelGGL((k_pairs<64>), dim3(g), dim3(256), 0, st, Q, d, probe, npairs, nprobe, n_lists, pivot,
-                           centred, lstat, qbound, probe_live, QN, QE, pqn, QH, dpad, rmx);
+                           centred, lstat, qbound, probe_live, QN, QE, pqn, QH, dpad, rmx, cnt8, nv, groups, err);
     else
         hipLaunchKernelGGL((k_pairs<16>), dim3(g), dim3(256), 0, st, Q, d, probe, npairs, nprobe, n_lists, pivot,
-                           centred, lstat, qbound, probe_live, QN, QE, pqn, QH, dpad, rmx);
+                           centred, lstat, qbound, probe_live, QN, QE, pqn, QH, dpad, rmx, cnt8, nv, groups, err);
     return hipGetLastError();
 }
 
@@ -2899,11 +2929,15 @@ int screen_topk(lira_index *idx, const float *q, int64_t nq, const int32_t *prob
                                (int)k, qbound);
         LIRA_HIP_TRY(hipGetLastError());
     }
-    if (plive && (!fused || seed_split))
+    if (plive && (!fused || seed_split)) {
+        // (k_pairs writes every pair's live entry: it counts them too, per XCD -- no k_count)
         LIRA_HIP_TRY(launch_pairs(q, idx->d, probe, npairs, (int)nprobe, (int)idx->n_lists, idx->pivot,
                                   idx->ipc ? 2 : centred ? 1 : 0, filter ? idx->lstat : nullptr, filter ? qbound : nullptr,
                                   plive, pl.pp ? QN : nullptr, pl.pp ? QE : nullptr, pl.pp ? pqn : nullptr, QH, idx->dpad,
-                                  idx->rmax, st));
+                                  idx->rmax, st, (int32_t *)(w + pl.off_cnt8), groups * (int)idx->n_lists, groups,
+                                  idx->err));
+        seed_counted = true;
+    }
     const int32_t *pprobe = plive ? plive : probe;  // the pairs that become work
     const int nvirt = groups * (int)idx->n_lists;
     LIRA_HIP_TRY(launch_plan(idx, pprobe, npairs, (int)nprobe, pl.bpc, groups == 2 ? pl.bpc_near : pl.bpc, pl.qr, groups, cnt, cursor, qoff, item_off,
