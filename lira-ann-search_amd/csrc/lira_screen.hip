@@ -756,17 +756,24 @@ struct SMergeArgs {
 };
 
 // exact score of the candidate at storage row pos (search.cpp:253-269 order)
-// (Xr: the row-major copy, so one lane reads its candidate contiguously)
+// (Xr: the row-major copy, so one lane reads its candidate contiguously).  q is
+// wave-uniform (the merge's query row): read through the constant address space
+// so its pieces come by scalar loads into SGPRs -- the 8 row pieces in flight then
+// hold the VGPRs alone (k_smerge 128 -> 92 VGPRs, 4 -> 5 waves per SIMD; SIFT1M
+// mixture merge 64 -> 49 us)
 template <int METRIC>
 __device__ __forceinline__ float exact_score(const float *q, const float *Xr, int64_t d, int pos) {
     const float *xp = Xr + (int64_t)pos * d;
     float acc = 0.0f;
     if ((d & 3) == 0 && ((uintptr_t)q & 15) == 0) {  // 16-B loads of the row, 8 in flight; the same sequential sum
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        typedef const __attribute__((address_space(4))) f4v cf4;
         const float4 *x4 = (const float4 *)xp;
-        const float4 *q4 = (const float4 *)q;
+        cf4 *q4 = (cf4 *)q;
 #pragma unroll 8
         for (int64_t j = 0; j < d / 4; ++j) {
-            const float4 xv = x4[j], qv = q4[j];
+            const float4 xv = x4[j];
+            const f4v qv = q4[j];
             if (METRIC == LIRA_METRIC_L2) {
                 float df = qv.x - xv.x; acc = acc + df * df;
                 df = qv.y - xv.y; acc = acc + df * df;
@@ -1958,12 +1965,14 @@ __device__ __forceinline__ void merge_batch_if(u64 (&lst)[R], u64 batch) {
 }
 
 // MODE 0: the common call -- no per-partition lists, no k_rescan queue (rmode 0) -- compiled
-// without those paths: 128 VGPRs and no spills (22 spilled with them; SIFT1M mixture merge
+// without those paths: no VGPR spills (22 spilled with them; SIFT1M mixture merge
 // 73 -> 64 us); MODE 1: every call
 template <int METRIC, int R, int MODE>
-__global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 VGPRs: 4 waves per SIMD)
+__global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 VGPRs; 92 at MODE 0, R 1: 5 waves per SIMD)
     __shared__ uint32_t s_pend[4][64];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // (w through readfirstlane: the query index, its row and every address derived
+    // from them are wave-uniform to the compiler -- scalar loads of the row in exact_score)
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t q = (int64_t)blockIdx.x * 4 + w;
     if (q >= a.nq) return;
     const int k = a.k, K2 = a.K2;

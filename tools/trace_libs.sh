@@ -10,7 +10,7 @@ for v in "$@"; do
   mkdir -p $out
   LIRA_HIP_LIB=$lib timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $out -o run --output-format csv -- \
       python3 bench.py --config $cfg --data $data --steps 10 --warmup 2 --no-cpu-baseline --no-exact --no-pipeline \
-      --contrast none --recall-sample 4 $BENCH_ARGS > $out/log.txt 2>&1
-  echo "== $v $cfg $data $BENCH_ARGS"
+      --contrast none --recall-sample 4 ${BENCH_ARGS:-} > $out/log.txt 2>&1
+  echo "== $v $cfg $data ${BENCH_ARGS:-}"
   python3 tools/kstats.py $out
 done
