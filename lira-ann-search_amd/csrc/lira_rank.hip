@@ -220,13 +220,19 @@ __device__ __forceinline__ float exact_l2_row(const float *qr, const float *cr, 
     float acc = 0.0f;
     int64_t j = 0;
     if ((((uintptr_t)cr | (uintptr_t)qr) & 15) == 0) {
+        // qr is wave-uniform (k_rank_select's query row): constant-address-space reads,
+        // so its pieces come by scalar loads and the VGPRs hold the centroid pieces only
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        typedef const __attribute__((address_space(4))) f4v cf4;
+        cf4 *q4 = (cf4 *)qr;
 #pragma unroll 2
         for (; j + 16 <= d; j += 16) {
-            float4 cv[4], qv[4];
+            float4 cv[4];
+            f4v qv[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 cv[e] = *(const float4 *)(cr + j + 4 * e);
-                qv[e] = *(const float4 *)(qr + j + 4 * e);
+                qv[e] = q4[(j >> 2) + e];
             }
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -261,7 +267,7 @@ __global__ __launch_bounds__(256) void k_rank_select(const float *__restrict__ A
                                                      int64_t d, int nprobe, int32_t *out) {
     __shared__ uint32_t s_cand[4][64];
     const int lane = threadIdx.x & 63;
-    const int64_t qi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t qi = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (qi >= nq) return;
     const float *arow = A + qi * nb;
     // T: any value with at least min(nprobe, nb) approximate values <= T works (the
