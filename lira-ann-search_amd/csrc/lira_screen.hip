@@ -761,7 +761,7 @@ struct SMergeArgs {
 // so its pieces come by scalar loads into SGPRs -- the 8 row pieces in flight then
 // hold the VGPRs alone (k_smerge 128 -> 92 VGPRs, 4 -> 5 waves per SIMD; SIFT1M
 // mixture merge 64 -> 49 us)
-template <int METRIC>
+template <int METRIC, int U = 8>
 __device__ __forceinline__ float exact_score(const float *q, const float *Xr, int64_t d, int pos) {
     const float *xp = Xr + (int64_t)pos * d;
     float acc = 0.0f;
@@ -770,7 +770,7 @@ __device__ __forceinline__ float exact_score(const float *q, const float *Xr, in
         typedef const __attribute__((address_space(4))) f4v cf4;
         const float4 *x4 = (const float4 *)xp;
         cf4 *q4 = (cf4 *)q;
-#pragma unroll 8
+#pragma unroll U
         for (int64_t j = 0; j < d / 4; ++j) {
             const float4 xv = x4[j];
             const f4v qv = q4[j];
@@ -1966,7 +1966,10 @@ __device__ __forceinline__ void merge_batch_if(u64 (&lst)[R], u64 batch) {
 
 // MODE 0: the common call -- no per-partition lists, no k_rescan queue (rmode 0) -- compiled
 // without those paths: no VGPR spills (22 spilled with them; SIFT1M mixture merge
-// 73 -> 64 us); MODE 1: every call
+// 73 -> 64 us); MODE 1: every call; MODE 2: MODE 0 for long rows (d >= 512): the
+// exact re-check with 16 row pieces in flight instead of 8 (103 VGPRs, 4 waves per
+// SIMD; GIST1M 1 k queries merge 47 -> 44 us mixture, 189 -> 174 latent; SIFT1M
+// 1 250 queries 18.6 -> 19.3 us, so not for short rows)
 template <int METRIC, int R, int MODE>
 __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 VGPRs; 92 at MODE 0, R 1: 5 waves per SIMD)
     __shared__ uint32_t s_pend[4][64];
@@ -1997,8 +2000,9 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
     uint32_t *pend = s_pend[w];
     int64_t ncand = 0;
     unsigned long long n_rechecked = 0, n_rescans = 0;
-    const int rmode = MODE ? a.rmode : 0;
-    const bool per_partition = MODE ? a.per_partition != 0 : false;
+    const int rmode = MODE == 1 ? a.rmode : 0;
+    const bool per_partition = MODE == 1 ? a.per_partition != 0 : false;
+    constexpr int U = MODE == 2 ? 16 : 8;
     const bool fall = rmode == 2 && a.rfall[q] != 0u;
     // lists + spills hold every key within reach: no list is re-scanned
     const bool sok = a.spill && !per_partition && a.scnt[q] <= (unsigned)a.scap;
@@ -2024,7 +2028,7 @@ __global__ __launch_bounds__(256, 4) void k_smerge(SMergeArgs a) {  // (<= 128 V
         u64 key = kEmptyKey;
         if (lane < pc) {
             const int pos = (int)pend[lane];
-            key = make_key(exact_score<METRIC>(qrow, a.Xr, a.d, pos), a.ids[pos]);
+            key = make_key(exact_score<METRIC, U>(qrow, a.Xr, a.d, pos), a.ids[pos]);
         }
         n_rechecked += pc;
         merge_batch_if<R>(lst, key);
@@ -2709,6 +2713,15 @@ static hipError_t launch_screen_rl(const ScreenArgs &a, const SPlan &pl, hipStre
 template <int M>
 static void launch_smerge(int R, const SMergeArgs &m, hipStream_t st) {
     const dim3 g((unsigned)((m.nq + 3) / 4)), b(256);
+    if (!m.per_partition && m.rmode == 0 && m.d >= 512) {
+        switch (R) {
+            case 1: hipLaunchKernelGGL((k_smerge<M, 1, 2>), g, b, 0, st, m); break;
+            case 2: hipLaunchKernelGGL((k_smerge<M, 2, 2>), g, b, 0, st, m); break;
+            case 4: hipLaunchKernelGGL((k_smerge<M, 4, 2>), g, b, 0, st, m); break;
+            default: hipLaunchKernelGGL((k_smerge<M, 8, 2>), g, b, 0, st, m); break;
+        }
+        return;
+    }
     if (!m.per_partition && m.rmode == 0) {
         switch (R) {
             case 1: hipLaunchKernelGGL((k_smerge<M, 1, 0>), g, b, 0, st, m); break;
